@@ -1,0 +1,316 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident MPI derived-datatype pack+unpack on MI355X.
+
+Metric (BASELINE.json): "pack+unpack GiB/s/GPU (device-resident), 256^3 double
+3D-vector; %HBM peak".  Default workload = BASELINE config 2: the 6-face halo of a
+256^3 double grid (x faces vector(65536,1,256), y faces vector(256,256,65536), z faces
+contiguous(65536)), the six faces of one field expressed as ONE committed struct type
+resized to the field extent, F = 16 fields per GPU (count = 16, a 2 GiB working set,
+well past the 256 MiB Infinity Cache).  One step = one pack (ddt_convertor_pack, whole
+message, device iovec) + one unpack of the same message.
+
+  value      = whole-job 2*S*N_gpus / (t_pack + t_unpack)        [GiB/s]
+  roofline   = algorithmic bytes (read S + write S per op) / kernel time vs 8 TB/s
+  cpu_baseline = the CPU oracle (oracle/ddt_oracle.c, a restatement of the reference
+               convertor) on the host cores of the same box, bounded sample.
+
+Other BASELINE configs: --config cfg1|cfg3|cfg4|cfg5 (cfg2 is the default).
+Launch: python bench.py --gpus N --steps K --warmup W (N > 1 via torch.distributed.run).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK = 8.0e12          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+GiB = float(1 << 30)
+
+
+# ------------------------------------------------------------------ workloads
+def halo_recipe(n=256, esize=8, tid=16):
+    """6 faces of an n^3 grid in C order [z][y][x] as one struct, resized to the field."""
+    field = n * n * n * esize
+    xface = ("vector", n * n, 1, n, ("basic", tid))
+    yface = ("vector", n, n, n * n, ("basic", tid))
+    zface = ("contig", n * n, ("basic", tid))
+    disps = [0, (n - 1) * esize, 0, (n - 1) * n * esize, 0, (n - 1) * n * n * esize]
+    st = ("struct", [1] * 6, disps, [xface, xface, yface, yface, zface, zface])
+    return ("resized", st, 0, field), field
+
+
+def face_recipes(n=256, esize=8, tid=16):
+    field = n * n * n * esize
+    return {
+        "x": ("resized", ("vector", n * n, 1, n, ("basic", tid)), 0, field),
+        "y": ("resized", ("vector", n, n, n * n, ("basic", tid)), 0, field),
+        "z": ("resized", ("contig", n * n, ("basic", tid)), 0, field),
+    }
+
+
+def lcg_disps(n):
+    """cfg4 displacements: x_{i+1} = (1664525 x_i + 1013904223) mod 2^28, x_0 = 0x5EED."""
+    out = np.empty(n, dtype=np.int64)
+    x = 0x5EED
+    # vectorised by jumping: compute in chunks with the closed form of the affine map
+    a, c, m = 1664525, 1013904223, 1 << 28
+    chunk = 1 << 16
+    # powers for the first chunk
+    first = np.empty(chunk, dtype=np.int64)
+    for i in range(chunk):
+        first[i] = x
+        x = (a * x + c) % m
+    out[:chunk] = first
+    # A = a^chunk, C = c*(a^chunk - 1)/(a - 1) mod m  (per-step affine composition)
+    A, C = 1, 0
+    for _ in range(chunk):
+        A, C = (A * a) % m, (C * a + c) % m
+    prev = first
+    for s in range(chunk, n, chunk):
+        nxt = (A * prev + C) % m
+        k = min(chunk, n - s)
+        out[s:s + k] = nxt[:k]
+        prev = nxt
+    return out
+
+
+def make_workload(name):
+    """-> (recipe, count, description dict)"""
+    if name == "cfg2":
+        rec, field = halo_recipe()
+        return rec, 16, {"workload": "256^3 double 6-face halo, struct of vector faces resized "
+                                     "to the 128 MiB field, count = 16 fields per GPU",
+                         "grid": [256, 256, 256], "dtype_elem": "double", "fields_per_gpu": 16,
+                         "faces": 6}
+    if name == "cfg1":
+        return ("vector", 1024, 1, 2, ("basic", 16)), 2048, {
+            "workload": "MPI_Type_vector(1024,1,2) double x 2048 (16 MiB packed)"}
+    if name == "cfg3":
+        n, e = 512, 4
+        field = n * n * n * e
+        faces = [("subarray", [n, n, n], [1, n, n], [n - 1, 0, 0], 0, ("basic", 15)),
+                 ("subarray", [n, n, n], [n, 1, n], [0, n - 1, 0], 0, ("basic", 15)),
+                 ("subarray", [n, n, n], [n, n, 1], [0, 0, n - 1], 0, ("basic", 15))]
+        st = ("struct", [1, 1, 1], [0, 0, 0], faces)
+        return ("resized", st, 0, field), 8, {
+            "workload": "512^3 float subarray faces (dim0/dim1/dim2, start 511) as one struct, "
+                        "count = 8 fields per GPU (64 fields over 8 GPUs)"}
+    if name == "cfg4":
+        n = 64 << 20
+        d = lcg_disps(n)
+        return ("indexed_block", 1, d, ("basic", 15)), 1, {
+            "workload": "MPI_Type_indexed 64Mi unique LCG displacements into 1 GiB float"}
+    if name == "cfg5":
+        st = ("struct", [1, 3], [0, 8], [("basic", 16), ("basic", 6)])
+        return ("hvector", 128 << 20, 1, 32, st), 1, {
+            "workload": "hvector(128Mi,1,32B) of struct{double,int[3]} (2.5 GiB packed)"}
+    raise SystemExit(f"unknown config {name}")
+
+
+def layout(info, count):
+    ext = info["ub"] - info["lb"]
+    lo = min(info["true_lb"], info["true_lb"] + (count - 1) * ext)
+    hi = max(info["true_ub"], info["true_ub"] + (count - 1) * ext)
+    return hi - lo, -lo
+
+
+# ------------------------------------------------------------------ CPU baseline
+def cpu_baseline(recipe, count, name, first=None, budget_s=12.0):
+    """Oracle (restated reference CPU convertor) pack+unpack on host cores, bounded sample.
+
+    The oracle is the checker here, never the measured product: it also re-packs the
+    first instance of the GPU's user buffer and reports whether the GPU bytes match."""
+    from tests import recipes as R
+    sample_count = count
+    if name == "cfg2":
+        sample_count = 2
+    elif name == "cfg3":
+        sample_count = 1
+    elif name in ("cfg4", "cfg5"):
+        return None   # sampled separately below
+    b = R.Built(recipe)
+    info = b.o.info()
+    span, origin = layout(info, sample_count)
+    user = np.ones(span, dtype=np.uint8)
+    user[::7] = 3
+    S = info["size"] * sample_count
+    packed = np.zeros(S, dtype=np.uint8)
+    threads = min(16, os.cpu_count() or 1)
+    ptr = user.ctypes.data + origin
+    b.o.run_mt(sample_count, ptr, packed.ctypes.data, threads, False)   # warm
+    reps, t_tot, t0 = 0, 0.0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s and reps < 200:
+        a = time.perf_counter()
+        b.o.run_mt(sample_count, ptr, packed.ctypes.data, threads, False)
+        b.o.run_mt(sample_count, ptr, packed.ctypes.data, threads, True)
+        t_tot += time.perf_counter() - a
+        reps += 1
+    gibs = 2 * S * reps / t_tot / GiB
+    match = None
+    if first is not None:
+        host, sorig, gpu_bytes = first
+        ref = np.frombuffer(b.o.pack(1, host, sorig, 0, info["size"], element_granular=False),
+                            dtype=np.uint8)
+        match = bool(np.array_equal(ref, gpu_bytes))
+    return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "gpu_matches_oracle": match,
+            "sample": f"{sample_count} of {count} instances of the same committed type, "
+                      f"{reps} pack+unpack reps, {S} packed bytes each, oracle/ddt_oracle.c "
+                      f"position-sharded over {threads} threads"}
+
+
+# ------------------------------------------------------------------ main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--faces", action="store_true", help="also time each face type alone")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import ompi_amd
+    from ompi_amd import recipe as ER
+
+    recipe, count, desc = make_workload(args.config)
+    dt = ER.build_committed(recipe)
+    info = dt.info()
+    S = info["size"] * count
+    span, origin = layout(info, count)
+
+    user = torch.empty(span, dtype=torch.uint8, device=dev)
+    user.copy_(torch.randint(1, 255, (span,), dtype=torch.uint8, device=dev))
+    packed = torch.empty(S, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    cp = ompi_amd.Convertor()
+    cu = ompi_amd.Convertor()
+    for c in (cp, cu):
+        c.set_stream(stream, True)
+    uptr = user.data_ptr() + origin
+
+    def pack():
+        cp.prepare_for_send(dt, count, uptr)
+        rc, _, md = cp.pack([(packed, S)])
+        assert rc == 1 and md == S
+
+    def unpack():
+        cu.prepare_for_recv(dt, count, uptr)
+        rc, _, md = cu.unpack([(packed, S)])
+        assert rc == 1 and md == S
+
+    pack()
+    unpack()
+    torch.cuda.synchronize()
+    first = None
+    if rank == 0 and args.config in ("cfg1", "cfg2", "cfg3"):
+        sspan, sorig = layout(info, 1)
+        first = (user[origin - sorig: origin - sorig + sspan].cpu().numpy(), sorig,
+                 packed[:info["size"]].cpu().numpy())
+
+    for _ in range(args.warmup):
+        pack()
+        unpack()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e0, e1, e2 in ev:
+        e0.record(stream)
+        pack()
+        e1.record(stream)
+        unpack()
+        e2.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([wall], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.barrier()
+        wall = float(t.item())
+    tp = float(np.mean([a.elapsed_time(b) for a, b, _ in ev])) / 1e3
+    tu = float(np.mean([b.elapsed_time(c) for _, b, c in ev])) / 1e3
+
+    result = None
+    if rank == 0:
+        ms_per_step = wall / args.steps * 1e3
+        value = 2.0 * S * world * args.steps / wall / GiB
+        achieved = 4.0 * S / (tp + tu)
+        result = {
+            "metric": "pack+unpack GiB/s/GPU (device-resident), 256^3 double 3D-vector; %HBM peak",
+            "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u8", "data": "synthetic",
+            "config": dict(desc, config=args.config, packed_bytes_per_gpu=S,
+                           parallelism=f"replicas x{world} (fields sharded by count, no collective)"),
+            "per_gpu_GiBs": round(2.0 * S / (tp + tu) / GiB, 3),
+            "kernel_ms": {"pack": round(tp * 1e3, 4), "unpack": round(tu * 1e3, 4)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 2), "peak": 8000.0,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": None},
+        }
+        tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+        if os.path.exists(tfile):
+            with open(tfile) as f:
+                result["roofline"]["traffic"] = json.load(f).get("bytes_per_step")
+
+    if args.faces and rank == 0:
+        faces = {}
+        for k, frec in (face_recipes().items() if args.config == "cfg2" else []):
+            ft = ER.build_committed(frec)
+            fS = ft.info()["size"] * count
+            fp = torch.empty(fS, dtype=torch.uint8, device=dev)
+            c1 = ompi_amd.Convertor()
+            c1.set_stream(stream, True)
+            evs = []
+            for i in range(args.warmup + args.steps):
+                a, b_, c_ = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                a.record(stream)
+                c1.prepare_for_send(ft, count, user.data_ptr())
+                c1.pack([(fp, fS)])
+                b_.record(stream)
+                c1.prepare_for_recv(ft, count, user.data_ptr())
+                c1.unpack([(fp, fS)])
+                c_.record(stream)
+                if i >= args.warmup:
+                    evs.append((a, b_, c_))
+            torch.cuda.synchronize()
+            fp_t = float(np.mean([a.elapsed_time(b_) for a, b_, _ in evs])) / 1e3
+            fu_t = float(np.mean([b_.elapsed_time(c_) for _, b_, c_ in evs])) / 1e3
+            faces[k] = {"GiBs": round(2 * fS / (fp_t + fu_t) / GiB, 2),
+                        "frac": round(4 * fS / (fp_t + fu_t) / HBM_PEAK, 4),
+                        "pack_us": round(fp_t * 1e6, 2), "unpack_us": round(fu_t * 1e6, 2)}
+        result["faces"] = faces
+
+    if rank == 0 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(recipe, count, args.config, first)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

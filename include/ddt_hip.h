@@ -1,0 +1,217 @@
+/*
+ * ddt_hip.h -- C ABI of libddt_hip.so, an MI355X-native MPI derived-datatype
+ * pack/unpack engine that sits behind Open MPI's datatype/convertor API.
+ *
+ * Every entry point uses plain pointers and sizes.  Each one names the Open MPI
+ * interface it replaces (paths relative to the Open MPI source tree).  The
+ * convertor functions keep the reference's argument meaning and return codes:
+ * pack/unpack return 1 when the whole message has been converted, 0 when more
+ * fragments remain, and a negative code on error (opal_convertor.h:179-196).
+ *
+ * Buffers: the user buffer handed to prepare_for_send/recv must be device
+ * memory (hipMalloc / hipMallocManaged) -- this is the accelerator slot of the
+ * convertor, selected by opal_convertor_prepare_for_{send,recv} when
+ * check_addr reports a device pointer (opal_convertor.c:593-608).  The packed
+ * iovec buffers may be device or host memory; host iovecs are staged through
+ * HBM with hipMemcpyAsync.
+ */
+#ifndef DDT_HIP_H
+#define DDT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <sys/uio.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes (mirror OPAL_SUCCESS / OPAL_ERR_* sign convention) ---- */
+#define DDT_SUCCESS 0
+#define DDT_ERROR (-1)
+#define DDT_ERR_OUT_OF_RESOURCE (-2)
+#define DDT_ERR_BAD_PARAM (-5)
+#define DDT_ERR_NOT_COMMITTED (-6)
+#define DDT_ERR_NOT_DEVICE (-7)     /* user buffer is not device memory */
+#define DDT_ERR_HIP (-8)            /* a HIP runtime call failed */
+#define DDT_ERR_TRUNCATE (-9)       /* MPI_ERR_TRUNCATE analogue for ddt_pack/ddt_unpack */
+#define DDT_ERR_NOT_SUPPORTED (-10)
+
+/* ---- predefined type ids: identical to OPAL_DATATYPE_* (opal_datatype_internal.h:71-99) ---- */
+#define DDT_INT1 4
+#define DDT_INT2 5
+#define DDT_INT4 6
+#define DDT_INT8 7
+#define DDT_INT16 8
+#define DDT_UINT1 9
+#define DDT_UINT2 10
+#define DDT_UINT4 11
+#define DDT_UINT8 12
+#define DDT_UINT16 13
+#define DDT_FLOAT2 14
+#define DDT_FLOAT4 15
+#define DDT_FLOAT8 16
+#define DDT_FLOAT12 17
+#define DDT_FLOAT16 18
+#define DDT_SHORT_FLOAT_COMPLEX 19
+#define DDT_FLOAT_COMPLEX 20
+#define DDT_DOUBLE_COMPLEX 21
+#define DDT_LONG_DOUBLE_COMPLEX 22
+#define DDT_BOOL 23
+#define DDT_WCHAR 24
+#define DDT_LONG 25
+#define DDT_UNSIGNED_LONG 26
+#define DDT_FLOAT128_COMPLEX 27
+
+/* ---- datatype flags (values of OPAL_DATATYPE_FLAG_*, opal_datatype.h:80-105) ---- */
+#define DDT_FLAG_PREDEFINED 0x0002u
+#define DDT_FLAG_COMMITTED 0x0004u
+#define DDT_FLAG_OVERLAP 0x0008u
+#define DDT_FLAG_CONTIGUOUS 0x0010u
+#define DDT_FLAG_NO_GAPS 0x0020u
+#define DDT_FLAG_USER_LB 0x0040u
+#define DDT_FLAG_USER_UB 0x0080u
+#define DDT_FLAG_DATA 0x0100u
+
+#define DDT_ORDER_C 0
+#define DDT_ORDER_FORTRAN 1
+
+typedef struct ddt_datatype ddt_datatype_t;
+typedef struct ddt_convertor ddt_convertor_t;
+
+/* ================= datatype construction (ompi/datatype/ompi_datatype.h:217-284) ================= */
+
+/* Predefined type handle (opal_datatype_basicDatatypes[id], opal_datatype.h:216-248). Never freed. */
+const ddt_datatype_t *ddt_predefined(int id);
+
+/* ompi_datatype_create_contiguous (ompi_datatype_create_contiguous.c:31-44) */
+int ddt_type_create_contiguous(size_t count, const ddt_datatype_t *oldtype, ddt_datatype_t **newtype);
+/* ompi_datatype_create_vector / _hvector (ompi_datatype_create_vector.c:32-88); hvector stride in bytes */
+int ddt_type_create_vector(size_t count, size_t blocklen, ptrdiff_t stride,
+                           const ddt_datatype_t *oldtype, ddt_datatype_t **newtype);
+int ddt_type_create_hvector(size_t count, size_t blocklen, ptrdiff_t stride_bytes,
+                            const ddt_datatype_t *oldtype, ddt_datatype_t **newtype);
+/* ompi_datatype_create_indexed / _hindexed (ompi_datatype_create_indexed.c:35-114) */
+int ddt_type_create_indexed(size_t count, const size_t *blocklens, const ptrdiff_t *disps,
+                            const ddt_datatype_t *oldtype, ddt_datatype_t **newtype);
+int ddt_type_create_hindexed(size_t count, const size_t *blocklens, const ptrdiff_t *disps_bytes,
+                             const ddt_datatype_t *oldtype, ddt_datatype_t **newtype);
+/* ompi_datatype_create_indexed_block / _hindexed_block (ompi_datatype_create_indexed.c:117-183) */
+int ddt_type_create_indexed_block(size_t count, size_t blocklen, const ptrdiff_t *disps,
+                                  const ddt_datatype_t *oldtype, ddt_datatype_t **newtype);
+int ddt_type_create_hindexed_block(size_t count, size_t blocklen, const ptrdiff_t *disps_bytes,
+                                   const ddt_datatype_t *oldtype, ddt_datatype_t **newtype);
+/* ompi_datatype_create_struct (ompi_datatype_create_struct.c:32-98); disps in bytes */
+int ddt_type_create_struct(size_t count, const size_t *blocklens, const ptrdiff_t *disps,
+                           const ddt_datatype_t *const *types, ddt_datatype_t **newtype);
+/* ompi_datatype_create_subarray (ompi_datatype_create_subarray.c:32-112) */
+int ddt_type_create_subarray(int ndims, const size_t *sizes, const size_t *subsizes,
+                             const size_t *starts, int order, const ddt_datatype_t *oldtype,
+                             ddt_datatype_t **newtype);
+/* ompi_datatype_create_resized (ompi_datatype.h:270-284) */
+int ddt_type_create_resized(const ddt_datatype_t *oldtype, ptrdiff_t lb, ptrdiff_t extent,
+                            ddt_datatype_t **newtype);
+/* ompi_datatype_duplicate (ompi_datatype_create.c:115-145) */
+int ddt_type_dup(const ddt_datatype_t *oldtype, ddt_datatype_t **newtype);
+/* opal_datatype_commit (opal_datatype_optimize.c:1739-1782): freezes the type map and
+ * builds the device plan lazily on first use. */
+int ddt_type_commit(ddt_datatype_t *type);
+/* ompi_datatype_destroy / OBJ_RELEASE; predefined handles are ignored. */
+int ddt_type_destroy(ddt_datatype_t **type);
+
+/* ---- queries (opal_datatype.h:290-330) ---- */
+int ddt_type_size(const ddt_datatype_t *type, size_t *size);
+int ddt_type_get_extent(const ddt_datatype_t *type, ptrdiff_t *lb, ptrdiff_t *extent);
+int ddt_type_get_true_extent(const ddt_datatype_t *type, ptrdiff_t *true_lb, ptrdiff_t *true_extent);
+uint32_t ddt_type_flags(const ddt_datatype_t *type);
+/* out[0..7] = size, lb, ub, true_lb, true_ub, align, flags, nbElems */
+int ddt_type_info(const ddt_datatype_t *type, int64_t *out8);
+
+/* Import a committed Open MPI description: `desc` is the opal_datatype_t::opt_desc
+ * (or ::desc) array of `used` dt_elem_desc_t entries, 32 bytes each, layout of
+ * opal_datatype_internal.h:119-160.  Bounds are copied from the opal_datatype_t.
+ * This is the bridge a convertor plug-in uses to hand its type map to the engine. */
+int ddt_type_from_opal_desc(const void *desc, size_t used, size_t size, ptrdiff_t lb, ptrdiff_t ub,
+                            ptrdiff_t true_lb, ptrdiff_t true_ub, ddt_datatype_t **newtype);
+
+/* ================= convertor (opal/datatype/opal_convertor.h) ================= */
+
+ddt_convertor_t *ddt_convertor_create(void);                   /* opal_convertor_create */
+void ddt_convertor_destroy(ddt_convertor_t *conv);             /* OBJ_RELEASE(convertor) */
+/* opal_convertor_prepare_for_send (opal_convertor.c:648-696) */
+int ddt_convertor_prepare_for_send(ddt_convertor_t *conv, const ddt_datatype_t *type, size_t count,
+                                   const void *buf);
+/* opal_convertor_prepare_for_recv (opal_convertor.c:616-646) */
+int ddt_convertor_prepare_for_recv(ddt_convertor_t *conv, const ddt_datatype_t *type, size_t count,
+                                   void *buf);
+/* opal_convertor_pack (opal_convertor.c:255-305): fAdvance slot = opal_pack_accelerator_simple
+ * (opal_datatype_pack_accelerator.c:161-295).  Never splits a predefined element. */
+int32_t ddt_convertor_pack(ddt_convertor_t *conv, struct iovec *iov, uint32_t *out_size,
+                           size_t *max_data);
+/* opal_convertor_unpack (opal_convertor.c:307-349): fAdvance slot = opal_unpack_accelerator_simple
+ * (opal_datatype_unpack_accelerator.c:210-368).  Accepts arbitrary byte windows. */
+int32_t ddt_convertor_unpack(ddt_convertor_t *conv, struct iovec *iov, uint32_t *out_size,
+                             size_t *max_data);
+/* opal_convertor_set_position (opal_convertor.h:357-394) */
+int ddt_convertor_set_position(ddt_convertor_t *conv, size_t *position);
+/* opal_convertor_get_packed_size / get_unpacked_size (opal_convertor.h:240-262) */
+int ddt_convertor_get_packed_size(const ddt_convertor_t *conv, size_t *size);
+/* bConverted and CONVERTOR_COMPLETED (opal_convertor.h:137-148) */
+int ddt_convertor_get_position(const ddt_convertor_t *conv, size_t *position);
+int ddt_convertor_is_completed(const ddt_convertor_t *conv);
+/* CONVERTOR_ACCELERATOR_ASYNC + convertor->stream (opal_convertor.h:150, pml_ob1_recvreq.c:627-663):
+ * with async != 0 the kernels are enqueued on `hip_stream` and pack/unpack return without
+ * synchronizing; the caller records an event on the stream.  async == 0 (default) = synchronous. */
+int ddt_convertor_set_stream(ddt_convertor_t *conv, void *hip_stream, int async);
+
+/* ================= MPI front end (ompi/mpi/c/pack.c.in, unpack.c.in, pack_size.c.in) ================= */
+
+/* MPI_Pack: packs incount instances at inbuf into outbuf[*position ..], advances *position. */
+int ddt_pack(const void *inbuf, size_t incount, const ddt_datatype_t *type, void *outbuf,
+             size_t outsize, size_t *position);
+/* MPI_Unpack */
+int ddt_unpack(const void *inbuf, size_t insize, size_t *position, void *outbuf, size_t outcount,
+               const ddt_datatype_t *type);
+/* MPI_Pack_size (homogeneous: incount * size) */
+int ddt_pack_size(size_t incount, const ddt_datatype_t *type, size_t *size);
+
+/* ================= engine extras ================= */
+
+/* Windowed pack/unpack on a stream, UCX generic-datatype form
+ * (pml_ucx_datatype.c:72-123): pack [offset, offset+max_len) of the packed stream of
+ * `count` instances at `buf`; *len returns the bytes produced. Byte-exact window. */
+int ddt_pack_window(const ddt_datatype_t *type, size_t count, const void *buf, size_t offset,
+                    void *dst, size_t max_len, size_t *len, void *hip_stream);
+int ddt_unpack_window(const ddt_datatype_t *type, size_t count, void *buf, size_t offset,
+                      const void *src, size_t len, void *hip_stream);
+/* Device typed copy (opal_datatype_copy_content_same_ddt, opal_datatype_copy.c:141-178):
+ * copies count instances from src layout to dst layout of the same type, D2D, one launch. */
+int ddt_copy_content_same_ddt(const ddt_datatype_t *type, size_t count, void *dst, const void *src,
+                              void *hip_stream);
+
+/* Plan introspection for tests/benchmarks: number of leaves, device metadata bytes. */
+int ddt_type_plan_info(const ddt_datatype_t *type, int64_t *out4);
+/* ---- introspection for the CPU test-suite (no data movement; never used by pack/unpack) ----
+ * ddt_type_plan_leaves: serialises the plan's leaf streams as int64 records
+ *   [kind, blen, src_off, dst_off, ndim, list_leaf_index, (cnt, sstr, dstr) x ndim] and returns
+ *   the number of int64 written (or the number needed when cap is too small, as a negative).
+ * ddt_debug_items: the launch descriptors (ddt_device.h Item, raw bytes) that pack/unpack would
+ *   run for the packed window [w0, w1) of `count` instances at `user` with the packed pointer
+ *   `pk` holding byte w0; *nitems receives the count, *item_size the size of one Item.
+ * ddt_type_plan_list: host copy of index-list leaf `leaf`: block displacements and lengths. */
+int64_t ddt_type_plan_leaves(const ddt_datatype_t *type, int64_t *out, size_t cap);
+int ddt_debug_items(const ddt_datatype_t *type, size_t count, uint64_t user, uint64_t pk,
+                    uint64_t w0, uint64_t w1, int same_layout, void *out, size_t cap_bytes,
+                    size_t *nitems, size_t *item_size);
+int64_t ddt_type_plan_list(const ddt_datatype_t *type, size_t leaf, int64_t *disp, uint64_t *len,
+                           size_t cap);
+/* Library self-check of host-side index arithmetic (fast division); returns 0 on success. */
+int ddt_selftest(void);
+const char *ddt_version(void);
+/* Message of the last failing call on this thread (empty if none). */
+const char *ddt_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DDT_HIP_H */

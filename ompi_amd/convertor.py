@@ -1,0 +1,148 @@
+"""Host-side mirror of the Open MPI convertor (opal/datatype/opal_convertor.h) over
+libddt_hip.so, plus the MPI_Pack / MPI_Unpack front end.
+
+Buffers are passed as raw addresses or as objects with ``data_ptr()`` (torch tensors:
+device memory and streams are PyTorch's plumbing; the data movement is the HIP engine).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Sequence, Tuple
+
+from ._lib import IOVec, check, lib
+from .datatype import Datatype
+
+
+def addr(x) -> int:
+    if x is None:
+        return 0
+    if hasattr(x, "data_ptr"):
+        return int(x.data_ptr())
+    if isinstance(x, int):
+        return x
+    raise TypeError(f"cannot take the address of {type(x)}")
+
+
+def stream_handle(s) -> int:
+    if s is None:
+        return 0
+    if hasattr(s, "cuda_stream"):
+        return int(s.cuda_stream)
+    return int(s)
+
+
+class Convertor:
+    """opal_convertor_t: prepare once, then pack/unpack iovec fragments from the current position."""
+
+    def __init__(self):
+        self.h = ctypes.c_void_p(lib().ddt_convertor_create())
+        if not self.h:
+            raise MemoryError("ddt_convertor_create")
+
+    def close(self):
+        if self.h:
+            lib().ddt_convertor_destroy(self.h)
+            self.h = ctypes.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def prepare_for_send(self, dt: Datatype, count: int, buf) -> "Convertor":
+        check(lib().ddt_convertor_prepare_for_send(self.h, dt.handle, count, addr(buf)),
+              "ddt_convertor_prepare_for_send")
+        return self
+
+    def prepare_for_recv(self, dt: Datatype, count: int, buf) -> "Convertor":
+        check(lib().ddt_convertor_prepare_for_recv(self.h, dt.handle, count, addr(buf)),
+              "ddt_convertor_prepare_for_recv")
+        return self
+
+    def set_stream(self, stream, async_: bool = True) -> None:
+        check(lib().ddt_convertor_set_stream(self.h, stream_handle(stream), int(async_)),
+              "ddt_convertor_set_stream")
+
+    def _advance(self, fn, iovs: Sequence[Tuple[object, int]]):
+        n = len(iovs)
+        arr = (IOVec * max(n, 1))()
+        for i, (b, ln) in enumerate(iovs):
+            arr[i].iov_base = addr(b)
+            arr[i].iov_len = int(ln)
+        out_size = ctypes.c_uint32(n)
+        max_data = ctypes.c_size_t(0)
+        rc = check(fn(self.h, arr, ctypes.byref(out_size), ctypes.byref(max_data)), fn.__name__)
+        lens: List[int] = [int(arr[i].iov_len) for i in range(out_size.value)]
+        return rc, lens, int(max_data.value)
+
+    def pack(self, iovs: Sequence[Tuple[object, int]]):
+        """opal_convertor_pack: returns (1 if complete else 0, bytes per iovec used, total)."""
+        return self._advance(lib().ddt_convertor_pack, iovs)
+
+    def unpack(self, iovs: Sequence[Tuple[object, int]]):
+        """opal_convertor_unpack."""
+        return self._advance(lib().ddt_convertor_unpack, iovs)
+
+    def set_position(self, position: int) -> int:
+        p = ctypes.c_size_t(position)
+        check(lib().ddt_convertor_set_position(self.h, ctypes.byref(p)), "ddt_convertor_set_position")
+        return int(p.value)
+
+    @property
+    def packed_size(self) -> int:
+        s = ctypes.c_size_t()
+        check(lib().ddt_convertor_get_packed_size(self.h, ctypes.byref(s)), "get_packed_size")
+        return int(s.value)
+
+    @property
+    def position(self) -> int:
+        s = ctypes.c_size_t()
+        check(lib().ddt_convertor_get_position(self.h, ctypes.byref(s)), "get_position")
+        return int(s.value)
+
+    @property
+    def completed(self) -> bool:
+        return bool(lib().ddt_convertor_is_completed(self.h))
+
+
+# ------------------------------------------------------------------ MPI front end
+def pack_size(incount: int, dt: Datatype) -> int:
+    s = ctypes.c_size_t()
+    check(lib().ddt_pack_size(incount, dt.handle, ctypes.byref(s)), "ddt_pack_size")
+    return int(s.value)
+
+
+def pack(inbuf, incount: int, dt: Datatype, outbuf, outsize: int, position: int = 0) -> int:
+    """MPI_Pack: returns the new position."""
+    p = ctypes.c_size_t(position)
+    check(lib().ddt_pack(addr(inbuf), incount, dt.handle, addr(outbuf), outsize, ctypes.byref(p)),
+          "ddt_pack")
+    return int(p.value)
+
+
+def unpack(inbuf, insize: int, position: int, outbuf, outcount: int, dt: Datatype) -> int:
+    """MPI_Unpack: returns the new position."""
+    p = ctypes.c_size_t(position)
+    check(lib().ddt_unpack(addr(inbuf), insize, ctypes.byref(p), addr(outbuf), outcount, dt.handle),
+          "ddt_unpack")
+    return int(p.value)
+
+
+def pack_window(dt: Datatype, count: int, buf, offset: int, dst, max_len: int, stream=None) -> int:
+    """UCX generic-datatype pack (pml_ucx_datatype.c:72-88): bytes [offset, offset+max_len)."""
+    n = ctypes.c_size_t()
+    check(lib().ddt_pack_window(dt.handle, count, addr(buf), offset, addr(dst), max_len,
+                                ctypes.byref(n), stream_handle(stream)), "ddt_pack_window")
+    return int(n.value)
+
+
+def unpack_window(dt: Datatype, count: int, buf, offset: int, src, length: int, stream=None) -> None:
+    check(lib().ddt_unpack_window(dt.handle, count, addr(buf), offset, addr(src), length,
+                                  stream_handle(stream)), "ddt_unpack_window")
+
+
+def copy_content_same_ddt(dt: Datatype, count: int, dst, src, stream=None) -> None:
+    """opal_datatype_copy_content_same_ddt: typed device-to-device copy in one launch."""
+    check(lib().ddt_copy_content_same_ddt(dt.handle, count, addr(dst), addr(src),
+                                          stream_handle(stream)), "ddt_copy_content_same_ddt")

@@ -1,0 +1,662 @@
+// ddt_convertor.cpp -- convertor state machine, HIP execution and the C ABI of
+// libddt_hip.so.
+//
+// Mirrors opal_convertor_t semantics (opal/datatype/opal_convertor.h:125-170,
+// opal_convertor.c:255-349, 526-696): prepare records (type, count, buffer) and
+// the packed size; pack/unpack consume iovecs from the current position
+// (bConverted) and return 1 once the whole message is converted.  Resume state is
+// just bConverted: every window is recomputed from the packed position in O(leaves)
+// (the reference keeps a descriptor stack, opal_convertor.h:111-117, and walks to
+// it in opal_convertor_generic_simple_position, opal_datatype_position.c:167-367).
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include <hip/hip_runtime.h>
+
+#include "ddt_core.h"
+#include "ddt_hip.h"
+#include "ddt_plan.h"
+
+using namespace ddt;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+#define HIPCHK(call)                                                                   \
+    do {                                                                               \
+        hipError_t _e = (call);                                                        \
+        if (_e != hipSuccess)                                                          \
+            return fail(DDT_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+enum MemKind { MEM_DEVICE, MEM_HOST };
+
+MemKind classify(const void *p)
+{
+    hipPointerAttribute_t a;
+    hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void) hipGetLastError();
+        return MEM_HOST;
+    }
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged
+        || a.type == hipMemoryTypeUnified || a.isManaged)
+        return MEM_DEVICE;
+    return MEM_HOST;
+}
+
+struct Window {
+    uint64_t w0, w1;   // packed-stream byte range
+    uint64_t ptr;      // device pointer holding byte w0
+};
+
+constexpr size_t kCacheEntries = 32;
+constexpr uint64_t kStageChunk = 16ull << 20;   // host staging pipeline chunk
+
+// Find or build the descriptor set of one launch and run it on `stream`.
+int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
+                const std::vector<Window> &wins, bool same_layout, int dir, hipStream_t stream)
+{
+    if (wins.empty())
+        return DDT_SUCCESS;
+    std::vector<uint64_t> key;
+    key.reserve(4 + 3 * wins.size());
+    key.push_back(count);
+    key.push_back(user);
+    key.push_back(same_layout ? 1 : 0);
+    for (const Window &w : wins) {
+        key.push_back(w.w0);
+        key.push_back(w.w1);
+        key.push_back(w.ptr);
+    }
+    try {
+        ensure_device_lists(P);
+    } catch (const std::exception &ex) {
+        return fail(DDT_ERR_OUT_OF_RESOURCE, ex.what());
+    }
+    std::shared_ptr<ItemSet> S;
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        for (size_t i = 0; i < P.cache.size(); ++i) {
+            if (P.cache[i]->key == key) {
+                S = P.cache[i];
+                if (i)
+                    std::rotate(P.cache.begin(), P.cache.begin() + long(i), P.cache.begin() + long(i) + 1);
+                break;
+            }
+        }
+    }
+    if (!S) {
+        S = std::make_shared<ItemSet>();
+        S->key = key;
+        try {
+            for (const Window &w : wins)
+                build_items(t, P, count, user, w.ptr, w.w0, w.w1, same_layout, S->items);
+        } catch (const std::exception &ex) {
+            return fail(DDT_ERR_NOT_SUPPORTED, ex.what());
+        }
+        assign_tasks(S->items);
+        S->ntasks = total_tasks(S->items);
+        if (!S->items.empty()) {
+            size_t bytes = S->items.size() * sizeof(Item);
+            Item *h = nullptr;
+            HIPCHK(hipHostMalloc((void **) &h, bytes, hipHostMallocDefault));
+            std::memcpy(h, S->items.data(), bytes);
+            hipError_t e = hipMalloc((void **) &S->d_items, bytes);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(S->d_items, h, bytes, hipMemcpyHostToDevice, stream);
+            if (e == hipSuccess)
+                e = hipStreamSynchronize(stream);   // h is released right after
+            (void) hipHostFree(h);
+            if (e != hipSuccess)
+                return fail(DDT_ERR_HIP, std::string("item upload: ") + hipGetErrorString(e));
+        }
+        HIPCHK(hipEventCreateWithFlags(&S->last_use, hipEventDisableTiming));
+        std::shared_ptr<ItemSet> evicted;
+        {
+            std::lock_guard<std::mutex> g(P.mu);
+            P.cache.insert(P.cache.begin(), S);
+            if (P.cache.size() > kCacheEntries) {
+                evicted = P.cache.back();
+                P.cache.pop_back();
+            }
+        }
+        evicted.reset();   // waits for its last launch
+    }
+    if (S->items.empty())
+        return DDT_SUCCESS;
+    HIPCHK(launch_move(S->d_items, uint32_t(S->items.size()), S->ntasks, dir, stream));
+    HIPCHK(hipEventRecord(S->last_use, stream));
+    return DDT_SUCCESS;
+}
+
+}  // namespace
+
+struct ddt_convertor {
+    ddt_datatype *dt = nullptr;
+    std::shared_ptr<Plan> plan;
+    uint64_t count = 0;
+    uint64_t base = 0;
+    bool send = false;
+    bool prepared = false;
+    bool completed = false;
+    uint64_t local_size = 0;
+    uint64_t bConverted = 0;
+    hipStream_t stream = nullptr;
+    bool async = false;
+    // host-iovec staging pipeline (two HBM slots, one copy stream)
+    void *stage[2] = {nullptr, nullptr};
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t ev_k[2] = {nullptr, nullptr}, ev_c[2] = {nullptr, nullptr};
+    ~ddt_convertor()
+    {
+        if (stream)
+            (void) hipStreamSynchronize(stream);
+        if (copy_stream) {
+            (void) hipStreamSynchronize(copy_stream);
+            (void) hipStreamDestroy(copy_stream);
+        }
+        for (int i = 0; i < 2; ++i) {
+            if (stage[i]) (void) hipFree(stage[i]);
+            if (ev_k[i]) (void) hipEventDestroy(ev_k[i]);
+            if (ev_c[i]) (void) hipEventDestroy(ev_c[i]);
+        }
+    }
+    int ensure_staging()
+    {
+        if (copy_stream)
+            return DDT_SUCCESS;
+        HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+        for (int i = 0; i < 2; ++i) {
+            HIPCHK(hipMalloc(&stage[i], kStageChunk));
+            HIPCHK(hipEventCreateWithFlags(&ev_k[i], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&ev_c[i], hipEventDisableTiming));
+        }
+        return DDT_SUCCESS;
+    }
+};
+
+namespace {
+
+// Move the packed windows of a convertor call: device iovecs in one launch, host iovecs
+// through the HBM staging pipeline (kernel on the user stream, copies on copy_stream).
+int execute(ddt_convertor *c, const std::vector<Window> &dev_wins,
+            const std::vector<std::pair<Window, void *>> &host_wins, int dir)
+{
+    int rc = run_windows(c->dt, *c->plan, c->count, c->base, dev_wins, false, dir, c->stream);
+    if (rc != DDT_SUCCESS)
+        return rc;
+    if (!host_wins.empty()) {
+        if ((rc = c->ensure_staging()) != DDT_SUCCESS)
+            return rc;
+        int k = 0;
+        bool used[2] = {false, false};
+        for (const auto &hw : host_wins) {
+            for (uint64_t off = hw.first.w0; off < hw.first.w1; off += kStageChunk, ++k) {
+                const int s = k & 1;
+                const uint64_t n = std::min<uint64_t>(kStageChunk, hw.first.w1 - off);
+                char *hp = static_cast<char *>(hw.second) + (off - hw.first.w0);
+                std::vector<Window> w{{off, off + n, uint64_t(uintptr_t(c->stage[s]))}};
+                if (dir == 0) {   // pack: kernel -> D2H
+                    if (used[s])
+                        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_c[s], 0));
+                    if ((rc = run_windows(c->dt, *c->plan, c->count, c->base, w, false, 0, c->stream)))
+                        return rc;
+                    HIPCHK(hipEventRecord(c->ev_k[s], c->stream));
+                    HIPCHK(hipStreamWaitEvent(c->copy_stream, c->ev_k[s], 0));
+                    HIPCHK(hipMemcpyAsync(hp, c->stage[s], n, hipMemcpyDeviceToHost, c->copy_stream));
+                    HIPCHK(hipEventRecord(c->ev_c[s], c->copy_stream));
+                } else {          // unpack: H2D -> kernel
+                    if (used[s])
+                        HIPCHK(hipStreamWaitEvent(c->copy_stream, c->ev_k[s], 0));
+                    HIPCHK(hipMemcpyAsync(c->stage[s], hp, n, hipMemcpyHostToDevice, c->copy_stream));
+                    HIPCHK(hipEventRecord(c->ev_c[s], c->copy_stream));
+                    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_c[s], 0));
+                    if ((rc = run_windows(c->dt, *c->plan, c->count, c->base, w, false, 1, c->stream)))
+                        return rc;
+                    HIPCHK(hipEventRecord(c->ev_k[s], c->stream));
+                }
+                used[s] = true;
+            }
+        }
+        // the user stream observes completion of the last copies
+        for (int s = 0; s < 2; ++s)
+            if (used[s])
+                HIPCHK(hipStreamWaitEvent(c->stream, c->ev_c[s], 0));
+    }
+    if (!c->async)
+        HIPCHK(hipStreamSynchronize(c->stream));
+    return DDT_SUCCESS;
+}
+
+int prepare(ddt_convertor *c, const ddt_datatype *t, size_t count, const void *buf, bool send)
+{
+    if (!c || !t)
+        return fail(DDT_ERR_BAD_PARAM, "null convertor or datatype");
+    if (!(t->flags & F_COMMITTED))
+        return fail(DDT_ERR_NOT_COMMITTED, "datatype not committed");
+    ddt_datatype *dt = const_cast<ddt_datatype *>(t);
+    c->dt = dt;
+    c->count = count;
+    c->base = uint64_t(uintptr_t(buf));
+    c->send = send;
+    c->local_size = uint64_t(t->size) * count;
+    c->bConverted = 0;
+    c->completed = (c->local_size == 0);
+    c->prepared = true;
+    if (c->local_size == 0)
+        return DDT_SUCCESS;
+    // accelerator slot: check_addr must report device memory (opal_convertor.c:593-608)
+    if (classify(buf) != MEM_DEVICE)
+        return fail(DDT_ERR_NOT_DEVICE, "user buffer is not device memory: the HIP engine is the "
+                                        "accelerator slot of the convertor");
+    try {
+        c->plan = get_plan(dt);
+    } catch (const std::exception &ex) {
+        return fail(DDT_ERR_OUT_OF_RESOURCE, ex.what());
+    }
+    return DDT_SUCCESS;
+}
+
+int32_t advance(ddt_convertor *c, struct iovec *iov, uint32_t *out_size, size_t *max_data, int dir)
+{
+    if (!c || !c->prepared || !out_size || !max_data || (*out_size && !iov))
+        return fail(DDT_ERR_BAD_PARAM, "convertor not prepared or bad iovec");
+    if (c->completed) {   // opal_convertor_pack/unpack: nothing left (opal_convertor.c:258-261)
+        if (*out_size)
+            iov[0].iov_len = 0;
+        *out_size = 0;
+        *max_data = 0;
+        return 1;
+    }
+    std::vector<Window> dev;
+    std::vector<std::pair<Window, void *>> host;
+    uint64_t pos = c->bConverted, total = 0;
+    uint32_t used = 0;
+    for (uint32_t i = 0; i < *out_size; ++i) {
+        if (pos >= c->local_size)
+            break;
+        uint64_t w1 = std::min<uint64_t>(pos + iov[i].iov_len, c->local_size);
+        if (dir == 0 && w1 < c->local_size) {   // pack never splits a predefined element
+            uint64_t s = snap_down_to_element(c->dt, w1);
+            w1 = std::max(s, pos);
+        }
+        uint64_t n = w1 - pos;
+        iov[i].iov_len = n;
+        used = i + 1;
+        if (n) {
+            if (!iov[i].iov_base)
+                return fail(DDT_ERR_BAD_PARAM, "null iov_base");
+            if (classify(iov[i].iov_base) == MEM_DEVICE)
+                dev.push_back({pos, w1, uint64_t(uintptr_t(iov[i].iov_base))});
+            else
+                host.push_back({{pos, w1, 0}, iov[i].iov_base});
+        }
+        pos = w1;
+        total += n;
+    }
+    int rc = execute(c, dev, host, dir);
+    if (rc != DDT_SUCCESS)
+        return rc;
+    c->bConverted = pos;
+    *out_size = used;
+    *max_data = total;
+    if (c->bConverted == c->local_size) {
+        c->completed = true;
+        return 1;
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+ddt_convertor_t *ddt_convertor_create(void) { return new (std::nothrow) ddt_convertor(); }
+
+void ddt_convertor_destroy(ddt_convertor_t *c) { delete c; }
+
+int ddt_convertor_prepare_for_send(ddt_convertor_t *c, const ddt_datatype_t *t, size_t count,
+                                   const void *buf)
+{
+    return prepare(c, t, count, buf, true);
+}
+
+int ddt_convertor_prepare_for_recv(ddt_convertor_t *c, const ddt_datatype_t *t, size_t count,
+                                   void *buf)
+{
+    return prepare(c, t, count, buf, false);
+}
+
+int32_t ddt_convertor_pack(ddt_convertor_t *c, struct iovec *iov, uint32_t *out_size, size_t *max_data)
+{
+    return advance(c, iov, out_size, max_data, 0);
+}
+
+int32_t ddt_convertor_unpack(ddt_convertor_t *c, struct iovec *iov, uint32_t *out_size,
+                             size_t *max_data)
+{
+    return advance(c, iov, out_size, max_data, 1);
+}
+
+int ddt_convertor_set_position(ddt_convertor_t *c, size_t *position)
+{
+    // opal_convertor_set_position (opal_convertor.h:357-394)
+    if (!c || !position || !c->prepared)
+        return fail(DDT_ERR_BAD_PARAM, "bad convertor");
+    if (c->local_size <= *position) {
+        c->completed = true;
+        c->bConverted = c->local_size;
+        *position = size_t(c->bConverted);
+        return DDT_SUCCESS;
+    }
+    c->completed = false;
+    c->bConverted = *position;
+    return DDT_SUCCESS;
+}
+
+int ddt_convertor_get_packed_size(const ddt_convertor_t *c, size_t *size)
+{
+    if (!c || !size)
+        return DDT_ERR_BAD_PARAM;
+    *size = size_t(c->local_size);
+    return DDT_SUCCESS;
+}
+
+int ddt_convertor_get_position(const ddt_convertor_t *c, size_t *position)
+{
+    if (!c || !position)
+        return DDT_ERR_BAD_PARAM;
+    *position = size_t(c->bConverted);
+    return DDT_SUCCESS;
+}
+
+int ddt_convertor_is_completed(const ddt_convertor_t *c) { return c && c->completed ? 1 : 0; }
+
+int ddt_convertor_set_stream(ddt_convertor_t *c, void *s, int async)
+{
+    if (!c)
+        return DDT_ERR_BAD_PARAM;
+    c->stream = static_cast<hipStream_t>(s);
+    c->async = async != 0;
+    return DDT_SUCCESS;
+}
+
+int ddt_pack_size(size_t incount, const ddt_datatype_t *t, size_t *size)
+{
+    if (!t || !size)
+        return DDT_ERR_BAD_PARAM;
+    *size = incount * size_t(t->size);
+    return DDT_SUCCESS;
+}
+
+int ddt_pack(const void *inbuf, size_t incount, const ddt_datatype_t *t, void *outbuf,
+             size_t outsize, size_t *position)
+{
+    // MPI_Pack (ompi/mpi/c/pack.c.in:41-164)
+    if (!t || !position || (!outbuf && outsize))
+        return fail(DDT_ERR_BAD_PARAM, "bad argument");
+    size_t need = incount * size_t(t->size);
+    if (*position > outsize || outsize - *position < need)
+        return fail(DDT_ERR_TRUNCATE, "output buffer too small");
+    if (need == 0)
+        return DDT_SUCCESS;
+    ddt_convertor c;
+    int rc = prepare(&c, t, incount, inbuf, true);
+    if (rc != DDT_SUCCESS)
+        return rc;
+    struct iovec iov{static_cast<char *>(outbuf) + *position, need};
+    uint32_t n = 1;
+    size_t max_data = 0;
+    int32_t r = advance(&c, &iov, &n, &max_data, 0);
+    if (r < 0)
+        return r;
+    *position += max_data;
+    return DDT_SUCCESS;
+}
+
+int ddt_unpack(const void *inbuf, size_t insize, size_t *position, void *outbuf, size_t outcount,
+               const ddt_datatype_t *t)
+{
+    // MPI_Unpack (ompi/mpi/c/unpack.c.in:38-171)
+    if (!t || !position || (!inbuf && insize))
+        return fail(DDT_ERR_BAD_PARAM, "bad argument");
+    size_t need = outcount * size_t(t->size);
+    if (*position > insize || insize - *position < need)
+        return fail(DDT_ERR_TRUNCATE, "input buffer too small");
+    if (need == 0)
+        return DDT_SUCCESS;
+    ddt_convertor c;
+    int rc = prepare(&c, t, outcount, outbuf, false);
+    if (rc != DDT_SUCCESS)
+        return rc;
+    struct iovec iov{const_cast<char *>(static_cast<const char *>(inbuf)) + *position, need};
+    uint32_t n = 1;
+    size_t max_data = 0;
+    int32_t r = advance(&c, &iov, &n, &max_data, 1);
+    if (r < 0)
+        return r;
+    *position += max_data;
+    return DDT_SUCCESS;
+}
+
+static int window_common(const ddt_datatype_t *t, size_t count, const void *buf, size_t offset,
+                         void *packed, size_t len, size_t *out_len, void *stream, int dir)
+{
+    if (!t || (!packed && len))
+        return fail(DDT_ERR_BAD_PARAM, "bad argument");
+    ddt_convertor c;
+    int rc = prepare(&c, t, count, buf, dir == 0);
+    if (rc != DDT_SUCCESS)
+        return rc;
+    c.stream = static_cast<hipStream_t>(stream);
+    c.async = true;
+    uint64_t w0 = std::min<uint64_t>(offset, c.local_size);
+    uint64_t w1 = std::min<uint64_t>(w0 + len, c.local_size);
+    std::vector<Window> dev;
+    std::vector<std::pair<Window, void *>> host;
+    if (w1 > w0) {
+        if (classify(packed) == MEM_DEVICE)
+            dev.push_back({w0, w1, uint64_t(uintptr_t(packed))});
+        else
+            host.push_back({{w0, w1, 0}, packed});
+    }
+    rc = execute(&c, dev, host, dir);
+    if (rc == DDT_SUCCESS && !host.empty())
+        HIPCHK(hipStreamSynchronize(c.stream));   // staging slots die with `c`
+    c.stream = nullptr;
+    if (out_len)
+        *out_len = size_t(w1 - w0);
+    return rc;
+}
+
+int ddt_pack_window(const ddt_datatype_t *t, size_t count, const void *buf, size_t offset,
+                    void *dst, size_t max_len, size_t *len, void *stream)
+{
+    return window_common(t, count, buf, offset, dst, max_len, len, stream, 0);
+}
+
+int ddt_unpack_window(const ddt_datatype_t *t, size_t count, void *buf, size_t offset,
+                      const void *src, size_t len, void *stream)
+{
+    return window_common(t, count, buf, offset, const_cast<void *>(src), len, nullptr, stream, 1);
+}
+
+int ddt_copy_content_same_ddt(const ddt_datatype_t *t, size_t count, void *dst, const void *src,
+                              void *stream)
+{
+    // opal_datatype_copy_content_same_ddt (opal_datatype_copy.c:141-178): device to device,
+    // one launch, user layout on both sides.
+    if (!t || ((!dst || !src) && count))
+        return fail(DDT_ERR_BAD_PARAM, "bad argument");
+    if (!(t->flags & F_COMMITTED))
+        return fail(DDT_ERR_NOT_COMMITTED, "datatype not committed");
+    if (count == 0 || t->size == 0)
+        return DDT_SUCCESS;
+    if (classify(dst) != MEM_DEVICE || classify(src) != MEM_DEVICE)
+        return fail(DDT_ERR_NOT_DEVICE, "typed copy needs device buffers");
+    ddt_datatype *dt = const_cast<ddt_datatype *>(t);
+    std::shared_ptr<Plan> P;
+    try {
+        P = get_plan(dt);
+    } catch (const std::exception &ex) {
+        return fail(DDT_ERR_OUT_OF_RESOURCE, ex.what());
+    }
+    std::vector<Window> w{{0, uint64_t(t->size) * count, uint64_t(uintptr_t(dst))}};
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rc = run_windows(dt, *P, count, uint64_t(uintptr_t(src)), w, true, 0, s);
+    if (rc != DDT_SUCCESS)
+        return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    return DDT_SUCCESS;
+}
+
+int ddt_type_plan_info(const ddt_datatype_t *t, int64_t *out4)
+{
+    if (!t || !out4)
+        return DDT_ERR_BAD_PARAM;
+    if (!(t->flags & F_COMMITTED))
+        return fail(DDT_ERR_NOT_COMMITTED, "datatype not committed");
+    std::shared_ptr<Plan> P;
+    try {
+        P = get_plan(const_cast<ddt_datatype *>(t));
+    } catch (const std::exception &ex) {
+        return fail(DDT_ERR_OUT_OF_RESOURCE, ex.what());
+    }
+    int64_t nl = 0, maxd = 0;
+    for (const Leaf &L : P->leaves) {
+        nl += L.kind == LEAF_LIST;
+        maxd = std::max<int64_t>(maxd, int64_t(L.dims.size()) + 1);
+    }
+    out4[0] = int64_t(P->leaves.size());
+    out4[1] = int64_t(P->dev_bytes);
+    out4[2] = nl;
+    out4[3] = maxd;
+    return DDT_SUCCESS;
+}
+
+int64_t ddt_type_plan_leaves(const ddt_datatype_t *t, int64_t *out, size_t cap)
+{
+    if (!t || !(t->flags & F_COMMITTED))
+        return fail(DDT_ERR_NOT_COMMITTED, "datatype not committed");
+    std::shared_ptr<Plan> P;
+    try {
+        P = get_plan(const_cast<ddt_datatype *>(t));
+    } catch (const std::exception &ex) {
+        return fail(DDT_ERR_OUT_OF_RESOURCE, ex.what());
+    }
+    std::vector<int64_t> v;
+    for (size_t i = 0; i < P->leaves.size(); ++i) {
+        const Leaf &L = P->leaves[i];
+        v.push_back(L.kind);
+        v.push_back(int64_t(L.kind == LEAF_AFFINE ? L.blen : L.list->total));
+        v.push_back(L.kind == LEAF_AFFINE ? L.src_off : L.list_shift);
+        v.push_back(L.dst_off);
+        v.push_back(int64_t(L.dims.size()));
+        v.push_back(int64_t(i));
+        for (const LeafDim &d : L.dims) {
+            v.push_back(int64_t(d.cnt));
+            v.push_back(d.sstr);
+            v.push_back(d.dstr);
+        }
+    }
+    if (v.size() > cap)
+        return -int64_t(v.size());
+    if (out)
+        std::memcpy(out, v.data(), v.size() * sizeof(int64_t));
+    return int64_t(v.size());
+}
+
+int64_t ddt_type_plan_list(const ddt_datatype_t *t, size_t leaf, int64_t *disp, uint64_t *len,
+                           size_t cap)
+{
+    if (!t || !(t->flags & F_COMMITTED))
+        return fail(DDT_ERR_NOT_COMMITTED, "datatype not committed");
+    std::shared_ptr<Plan> P = get_plan(const_cast<ddt_datatype *>(t));
+    if (leaf >= P->leaves.size() || P->leaves[leaf].kind != LEAF_LIST)
+        return fail(DDT_ERR_BAD_PARAM, "not a list leaf");
+    const IndexList &X = *P->leaves[leaf].list;
+    size_t n = X.nblk();
+    if (n > cap)
+        return -int64_t(n);
+    for (size_t k = 0; k < n; ++k) {
+        disp[k] = X.disp[k];
+        len[k] = X.len.empty() ? X.ulen : X.len[k];
+    }
+    return int64_t(n);
+}
+
+int ddt_debug_items(const ddt_datatype_t *t, size_t count, uint64_t user, uint64_t pk, uint64_t w0,
+                    uint64_t w1, int same_layout, void *out, size_t cap_bytes, size_t *nitems,
+                    size_t *item_size)
+{
+    if (!t || !(t->flags & F_COMMITTED))
+        return fail(DDT_ERR_NOT_COMMITTED, "datatype not committed");
+    std::shared_ptr<Plan> P = get_plan(const_cast<ddt_datatype *>(t));
+    std::vector<Item> items;
+    try {
+        build_items(t, *P, count, user, pk, w0, w1, same_layout != 0, items);
+    } catch (const std::exception &ex) {
+        return fail(DDT_ERR_NOT_SUPPORTED, ex.what());
+    }
+    assign_tasks(items);
+    if (item_size)
+        *item_size = sizeof(Item);
+    if (nitems)
+        *nitems = items.size();
+    if (items.size() * sizeof(Item) > cap_bytes)
+        return DDT_ERR_OUT_OF_RESOURCE;
+    if (out && !items.empty())
+        std::memcpy(out, items.data(), items.size() * sizeof(Item));
+    return DDT_SUCCESS;
+}
+
+int ddt_selftest(void)
+{
+    // exhaustive over small divisors, random over large ones
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (uint32_t d = 1; d < 5000; ++d) {
+        FastDiv f = make_fastdiv(d);
+        for (int k = 0; k < 200; ++k) {
+            x ^= x << 13;
+            x ^= x >> 7;
+            x ^= x << 17;
+            uint32_t n = uint32_t(x);
+            if (k < 4)
+                n = k == 0 ? 0 : (k == 1 ? 0xffffffffu : (k == 2 ? d : d - 1));
+            if (fastdiv(n, f) != n / d)
+                return 1;
+        }
+    }
+    for (int k = 0; k < 200000; ++k) {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        uint32_t d = uint32_t(x >> 32) | 1u, n = uint32_t(x);
+        if (k & 1)
+            d >>= (k % 31);
+        if (d == 0)
+            d = 1;
+        FastDiv f = make_fastdiv(d);
+        if (fastdiv(n, f) != n / d || fastdiv(0xffffffffu, f) != 0xffffffffu / d)
+            return 2;
+    }
+    return 0;
+}
+
+const char *ddt_version(void) { return "ddt-hip 0.1 (gfx950)"; }
+
+const char *ddt_last_error(void) { return g_last_error.c_str(); }
+
+}  // extern "C"

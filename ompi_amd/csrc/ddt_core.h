@@ -1,0 +1,150 @@
+// ddt_core.h -- host-side type map, commit normalisation and device plan for the
+// MI355X derived-datatype engine.  Internal to libddt_hip.so.
+//
+// The type map is kept as a tree that mirrors the committed Open MPI description
+// (opal_datatype_internal.h:119-160): DATA entries (count blocks of blen bytes,
+// stride extent, first block at disp) and LOOP entries (loops iterations of a body,
+// stride extent).  A third node kind, LIST, is a compact run of single-block DATA
+// entries produced by the indexed constructors (the reference stores one 32-byte
+// DATA entry per block: 1 GiB of opt_desc for 64 M blocks).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "ddt_device.h"
+
+namespace ddt {
+
+enum : uint32_t {
+    F_PREDEFINED = 0x0002u,
+    F_COMMITTED = 0x0004u,
+    F_OVERLAP = 0x0008u,
+    F_CONTIGUOUS = 0x0010u,
+    F_NO_GAPS = 0x0020u,
+    F_USER_LB = 0x0040u,
+    F_USER_UB = 0x0080u,
+    F_DATA = 0x0100u,
+};
+
+// Element boundaries inside one block of a merged mixed-type DATA run: the element
+// start offsets within one period.  Null pattern = every multiple of esize.
+struct Pattern {
+    uint64_t period = 0;
+    std::vector<uint32_t> starts;  // sorted, starts[0] == 0
+};
+
+struct IndexList {
+    std::vector<int64_t> disp;   // byte displacement of each block (before Node::disp shift)
+    std::vector<uint64_t> len;   // bytes of each block; empty => all blocks are `ulen`
+    uint64_t ulen = 0;
+    int64_t esize = 1;
+    // derived at commit
+    std::vector<uint64_t> poff;  // packed offset of each block (variable lengths only)
+    uint64_t total = 0;          // packed bytes of the whole list
+    int64_t min_disp = 0, max_end = 0;
+    uint64_t disp_gcd = 0;       // gcd of all displacements (alignment of the gather side)
+    uint64_t len_gcd = 0;
+    size_t nblk() const { return disp.size(); }
+};
+
+struct Node {
+    enum Kind : uint8_t { DATA, LOOP, LIST } kind = DATA;
+    int64_t esize = 1;      // DATA/LIST: basic element size
+    uint64_t count = 1;     // DATA: blocks; LOOP: iterations
+    uint64_t blen = 0;      // DATA: bytes per block
+    int64_t extent = 0;     // DATA: block stride; LOOP: iteration stride
+    int64_t disp = 0;       // DATA: first block displacement; LIST: shift for every block
+    std::vector<Node> body; // LOOP
+    uint64_t body_size = 0; // LOOP: packed bytes per iteration (== END_LOOP size)
+    std::shared_ptr<const IndexList> list;  // LIST
+    std::shared_ptr<const Pattern> pat;     // DATA merged from mixed element sizes
+    uint64_t packed_bytes() const;
+};
+
+// One affine "leaf stream" of the plan: blocks of blen bytes whose source address is
+// src_off + sum_j idx_j*sstr_j and packed offset dst_off + sum_j idx_j*dstr_j, with
+// idx_j in [0, cnt_j).  dims are ordered outer -> inner; packed offsets are monotone
+// in the lexicographic order of idx (type-map order).
+struct LeafDim {
+    uint64_t cnt;
+    int64_t sstr;
+    int64_t dstr;
+};
+
+struct Leaf {
+    int kind = LEAF_AFFINE;       // LEAF_AFFINE or LEAF_LIST
+    uint64_t blen = 0;            // affine: bytes per block
+    int64_t src_off = 0;
+    int64_t dst_off = 0;
+    std::vector<LeafDim> dims;    // outer -> inner (without the instance dim)
+    std::shared_ptr<const IndexList> list;  // LEAF_LIST
+    int64_t list_shift = 0;
+    uint64_t bytes_per_iter = 0;  // packed bytes of the leaf per iteration of the dims (blen or list total)
+};
+
+struct DevList {                  // device copy of an IndexList
+    void *disp = nullptr;         // int32 or int64 per block (relative to min_disp when 32-bit)
+    uint32_t *len = nullptr;      // variable lengths
+    uint64_t *goff = nullptr;     // packed offset of every 64-block group (variable lengths)
+    bool disp32 = false;
+    int64_t disp_base = 0;
+};
+
+// Launch descriptors of one (count, buffers, windows) request, resident in HBM.
+// Repeated requests (the halo-exchange pattern: same type, same buffers every
+// iteration) reuse them with no host work and no upload.
+struct ItemSet {
+    std::vector<uint64_t> key;
+    std::vector<Item> items;
+    Item *d_items = nullptr;
+    uint32_t ntasks = 0;
+    hipEvent_t last_use = nullptr;
+    ~ItemSet();
+};
+
+struct Plan {
+    std::vector<Leaf> leaves;
+    std::vector<DevList> dev;     // one per LIST leaf (index in Leaf order, others empty)
+    uint64_t dev_bytes = 0;       // device metadata bytes
+    bool dev_ready = false;       // index lists uploaded
+    std::mutex mu;
+    std::vector<std::shared_ptr<ItemSet>> cache;   // most recent first
+    ~Plan();
+};
+
+}  // namespace ddt
+
+struct ddt_datatype {
+    uint16_t id = 0;              // predefined OPAL id, 0 for derived
+    uint32_t flags = ddt::F_CONTIGUOUS;
+    int64_t size = 0;
+    int64_t lb = INT64_MAX, ub = INT64_MIN;
+    int64_t true_lb = INT64_MAX, true_ub = INT64_MIN;
+    int64_t align = 1;
+    uint64_t nbElems = 0;
+    std::vector<ddt::Node> desc;  // type map (uncommitted form)
+    std::vector<ddt::Node> opt;   // committed + normalised form
+    std::vector<uint64_t> opt_prefix;  // packed offset of each top-level opt node
+    std::mutex plan_mu;
+    std::shared_ptr<ddt::Plan> plan;
+    int64_t extent() const { return ub - lb; }
+};
+
+namespace ddt {
+// typemap.cpp
+ddt_datatype *new_type();
+int commit(ddt_datatype *t);
+void normalize(std::vector<Node> &nodes);
+// Largest element boundary <= p (p in [0, count*size]) of the packed stream.
+uint64_t snap_down_to_element(const ddt_datatype *t, uint64_t p);
+// plan.cpp
+std::shared_ptr<Plan> get_plan(ddt_datatype *t);
+void ensure_device_lists(Plan &P);
+}  // namespace ddt

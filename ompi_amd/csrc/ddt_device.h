@@ -1,0 +1,85 @@
+// ddt_device.h -- launch descriptors shared by the host plan compiler and the
+// gfx950 kernels (ddt_kernels.hip).  Plain-old-data only.
+#pragma once
+
+#include <cstdint>
+
+#ifndef __HIPCC__
+#define DDT_HD inline
+#else
+#define DDT_HD __host__ __device__ inline
+#endif
+
+namespace ddt {
+
+constexpr int MAXD = 8;             // affine dims per item, instance dim included
+constexpr int THREADS = 256;        // workgroup size (4 wave64)
+
+enum LeafKind : int { LEAF_AFFINE = 0, LEAF_LIST = 1 };
+
+enum ItemKind : uint32_t {
+    ITEM_AFFINE = 0,    // units of U bytes over an affine nest
+    ITEM_LIST_UNI = 1,  // units of U bytes over an index list with one block length
+    ITEM_LIST_VAR = 2,  // one wave per 64-block group of a variable-length index list
+    ITEM_FRAG = 3,      // a sub-unit byte fragment at a window edge
+};
+
+// Exact unsigned 32-bit division by an invariant divisor d >= 1:
+//   l = ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1,
+//   n / d = (umulhi(n, m) + n) >> l      for every n < 2^32.
+struct FastDiv {
+    uint32_t d = 1, m = 1, l = 0, pad = 0;
+};
+
+DDT_HD FastDiv make_fastdiv(uint32_t d)
+{
+    FastDiv f;
+    f.d = d;
+    uint32_t l = 0;
+    while (l < 32 && (uint64_t(1) << l) < d) ++l;
+    f.l = l;
+    f.m = uint32_t(((uint64_t(1) << 32) * ((uint64_t(1) << l) - d)) / d + 1);
+    return f;
+}
+
+DDT_HD uint32_t fastdiv(uint32_t n, const FastDiv &f)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+    uint32_t hi = __umulhi(n, f.m);
+#else
+    uint32_t hi = uint32_t((uint64_t(n) * f.m) >> 32);
+#endif
+    return uint32_t((uint64_t(hi) + n) >> f.l);
+}
+
+struct Item {
+    uint32_t kind;
+    uint32_t U;             // unit bytes: 1, 2, 4, 8, 16
+    uint32_t ndim;          // dims in use (outer -> inner), instance dim first
+    uint32_t idx64;         // 1: total units >= 2^32, use 64-bit index arithmetic
+    uint64_t u0, u1;        // unit range [u0, u1) of this item
+    uint64_t units_per_task;
+    uint32_t task_begin;    // first workgroup of this item
+    uint32_t ntasks;
+    uint64_t upb;           // units per block (affine / list-uniform)
+    FastDiv fd_upb;
+    uint64_t user;          // user-side base address (uintptr)
+    uint64_t packed;        // packed-side base address (uintptr)
+    uint64_t cnt[MAXD];
+    FastDiv fd[MAXD];
+    int64_t ustr[MAXD];     // user-side stride per dim (bytes)
+    int64_t pstr[MAXD];     // packed-side stride per dim (bytes)
+    // index lists
+    uint64_t ldisp;         // device pointer: int32 or int64 displacement per block
+    uint64_t llen;          // device pointer: uint32 length per block (LIST_VAR)
+    uint64_t lgoff;         // device pointer: uint64 packed offset per 64-block group (LIST_VAR)
+    uint64_t nblk;          // blocks in the list
+    FastDiv fd_nblk;
+    uint64_t ulen;          // uniform block bytes (LIST_UNI)
+    uint32_t ldisp32;       // displacement array is int32
+    uint32_t leaf;          // plan leaf this item belongs to (diagnostics)
+    int64_t w0, w1;         // LIST_VAR / FRAG: window [w0, w1) in packed-stream coordinates
+    uint64_t nbytes;        // FRAG: bytes
+};
+
+}  // namespace ddt

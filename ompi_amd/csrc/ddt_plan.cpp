@@ -1,0 +1,487 @@
+// ddt_plan.cpp -- compiles a committed type map into device launch descriptors.
+//
+// A committed description (DATA / LOOP / LIST nodes, the engine's analogue of
+// opal_datatype_t::opt_desc) is flattened into "leaf streams": every DATA entry,
+// together with the LOOPs that enclose it, is an affine nest of blocks whose user
+// address and packed offset are both linear in the loop indices.  Leaves are
+// independent (their packed ranges interleave but never overlap), so a pack or an
+// unpack is ONE kernel launch over all leaves, with no descriptor walk on the host
+// per block -- the reference issues one cbmemcpy per block instead
+// (opal_datatype_accelerator_copy.h:51-75).
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+
+#include <hip/hip_runtime.h>
+
+#include "ddt_core.h"
+#include "ddt_plan.h"
+
+namespace ddt {
+
+Plan::~Plan()
+{
+    cache.clear();   // waits for the last launch that used each descriptor set
+    for (DevList &d : dev) {
+        if (d.disp) (void) hipFree(d.disp);
+        if (d.len) (void) hipFree(d.len);
+        if (d.goff) (void) hipFree(d.goff);
+    }
+}
+
+ItemSet::~ItemSet()
+{
+    if (last_use)
+        (void) hipEventSynchronize(last_use);
+    if (d_items)
+        (void) hipFree(d_items);
+    if (last_use)
+        (void) hipEventDestroy(last_use);
+}
+
+namespace {
+
+void collect(const std::vector<Node> &nodes, std::vector<LeafDim> &dims, int64_t pbase,
+             std::vector<Leaf> &out)
+{
+    int64_t p = pbase;
+    for (const Node &n : nodes) {
+        switch (n.kind) {
+        case Node::DATA: {
+            Leaf L;
+            L.kind = LEAF_AFFINE;
+            L.blen = n.blen;
+            L.src_off = n.disp;
+            L.dst_off = p;
+            L.dims = dims;
+            if (n.count > 1)
+                L.dims.push_back({n.count, n.extent, int64_t(n.blen)});
+            L.bytes_per_iter = n.count * n.blen;
+            if (n.blen > 0 && n.count > 0)
+                out.push_back(std::move(L));
+            p += int64_t(n.count * n.blen);
+            break;
+        }
+        case Node::LOOP:
+            dims.push_back({n.count, n.extent, int64_t(n.body_size)});
+            collect(n.body, dims, p, out);
+            dims.pop_back();
+            p += int64_t(n.count * n.body_size);
+            break;
+        case Node::LIST: {
+            Leaf L;
+            L.kind = LEAF_LIST;
+            L.list = n.list;
+            L.list_shift = n.disp;
+            L.dst_off = p;
+            L.dims = dims;
+            L.bytes_per_iter = n.list->total;
+            if (n.list->total > 0)
+                out.push_back(std::move(L));
+            p += int64_t(n.list->total);
+            break;
+        }
+        }
+    }
+}
+
+inline uint64_t lowbit(uint64_t x) { return x & (~x + 1); }
+
+uint32_t pick_unit(uint64_t g)
+{
+    // largest power of two <= 16 dividing every quantity folded into g (g == 0: all zero)
+    if (g == 0)
+        return 16;
+    uint64_t b = lowbit(g);
+    return uint32_t(b >= 16 ? 16 : b);
+}
+
+uint64_t absu(int64_t v) { return v < 0 ? uint64_t(-v) : uint64_t(v); }
+
+// Remove unit dims and fuse dims that are contiguous on both sides.
+void simplify(std::vector<LeafDim> &d, uint64_t *blen)
+{
+    std::vector<LeafDim> o;
+    for (const LeafDim &x : d)
+        if (x.cnt != 1)
+            o.push_back(x);
+    if (blen) {
+        while (!o.empty() && o.back().sstr == int64_t(*blen) && o.back().dstr == int64_t(*blen)) {
+            *blen *= o.back().cnt;
+            o.pop_back();
+        }
+    }
+    bool changed = true;
+    while (changed) {
+        changed = false;
+        for (size_t j = 0; j + 1 < o.size(); ++j) {
+            const LeafDim &a = o[j], &b = o[j + 1];
+            if (a.sstr == int64_t(b.cnt) * b.sstr && a.dstr == int64_t(b.cnt) * b.dstr) {
+                LeafDim m{a.cnt * b.cnt, b.sstr, b.dstr};
+                o.erase(o.begin() + long(j), o.begin() + long(j) + 2);
+                o.insert(o.begin() + long(j), m);
+                changed = true;
+                break;
+            }
+        }
+    }
+    d.swap(o);
+}
+
+}  // namespace
+
+std::shared_ptr<Plan> get_plan(ddt_datatype *t)
+{
+    std::lock_guard<std::mutex> g(t->plan_mu);
+    if (t->plan)
+        return t->plan;
+    auto P = std::make_shared<Plan>();
+    std::vector<LeafDim> dims;
+    collect(t->opt, dims, 0, P->leaves);
+    P->dev.resize(P->leaves.size());
+    for (size_t i = 0; i < P->leaves.size(); ++i) {
+        Leaf &L = P->leaves[i];
+        if (L.kind == LEAF_AFFINE) {
+            simplify(L.dims, &L.blen);
+            continue;
+        }
+        simplify(L.dims, nullptr);
+        const IndexList &X = *L.list;
+        DevList &D = P->dev[i];
+        int64_t span = X.max_end - X.min_disp;
+        D.disp32 = span < (int64_t(1) << 31);
+        D.disp_base = D.disp32 ? X.min_disp : 0;
+    }
+    t->plan = P;
+    return P;
+}
+
+// Upload the index lists of a plan to HBM (first execution only).
+void ensure_device_lists(Plan &P)
+{
+    std::lock_guard<std::mutex> g(P.mu);
+    if (P.dev_ready)
+        return;
+    for (size_t i = 0; i < P.leaves.size(); ++i) {
+        const Leaf &L = P.leaves[i];
+        if (L.kind != LEAF_LIST)
+            continue;
+        const IndexList &X = *L.list;
+        DevList &D = P.dev[i];
+        size_t n = X.nblk();
+        if (D.disp32) {
+            std::vector<int32_t> tmp(n);
+            for (size_t k = 0; k < n; ++k)
+                tmp[k] = int32_t(X.disp[k] - D.disp_base);
+            if (hipMalloc(&D.disp, n * 4) != hipSuccess)
+                throw std::runtime_error("hipMalloc(list disp)");
+            if (hipMemcpy(D.disp, tmp.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess)
+                throw std::runtime_error("hipMemcpy(list disp)");
+            P.dev_bytes += n * 4;
+        } else {
+            if (hipMalloc(&D.disp, n * 8) != hipSuccess)
+                throw std::runtime_error("hipMalloc(list disp)");
+            if (hipMemcpy(D.disp, X.disp.data(), n * 8, hipMemcpyHostToDevice) != hipSuccess)
+                throw std::runtime_error("hipMemcpy(list disp)");
+            P.dev_bytes += n * 8;
+        }
+        if (!X.len.empty()) {
+            std::vector<uint32_t> len(n);
+            for (size_t k = 0; k < n; ++k) {
+                if (X.len[k] > 0xffffffffull)
+                    throw std::runtime_error("list block > 4 GiB");
+                len[k] = uint32_t(X.len[k]);
+            }
+            size_t ng = (n + 63) / 64;
+            std::vector<uint64_t> goff(ng);
+            for (size_t gi = 0; gi < ng; ++gi)
+                goff[gi] = X.poff[gi * 64];
+            if (hipMalloc((void **) &D.len, n * 4) != hipSuccess
+                || hipMalloc((void **) &D.goff, ng * 8) != hipSuccess)
+                throw std::runtime_error("hipMalloc(list len)");
+            if (hipMemcpy(D.len, len.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess
+                || hipMemcpy(D.goff, goff.data(), ng * 8, hipMemcpyHostToDevice) != hipSuccess)
+                throw std::runtime_error("hipMemcpy(list len)");
+            P.dev_bytes += n * 4 + ng * 8;
+        }
+    }
+    P.dev_ready = true;
+}
+
+// ------------------------------------------------------------------ items for one call
+namespace {
+
+// Leaf bytes whose packed offset (relative to the leaf's nest origin) is < rel.
+uint64_t leaf_bytes_before(const std::vector<LeafDim> &dims, uint64_t inner, int64_t rel)
+{
+    if (rel <= 0)
+        return 0;
+    uint64_t acc = 0;
+    for (size_t j = 0; j < dims.size(); ++j) {
+        uint64_t per = inner;
+        for (size_t k = j + 1; k < dims.size(); ++k)
+            per *= dims[k].cnt;
+        uint64_t i = uint64_t(rel) / uint64_t(dims[j].dstr);
+        if (i >= dims[j].cnt)
+            return acc + dims[j].cnt * per;
+        acc += i * per;
+        rel -= int64_t(i) * dims[j].dstr;
+    }
+    return acc + std::min<uint64_t>(uint64_t(rel), inner);
+}
+
+// leaf-local byte offset x -> (user offset, packed offset) relative to the leaf origin
+void decompose(const std::vector<LeafDim> &dims, uint64_t inner, uint64_t x, int64_t *uoff,
+               int64_t *poff, uint64_t *r)
+{
+    uint64_t blk = x / inner;
+    *r = x % inner;
+    int64_t u = 0, p = 0;
+    for (size_t j = dims.size(); j-- > 0;) {
+        uint64_t idx = blk % dims[j].cnt;
+        blk /= dims[j].cnt;
+        u += int64_t(idx) * dims[j].sstr;
+        p += int64_t(idx) * dims[j].dstr;
+    }
+    *uoff = u;
+    *poff = p;
+}
+
+void fill_dims(Item &it, const std::vector<LeafDim> &dims)
+{
+    if (dims.size() > size_t(MAXD))
+        throw std::runtime_error("type nesting deeper than the engine's MAXD");
+    it.ndim = uint32_t(dims.size());
+    for (size_t j = 0; j < dims.size(); ++j) {
+        it.cnt[j] = dims[j].cnt;
+        it.fd[j] = make_fastdiv(dims[j].cnt < 0xffffffffull ? uint32_t(dims[j].cnt) : 1u);
+        it.ustr[j] = dims[j].sstr;
+        it.pstr[j] = dims[j].dstr;
+    }
+}
+
+uint64_t units_per_task(uint32_t U)
+{
+    return U >= 16 ? 2048 : (U == 8 ? 4096 : 8192);
+}
+
+void add_frag(std::vector<Item> &items, uint64_t user, uint64_t packed, uint64_t n)
+{
+    if (n == 0)
+        return;
+    Item f{};
+    f.kind = ITEM_FRAG;
+    f.U = 1;
+    f.user = user;
+    f.packed = packed;
+    f.nbytes = n;
+    f.u0 = 0;
+    f.u1 = 1;
+    f.units_per_task = 1;
+    items.push_back(f);
+}
+
+}  // namespace
+
+// Build the launch items moving the packed window [W0, W1) of `count` instances.
+// user = user buffer base; pk = packed pointer corresponding to W0.  same_layout: the
+// packed side uses the user-side layout (typed copy, opal_datatype_copy.c:141-178).
+void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t user, uint64_t pk,
+                 uint64_t W0, uint64_t W1, bool same_layout, std::vector<Item> &items)
+{
+    const LeafDim inst{count, t->extent(), t->size};
+    for (size_t li = 0; li < P.leaves.size(); ++li) {
+        const Leaf &L = P.leaves[li];
+        std::vector<LeafDim> dims;
+        dims.reserve(L.dims.size() + 1);
+        dims.push_back(inst);
+        dims.insert(dims.end(), L.dims.begin(), L.dims.end());
+        if (same_layout)
+            for (LeafDim &d : dims)
+                d.dstr = d.sstr;
+        const int64_t leaf_pk = int64_t(pk) - int64_t(W0) + (same_layout ? L.src_off : L.dst_off);
+        // window in leaf-local bytes (packed-stream order == type-map order)
+        uint64_t f0, f1;
+        if (same_layout) {
+            f0 = 0;   // typed copy always moves whole messages
+            uint64_t tot = L.bytes_per_iter;
+            for (const LeafDim &d : dims)
+                tot *= d.cnt;
+            f1 = tot;
+        } else {
+            std::vector<LeafDim> dd = dims;
+            uint64_t inner = L.kind == LEAF_AFFINE ? L.blen : L.list->total;
+            f0 = leaf_bytes_before(dd, inner, int64_t(W0) - L.dst_off);
+            f1 = leaf_bytes_before(dd, inner, int64_t(W1) - L.dst_off);
+        }
+        if (f1 <= f0)
+            continue;
+
+        if (L.kind == LEAF_AFFINE) {
+            uint64_t blen = L.blen;
+            std::vector<LeafDim> sd = dims;
+            simplify(sd, &blen);
+            uint64_t g = blen | absu(int64_t(user) + L.src_off) | absu(leaf_pk);
+            for (const LeafDim &d : sd)
+                g |= absu(d.sstr) | absu(d.dstr);
+            uint32_t U = pick_unit(g);
+            uint64_t u0 = (f0 + U - 1) / U, u1 = f1 / U;
+            auto frag_at = [&](uint64_t x, uint64_t n) {
+                int64_t uo, po;
+                uint64_t r;
+                decompose(sd, blen, x, &uo, &po, &r);
+                add_frag(items, uint64_t(int64_t(user) + L.src_off + uo + int64_t(r)),
+                         uint64_t(leaf_pk + po + int64_t(r)), n);
+            };
+            if (u0 >= u1) {
+                // the whole window lies inside one unit (or between two adjacent ones)
+                uint64_t x = f0;
+                while (x < f1) {   // split at block boundaries (<= 2 pieces)
+                    uint64_t end = std::min<uint64_t>(f1, (x / blen + 1) * blen);
+                    frag_at(x, end - x);
+                    x = end;
+                }
+                continue;
+            }
+            if (f0 < u0 * U)
+                frag_at(f0, u0 * U - f0);
+            if (u1 * U < f1)
+                frag_at(u1 * U, f1 - u1 * U);
+            Item it{};
+            it.kind = ITEM_AFFINE;
+            it.leaf = uint32_t(li);
+            it.U = U;
+            fill_dims(it, sd);
+            it.upb = blen / U;
+            it.fd_upb = make_fastdiv(it.upb < 0xffffffffull ? uint32_t(it.upb) : 1u);
+            uint64_t total_units = it.upb;
+            bool big = it.upb >= 0xffffffffull;
+            for (const LeafDim &d : sd) {
+                total_units *= d.cnt;
+                big = big || d.cnt >= 0xffffffffull;
+            }
+            it.idx64 = (big || total_units >= 0xffffffffull) ? 1 : 0;
+            it.u0 = u0;
+            it.u1 = u1;
+            it.units_per_task = units_per_task(U);
+            it.user = uint64_t(int64_t(user) + L.src_off);
+            it.packed = uint64_t(leaf_pk);
+            items.push_back(it);
+            continue;
+        }
+
+        // ---------------- LIST leaf
+        const IndexList &X = *L.list;
+        const DevList &D = P.dev[li];
+        std::vector<LeafDim> od = dims;
+        simplify(od, nullptr);
+        const uint64_t nb = X.nblk();
+        const int64_t ubase = int64_t(user) + L.list_shift;
+        if (X.len.empty()) {   // uniform block length
+            uint64_t g = X.ulen | X.disp_gcd | absu(ubase) | absu(leaf_pk);
+            for (const LeafDim &d : od)
+                g |= absu(d.sstr) | absu(d.dstr);
+            uint32_t U = pick_unit(g);
+            uint64_t u0 = (f0 + U - 1) / U, u1 = f1 / U;
+            auto frag_at = [&](uint64_t x, uint64_t n) {
+                int64_t uo, po;
+                uint64_t r;
+                decompose(od, X.total, x, &uo, &po, &r);
+                uint64_t blk = r / X.ulen, rr = r % X.ulen;
+                add_frag(items, uint64_t(ubase + uo + X.disp[blk] + int64_t(rr)),
+                         uint64_t(leaf_pk + po + int64_t(blk * X.ulen + rr)), n);
+            };
+            if (u0 >= u1) {
+                uint64_t x = f0;
+                while (x < f1) {
+                    uint64_t end = std::min<uint64_t>(f1, (x / X.ulen + 1) * X.ulen);
+                    frag_at(x, end - x);
+                    x = end;
+                }
+                continue;
+            }
+            if (f0 < u0 * U)
+                frag_at(f0, u0 * U - f0);
+            if (u1 * U < f1)
+                frag_at(u1 * U, f1 - u1 * U);
+            Item it{};
+            it.kind = ITEM_LIST_UNI;
+            it.leaf = uint32_t(li);
+            it.U = U;
+            fill_dims(it, od);
+            it.upb = X.ulen / U;
+            it.fd_upb = make_fastdiv(it.upb < 0xffffffffull ? uint32_t(it.upb) : 1u);
+            it.nblk = nb;
+            it.fd_nblk = make_fastdiv(nb < 0xffffffffull ? uint32_t(nb) : 1u);
+            uint64_t total_units = it.upb * nb;
+            for (const LeafDim &d : od)
+                total_units *= d.cnt;
+            it.idx64 = (total_units >= 0xffffffffull || it.upb >= 0xffffffffull) ? 1 : 0;
+            it.ulen = X.ulen;
+            it.ldisp = uint64_t(uintptr_t(D.disp));
+            it.ldisp32 = D.disp32 ? 1 : 0;
+            it.u0 = u0;
+            it.u1 = u1;
+            it.units_per_task = units_per_task(U);
+            it.user = uint64_t(ubase + D.disp_base);
+            it.packed = uint64_t(leaf_pk);
+            items.push_back(it);
+            continue;
+        }
+        // variable block lengths: unit = one 64-block group (one wave), lanes clip
+        uint64_t g = X.len_gcd | X.disp_gcd | absu(ubase) | absu(leaf_pk);
+        for (const LeafDim &d : od)
+            g |= absu(d.sstr) | absu(d.dstr);
+        const uint64_t ng = (nb + 63) / 64;
+        auto unit_of = [&](uint64_t x, bool upper) -> uint64_t {
+            uint64_t o = x / X.total, r = x % X.total;
+            if (upper && r == 0)
+                return o * ng;
+            uint64_t q = upper ? r - 1 : r;
+            auto itb = std::upper_bound(X.poff.begin(), X.poff.end(), q);
+            uint64_t blk = uint64_t(itb - X.poff.begin()) - 1;
+            return o * ng + blk / 64 + (upper ? 1 : 0);
+        };
+        Item it{};
+        it.kind = ITEM_LIST_VAR;
+        it.leaf = uint32_t(li);
+        it.U = pick_unit(g);
+        fill_dims(it, od);
+        it.nblk = nb;
+        it.upb = ng;   // groups per list
+        it.fd_upb = make_fastdiv(ng < 0xffffffffull ? uint32_t(ng) : 1u);
+        it.idx64 = 0;
+        it.ldisp = uint64_t(uintptr_t(D.disp));
+        it.ldisp32 = D.disp32 ? 1 : 0;
+        it.llen = uint64_t(uintptr_t(D.len));
+        it.lgoff = uint64_t(uintptr_t(D.goff));
+        it.ulen = X.total;   // packed bytes per list instance
+        it.u0 = unit_of(f0, false);
+        it.u1 = unit_of(f1, true);
+        it.units_per_task = 16;
+        it.user = uint64_t(ubase + D.disp_base);
+        it.packed = uint64_t(leaf_pk);
+        it.w0 = int64_t(f0);   // clip window in leaf-local packed bytes
+        it.w1 = int64_t(f1);
+        items.push_back(it);
+    }
+}
+
+void assign_tasks(std::vector<Item> &items)
+{
+    uint32_t tb = 0;
+    for (Item &it : items) {
+        uint64_t units = it.u1 - it.u0;
+        uint64_t nt = (units + it.units_per_task - 1) / it.units_per_task;
+        it.task_begin = tb;
+        it.ntasks = uint32_t(nt);
+        tb += uint32_t(nt);
+    }
+}
+
+uint32_t total_tasks(const std::vector<Item> &items)
+{
+    return items.empty() ? 0 : items.back().task_begin + items.back().ntasks;
+}
+
+}  // namespace ddt

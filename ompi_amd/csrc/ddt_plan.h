@@ -1,0 +1,22 @@
+// ddt_plan.h -- plan compiler and kernel launch interface (internal).
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "ddt_core.h"
+
+namespace ddt {
+
+void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t user, uint64_t pk,
+                 uint64_t W0, uint64_t W1, bool same_layout, std::vector<Item> &items);
+void assign_tasks(std::vector<Item> &items);
+uint32_t total_tasks(const std::vector<Item> &items);
+
+// ddt_kernels.hip: dir 0 = pack / typed copy (user side -> packed side), 1 = unpack.
+hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir,
+                       hipStream_t stream);
+
+}  // namespace ddt

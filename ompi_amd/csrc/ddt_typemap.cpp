@@ -1,0 +1,971 @@
+// ddt_typemap.cpp -- MPI derived-datatype construction and commit for the MI355X engine.
+//
+// Bounds, size and flag bookkeeping follow opal_datatype_add
+// (opal/datatype/opal_datatype_add.c:133-460); the constructors issue the same
+// sequence of adds as ompi/datatype/ompi_datatype_create_*.c, so lb/ub/extent,
+// true bounds and the type-map order are those of the reference.  The type-map
+// representation itself is the engine's own (ddt_core.h).
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+
+#include "ddt_core.h"
+#include "ddt_hip.h"
+
+using namespace ddt;
+
+namespace {
+
+// LP64 x86-64 sizes of opal_datatype_local_sizes (opal_datatype_module.c:143-180),
+// natural alignment (opal_datatype_constructors.h:87-96).
+const int64_t kSize[29] = {0, 0, 0, 0, 1, 2, 4, 8, 16, 1, 2, 4, 8, 16, 2,
+                           4, 8, 16, 16, 4, 8, 16, 32, 1, 4, 8, 8, 32, 0};
+const int64_t kAlign[29] = {0, 0, 0, 0, 1, 2, 4, 8, 16, 1, 2, 4, 8, 16, 2,
+                            4, 8, 16, 16, 2, 4, 8, 16, 1, 4, 8, 8, 16, 0};
+
+constexpr size_t kListMin = 8;       // indexed runs longer than this become LIST nodes
+constexpr size_t kPatternMax = 256;  // max element starts kept for a merged mixed block
+
+ddt_datatype g_predef[29];
+std::once_flag g_predef_once;
+
+void init_predefined()
+{
+    for (int id = 4; id <= 27; ++id) {
+        ddt_datatype &t = g_predef[id];
+        t.id = uint16_t(id);
+        t.size = kSize[id];
+        t.lb = 0;
+        t.ub = kSize[id];
+        t.true_lb = 0;
+        t.true_ub = kSize[id];
+        t.align = kAlign[id];
+        t.nbElems = 1;
+        t.flags = F_PREDEFINED | F_CONTIGUOUS | F_NO_GAPS | F_DATA | F_COMMITTED;
+        Node n;
+        n.kind = Node::DATA;
+        n.esize = kSize[id];
+        n.count = 1;
+        n.blen = uint64_t(kSize[id]);
+        n.extent = kSize[id];
+        n.disp = 0;
+        t.desc.push_back(n);
+        t.opt = t.desc;
+        t.opt_prefix = {0, uint64_t(kSize[id])};
+    }
+}
+
+void shift_nodes(std::vector<Node> &nodes, int64_t d)
+{
+    for (Node &n : nodes) {
+        if (n.kind == Node::LOOP)
+            shift_nodes(n.body, d);
+        else
+            n.disp += d;
+    }
+}
+
+bool is_predefined(const ddt_datatype *t) { return (t->flags & F_PREDEFINED) && t->id != 0; }
+
+// Bounds / size / flags of opal_datatype_add (opal_datatype_add.c:133-460).  Returns the
+// previous true_ub (for the contiguity test) or sets *skip when nothing is appended.
+struct AddState {
+    int64_t old_true_ub;
+    bool skip;
+};
+
+// opal_datatype_add treats an extent of -1 as "use the added type's ub - lb"
+// (opal_datatype_add.c:156-161), including when a constructor computed -1 from a
+// negative stride; reproduced so bounds and type map match the reference.
+inline int64_t effective_extent(const ddt_datatype *add, int64_t extent)
+{
+    return extent == -1 ? add->ub - add->lb : extent;
+}
+
+AddState add_bounds(ddt_datatype *base, const ddt_datatype *add, uint64_t count, int64_t disp,
+                    int64_t extent)
+{
+    AddState st{0, true};
+    if (count == 0)
+        return st;
+    extent = effective_extent(add, extent);
+    int64_t lb, ub;
+    {   // OPAL_DATATYPE_LB_UB_CONT (:98-116)
+        int64_t upper = disp + extent * int64_t(count - 1), lower = disp;
+        if (lower < upper) {
+            lb = lower;
+            ub = upper;
+        } else {
+            lb = upper;
+            ub = lower;
+        }
+        lb += add->lb;
+        ub += add->ub;
+    }
+    int64_t true_lb = lb - (add->lb - add->true_lb);
+    int64_t true_ub = ub - (add->ub - add->true_ub);
+    if (true_lb > true_ub)
+        std::swap(true_lb, true_ub);
+    if ((add->flags ^ base->flags) & F_USER_LB) {
+        if (base->flags & F_USER_LB)
+            lb = base->lb;
+        base->flags |= F_USER_LB;
+    } else {
+        lb = std::min(base->lb, lb);
+    }
+    if ((base->flags ^ add->flags) & F_USER_UB) {
+        if (base->flags & F_USER_UB)
+            ub = base->ub;
+        base->flags |= F_USER_UB;
+    } else {
+        ub = std::max(base->ub, ub);
+    }
+    base->lb = lb;
+    base->ub = ub;
+    base->align = std::max(base->align, add->align);
+    if (!(base->flags & F_USER_UB)) {
+        int64_t eps = (base->ub - base->lb) % base->align;  // C remainder, as the reference
+        if (eps != 0)
+            base->ub += base->align - eps;
+    }
+    base->flags |= F_DATA;
+    if (add->size == 0)
+        return st;
+    base->size += int64_t(count) * add->size;
+    st.old_true_ub = (base->nbElems == 0) ? disp : base->true_ub;
+    base->true_lb = std::min(true_lb, base->true_lb);
+    base->true_ub = std::max(true_ub, base->true_ub);
+    if (!is_predefined(add)) {
+        base->flags |= (add->flags & F_USER_LB);
+        base->flags |= (add->flags & F_USER_UB);
+    }
+    st.skip = false;
+    return st;
+}
+
+void add_finish(ddt_datatype *base, const ddt_datatype *add, uint64_t count, int64_t disp,
+                int64_t extent, const AddState &st)
+{
+    extent = effective_extent(add, extent);
+    uint32_t local = base->flags & add->flags;
+    base->flags &= ~(F_CONTIGUOUS | F_NO_GAPS);
+    if ((local & F_CONTIGUOUS) && (disp + add->true_lb) == st.old_true_ub
+        && (add->size == extent || count < 2)) {
+        base->flags |= F_CONTIGUOUS;
+        if (base->size == base->ub - base->lb)
+            base->flags |= F_NO_GAPS;
+    }
+    base->nbElems += count * add->nbElems;
+}
+
+// opal_datatype_add: bounds + append of `count` replicas of `add` at disp + i*extent.
+void type_add(ddt_datatype *base, const ddt_datatype *add, uint64_t count, int64_t disp,
+              int64_t extent)
+{
+    extent = effective_extent(add, extent);
+    AddState st = add_bounds(base, add, count, disp, extent);
+    if (st.skip)
+        return;
+    if (is_predefined(add)) {   // predefined branch (:319-345)
+        Node n;
+        n.kind = Node::DATA;
+        n.esize = add->size;
+        n.disp = disp;
+        if (extent == add->size) {
+            n.count = 1;
+            n.blen = count * uint64_t(add->size);
+            n.extent = int64_t(n.blen);
+        } else {
+            n.count = count;
+            n.blen = uint64_t(add->size);
+            n.extent = extent;
+        }
+        base->desc.push_back(std::move(n));
+    } else {
+        std::vector<Node> sub = add->desc;
+        shift_nodes(sub, disp);
+        bool done = false;
+        if (sub.size() == 1 && sub[0].kind == Node::DATA) {   // single DATA entry (:361-397)
+            Node e = sub[0];
+            if (count == 1) {
+                base->desc.push_back(e);
+                done = true;
+            } else if (e.count == 1) {
+                if (int64_t(e.blen) == extent) {
+                    e.blen *= count;
+                    e.extent = int64_t(e.blen);
+                } else {
+                    e.count = count;
+                    e.extent = extent;
+                }
+                base->desc.push_back(e);
+                done = true;
+            } else if (extent == int64_t(e.count) * e.extent && e.count * count < (1ull << 40)) {
+                e.count *= count;
+                base->desc.push_back(e);
+                done = true;
+            }
+        }
+        if (!done) {   // build_loop (:400-431)
+            if (count == 1) {
+                for (Node &n : sub)
+                    base->desc.push_back(std::move(n));
+            } else {
+                Node l;
+                l.kind = Node::LOOP;
+                l.count = count;
+                l.extent = extent;
+                l.body = std::move(sub);
+                l.body_size = uint64_t(add->size);
+                base->desc.push_back(std::move(l));
+            }
+        }
+    }
+    add_finish(base, add, count, disp, extent, st);
+}
+
+ddt_datatype *make_empty()
+{
+    // opal_datatype_empty (opal_datatype_constructors.h:67-75) via ompi_datatype_duplicate
+    ddt_datatype *t = new_type();
+    t->lb = t->ub = t->true_lb = t->true_ub = 0;
+    t->align = 1;
+    t->nbElems = 1;
+    t->flags = F_CONTIGUOUS | F_NO_GAPS;
+    return t;
+}
+
+ddt_datatype *clone_type(const ddt_datatype *o)
+{
+    // opal_datatype_clone (opal_datatype_clone.c:35-80): copy everything, drop PREDEFINED
+    ddt_datatype *t = new_type();
+    t->id = 0;
+    t->flags = o->flags & ~(F_PREDEFINED | F_COMMITTED);
+    t->size = o->size;
+    t->lb = o->lb;
+    t->ub = o->ub;
+    t->true_lb = o->true_lb;
+    t->true_ub = o->true_ub;
+    t->align = o->align;
+    t->nbElems = o->nbElems;
+    t->desc = o->desc;
+    return t;
+}
+
+// Can `old` be replicated as a single contiguous block of its own size (LIST element)?
+bool simple_block(const ddt_datatype *old)
+{
+    return old->size > 0 && old->desc.size() == 1 && old->desc[0].kind == Node::DATA
+           && old->desc[0].count == 1 && int64_t(old->desc[0].blen) == old->size
+           && old->extent() == old->size && old->desc[0].disp == 0 && !old->desc[0].pat;
+}
+
+uint64_t gcd64(uint64_t a, uint64_t b) { return b ? gcd64(b, a % b) : a; }
+
+std::shared_ptr<IndexList> finish_list(std::shared_ptr<IndexList> L)
+{
+    size_t n = L->disp.size();
+    L->min_disp = INT64_MAX;
+    L->max_end = INT64_MIN;
+    uint64_t g = 0, gl = 0, acc = 0;
+    if (!L->len.empty()) {
+        L->poff.resize(n);
+        for (size_t i = 0; i < n; ++i) {
+            L->poff[i] = acc;
+            acc += L->len[i];
+            gl = gcd64(gl, L->len[i]);
+            L->min_disp = std::min(L->min_disp, L->disp[i]);
+            L->max_end = std::max(L->max_end, L->disp[i] + int64_t(L->len[i]));
+            g = gcd64(g, uint64_t(L->disp[i] < 0 ? -L->disp[i] : L->disp[i]));
+        }
+        // all equal lengths -> uniform list
+        if (n > 0 && gl == L->len[0]) {
+            bool uni = true;
+            for (size_t i = 1; i < n && uni; ++i)
+                uni = L->len[i] == L->len[0];
+            if (uni) {
+                L->ulen = L->len[0];
+                L->len.clear();
+                L->poff.clear();
+            }
+        }
+    } else {
+        acc = L->ulen * n;
+        gl = L->ulen;
+        for (size_t i = 0; i < n; ++i) {
+            L->min_disp = std::min(L->min_disp, L->disp[i]);
+            L->max_end = std::max(L->max_end, L->disp[i] + int64_t(L->ulen));
+            g = gcd64(g, uint64_t(L->disp[i] < 0 ? -L->disp[i] : L->disp[i]));
+        }
+    }
+    L->total = acc;
+    L->disp_gcd = g ? g : 0;
+    L->len_gcd = gl;
+    return L;
+}
+
+// Shared driver of the four indexed constructors (ompi_datatype_create_indexed.c:35-183):
+// merges blocks that abut in type-map order, then either emits per-block adds or, for
+// long runs of a simple element type, one LIST node with the identical bounds.
+struct Block {
+    int64_t disp_bytes;
+    uint64_t nelem;
+};
+
+ddt_datatype *build_indexed(const std::vector<Block> &blocks, const ddt_datatype *old)
+{
+    ddt_datatype *t = new_type();
+    int64_t extent = old->extent();
+    if (blocks.size() > kListMin && simple_block(old)) {
+        auto L = std::make_shared<IndexList>();
+        L->esize = old->desc[0].esize;
+        L->disp.reserve(blocks.size());
+        L->len.reserve(blocks.size());
+        for (const Block &b : blocks) {
+            AddState st = add_bounds(t, old, b.nelem, b.disp_bytes, extent);
+            if (!st.skip) {
+                L->disp.push_back(b.disp_bytes);
+                L->len.push_back(b.nelem * uint64_t(old->size));
+                add_finish(t, old, b.nelem, b.disp_bytes, extent, st);
+            }
+        }
+        Node n;
+        n.kind = Node::LIST;
+        n.esize = L->esize;
+        n.list = finish_list(L);
+        t->desc.push_back(std::move(n));
+    } else {
+        for (const Block &b : blocks)
+            type_add(t, old, b.nelem, b.disp_bytes, extent);
+    }
+    return t;
+}
+
+}  // namespace
+
+namespace ddt {
+
+uint64_t Node::packed_bytes() const
+{
+    switch (kind) {
+    case DATA: return count * blen;
+    case LOOP: return count * body_size;
+    case LIST: return list ? list->total : 0;
+    }
+    return 0;
+}
+
+ddt_datatype *new_type() { return new ddt_datatype(); }
+
+// ---------------------------------------------------------------- commit normalisation
+namespace {
+
+bool element_starts(const Node &n, std::vector<uint32_t> &out)
+{
+    // element start offsets of one block of DATA node n
+    if (n.blen > 0xffffffffull)
+        return false;
+    if (n.pat) {
+        uint64_t P = n.pat->period;
+        for (uint64_t k = 0; k < n.blen; k += P)
+            for (uint32_t s : n.pat->starts) {
+                if (out.size() >= kPatternMax)
+                    return false;
+                out.push_back(uint32_t(k + s));
+            }
+    } else {
+        for (uint64_t s = 0; s < n.blen; s += uint64_t(n.esize)) {
+            if (out.size() >= kPatternMax)
+                return false;
+            out.push_back(uint32_t(s));
+        }
+    }
+    return true;
+}
+
+// Try to merge DATA b (count 1) onto the end of DATA a (count 1): contiguous in memory and
+// therefore in the packed stream.
+bool try_merge(Node &a, const Node &b)
+{
+    if (a.kind != Node::DATA || b.kind != Node::DATA || a.count != 1 || b.count != 1)
+        return false;
+    if (a.disp + int64_t(a.blen) != b.disp)
+        return false;
+    if (!a.pat && !b.pat && a.esize == b.esize) {
+        a.blen += b.blen;
+        a.extent = int64_t(a.blen);
+        return true;
+    }
+    std::vector<uint32_t> sa, sb;
+    if (!element_starts(a, sa) || !element_starts(b, sb) || sa.size() + sb.size() > kPatternMax)
+        return false;
+    auto p = std::make_shared<Pattern>();
+    p->period = a.blen + b.blen;
+    p->starts = sa;
+    for (uint32_t s : sb)
+        p->starts.push_back(uint32_t(s + a.blen));
+    a.blen += b.blen;
+    a.extent = int64_t(a.blen);
+    a.esize = std::min(a.esize, b.esize);
+    a.pat = p;
+    return true;
+}
+
+void push_merge(std::vector<Node> &out, Node &&n)
+{
+    if (n.kind == Node::DATA && n.count > 1 && n.extent == int64_t(n.blen)) {
+        n.blen *= n.count;
+        n.count = 1;
+        n.extent = int64_t(n.blen);
+    }
+    if (n.kind == Node::DATA && n.count * n.blen == 0)
+        return;
+    if (!out.empty() && try_merge(out.back(), n))
+        return;
+    out.push_back(std::move(n));
+}
+
+}  // namespace
+
+void normalize(std::vector<Node> &nodes)
+{
+    std::vector<Node> out;
+    out.reserve(nodes.size());
+    for (Node &n : nodes) {
+        if (n.kind == Node::LOOP) {
+            normalize(n.body);
+            if (n.body.empty() || n.count == 0 || n.body_size == 0)
+                continue;
+            if (n.count == 1) {
+                for (Node &c : n.body)
+                    push_merge(out, std::move(c));
+                continue;
+            }
+            if (n.body.size() == 1 && n.body[0].kind == Node::DATA) {
+                Node e = n.body[0];
+                if (e.count == 1) {
+                    if (int64_t(e.blen) == n.extent) {
+                        // contiguous iterations: one block; a pattern keeps its period
+                        e.blen *= n.count;
+                        e.extent = int64_t(e.blen);
+                    } else {
+                        e.count = n.count;
+                        e.extent = n.extent;
+                    }
+                    push_merge(out, std::move(e));
+                    continue;
+                } else if (n.extent == int64_t(e.count) * e.extent) {
+                    e.count *= n.count;
+                    push_merge(out, std::move(e));
+                    continue;
+                }
+            }
+            out.push_back(std::move(n));
+        } else if (n.kind == Node::DATA) {
+            push_merge(out, std::move(n));
+        } else {
+            if (n.list && n.list->total > 0)
+                out.push_back(std::move(n));
+        }
+    }
+    nodes.swap(out);
+}
+
+int commit(ddt_datatype *t)
+{
+    if (t->flags & F_COMMITTED)
+        return DDT_SUCCESS;
+    t->opt = t->desc;
+    normalize(t->opt);
+    t->opt_prefix.assign(1, 0);
+    for (const Node &n : t->opt)
+        t->opt_prefix.push_back(t->opt_prefix.back() + n.packed_bytes());
+    t->flags |= F_COMMITTED;
+    return DDT_SUCCESS;
+}
+
+namespace {
+uint64_t snap_in_node(const Node &n, uint64_t off)
+{
+    switch (n.kind) {
+    case Node::DATA: {
+        uint64_t blk = off / n.blen, r = off % n.blen;
+        uint64_t s;
+        if (n.pat) {
+            uint64_t P = n.pat->period, k = r / P, rr = r % P;
+            auto it = std::upper_bound(n.pat->starts.begin(), n.pat->starts.end(), uint32_t(rr));
+            s = k * P + *(it - 1);
+        } else {
+            s = (r / uint64_t(n.esize)) * uint64_t(n.esize);
+        }
+        return blk * n.blen + s;
+    }
+    case Node::LOOP: {
+        uint64_t it = off / n.body_size, r = off % n.body_size, acc = 0;
+        for (const Node &c : n.body) {
+            uint64_t b = c.packed_bytes();
+            if (r < acc + b)
+                return it * n.body_size + acc + snap_in_node(c, r - acc);
+            acc += b;
+        }
+        return it * n.body_size + acc;
+    }
+    case Node::LIST: {
+        const IndexList &L = *n.list;
+        uint64_t e = uint64_t(L.esize);
+        if (L.len.empty()) {
+            uint64_t blk = off / L.ulen, r = off % L.ulen;
+            return blk * L.ulen + (r / e) * e;
+        }
+        auto it = std::upper_bound(L.poff.begin(), L.poff.end(), off);
+        uint64_t start = *(it - 1);
+        return start + ((off - start) / e) * e;
+    }
+    }
+    return off;
+}
+}  // namespace
+
+uint64_t snap_down_to_element(const ddt_datatype *t, uint64_t p)
+{
+    if (t->size <= 0)
+        return p;
+    uint64_t size = uint64_t(t->size), inst = p / size, q = p % size;
+    if (q == 0)
+        return p;
+    auto it = std::upper_bound(t->opt_prefix.begin(), t->opt_prefix.end(), q);
+    size_t idx = size_t(it - t->opt_prefix.begin()) - 1;
+    if (idx >= t->opt.size())
+        return p;
+    return inst * size + t->opt_prefix[idx] + snap_in_node(t->opt[idx], q - t->opt_prefix[idx]);
+}
+
+}  // namespace ddt
+
+// ================================================================ C ABI: construction
+extern "C" {
+
+const ddt_datatype_t *ddt_predefined(int id)
+{
+    std::call_once(g_predef_once, init_predefined);
+    if (id < 4 || id > 27)
+        return nullptr;
+    return &g_predef[id];
+}
+
+int ddt_type_create_contiguous(size_t count, const ddt_datatype_t *old, ddt_datatype_t **out)
+{
+    if (!old || !out)
+        return DDT_ERR_BAD_PARAM;
+    if (count == 0 || old->size == 0) {
+        *out = make_empty();
+        return DDT_SUCCESS;
+    }
+    ddt_datatype *t = new_type();
+    type_add(t, old, count, 0, old->extent());
+    *out = t;
+    return DDT_SUCCESS;
+}
+
+int ddt_type_create_vector(size_t count, size_t blen, ptrdiff_t stride, const ddt_datatype_t *old,
+                           ddt_datatype_t **out)
+{
+    // ompi_datatype_create_vector (ompi_datatype_create_vector.c:32-58)
+    if (!old || !out)
+        return DDT_ERR_BAD_PARAM;
+    int64_t extent = old->extent();
+    if (count == 0 || blen == 0) {
+        *out = make_empty();
+        return DDT_SUCCESS;
+    }
+    ddt_datatype *t = new_type();
+    if (int64_t(blen) == stride || count <= 1) {
+        type_add(t, old, count * blen, 0, extent);
+    } else if (blen == 1) {
+        type_add(t, old, count, 0, extent * stride);
+    } else {
+        type_add(t, old, blen, 0, extent);
+        ddt_datatype *t2 = new_type();
+        type_add(t2, t, count, 0, extent * stride);
+        delete t;
+        t = t2;
+    }
+    *out = t;
+    return DDT_SUCCESS;
+}
+
+int ddt_type_create_hvector(size_t count, size_t blen, ptrdiff_t stride, const ddt_datatype_t *old,
+                            ddt_datatype_t **out)
+{
+    // ompi_datatype_create_hvector (ompi_datatype_create_vector.c:61-88)
+    if (!old || !out)
+        return DDT_ERR_BAD_PARAM;
+    int64_t extent = old->extent();
+    if (count == 0 || blen == 0) {
+        *out = make_empty();
+        return DDT_SUCCESS;
+    }
+    ddt_datatype *t = new_type();
+    if (extent * int64_t(blen) == stride || count <= 1) {
+        type_add(t, old, count * blen, 0, extent);
+    } else if (blen == 1) {
+        type_add(t, old, count, 0, stride);
+    } else {
+        type_add(t, old, blen, 0, extent);
+        ddt_datatype *t2 = new_type();
+        type_add(t2, t, count, 0, stride);
+        delete t;
+        t = t2;
+    }
+    *out = t;
+    return DDT_SUCCESS;
+}
+
+static int indexed_common(size_t count, const size_t *blens, const ptrdiff_t *disps, size_t ublen,
+                          bool uniform, bool bytes, const ddt_datatype_t *old, ddt_datatype_t **out)
+{
+    if (!old || !out || (count && !disps) || (!uniform && count && !blens))
+        return DDT_ERR_BAD_PARAM;
+    int64_t extent = old->extent();
+    size_t i = 0;
+    if (!uniform) {
+        for (; i < count && blens[i] == 0; ++i)
+            ;
+        if (i == count || old->size == 0) {
+            *out = make_empty();
+            return DDT_SUCCESS;
+        }
+    } else if (count == 0 || ublen == 0) {
+        *out = make_empty();
+        return DDT_SUCCESS;
+    }
+    auto bl = [&](size_t k) { return uniform ? ublen : blens[k]; };
+    std::vector<Block> blocks;
+    blocks.reserve(count - i);
+    int64_t disp = disps[i];
+    uint64_t dlen = bl(i);
+    int64_t endat = bytes ? disp + int64_t(dlen) * extent : disp + int64_t(dlen);
+    for (i += 1; i < count; ++i) {
+        if (bl(i) == 0)
+            continue;
+        if (endat == disps[i]) {
+            dlen += bl(i);
+            endat += bytes ? int64_t(bl(i)) * extent : int64_t(bl(i));
+        } else {
+            blocks.push_back({bytes ? disp : disp * extent, dlen});
+            disp = disps[i];
+            dlen = bl(i);
+            endat = bytes ? disp + int64_t(dlen) * extent : disp + int64_t(dlen);
+        }
+    }
+    blocks.push_back({bytes ? disp : disp * extent, dlen});
+    *out = build_indexed(blocks, old);
+    return DDT_SUCCESS;
+}
+
+int ddt_type_create_indexed(size_t count, const size_t *blens, const ptrdiff_t *disps,
+                            const ddt_datatype_t *old, ddt_datatype_t **out)
+{
+    return indexed_common(count, blens, disps, 0, false, false, old, out);
+}
+
+int ddt_type_create_hindexed(size_t count, const size_t *blens, const ptrdiff_t *disps,
+                             const ddt_datatype_t *old, ddt_datatype_t **out)
+{
+    return indexed_common(count, blens, disps, 0, false, true, old, out);
+}
+
+int ddt_type_create_indexed_block(size_t count, size_t blen, const ptrdiff_t *disps,
+                                  const ddt_datatype_t *old, ddt_datatype_t **out)
+{
+    return indexed_common(count, nullptr, disps, blen, true, false, old, out);
+}
+
+int ddt_type_create_hindexed_block(size_t count, size_t blen, const ptrdiff_t *disps,
+                                   const ddt_datatype_t *old, ddt_datatype_t **out)
+{
+    return indexed_common(count, nullptr, disps, blen, true, true, old, out);
+}
+
+int ddt_type_create_struct(size_t count, const size_t *blens, const ptrdiff_t *disps,
+                           const ddt_datatype_t *const *types, ddt_datatype_t **out)
+{
+    // ompi_datatype_create_struct (ompi_datatype_create_struct.c:32-98)
+    if (!out || (count && (!blens || !disps || !types)))
+        return DDT_ERR_BAD_PARAM;
+    size_t i = 0;
+    for (; i < count && blens[i] == 0; ++i)
+        ;
+    if (i == count) {
+        *out = make_empty();
+        return DDT_SUCCESS;
+    }
+    for (size_t k = i; k < count; ++k)
+        if (!types[k])
+            return DDT_ERR_BAD_PARAM;
+    const ddt_datatype *lastType = types[i];
+    uint64_t lastBlock = blens[i];
+    int64_t lastExtent = lastType->extent();
+    int64_t lastDisp = disps[i];
+    int64_t endto = lastDisp + lastExtent * int64_t(lastBlock);
+    ddt_datatype *t = new_type();
+    for (i += 1; i < count; ++i) {
+        if (types[i] == lastType && disps[i] == endto) {
+            lastBlock += blens[i];
+            endto = lastDisp + int64_t(lastBlock) * lastExtent;
+        } else {
+            type_add(t, lastType, lastBlock, lastDisp, lastExtent);
+            lastType = types[i];
+            lastExtent = lastType->extent();
+            lastBlock = blens[i];
+            lastDisp = disps[i];
+            endto = lastDisp + lastExtent * int64_t(lastBlock);
+        }
+    }
+    type_add(t, lastType, lastBlock, lastDisp, lastExtent);
+    *out = t;
+    return DDT_SUCCESS;
+}
+
+static void resize_in_place(ddt_datatype *t, int64_t lb, int64_t extent)
+{
+    // opal_datatype_resize (opal_datatype_resize.c:23-41)
+    t->lb = lb;
+    t->ub = lb + extent;
+    t->flags &= ~F_NO_GAPS;
+    t->flags |= F_USER_LB | F_USER_UB;
+    if (extent == t->size && (t->flags & F_CONTIGUOUS))
+        t->flags |= F_NO_GAPS;
+}
+
+int ddt_type_create_resized(const ddt_datatype_t *old, ptrdiff_t lb, ptrdiff_t extent,
+                            ddt_datatype_t **out)
+{
+    if (!old || !out)
+        return DDT_ERR_BAD_PARAM;
+    ddt_datatype *t = clone_type(old);
+    resize_in_place(t, lb, extent);
+    *out = t;
+    return DDT_SUCCESS;
+}
+
+int ddt_type_dup(const ddt_datatype_t *old, ddt_datatype_t **out)
+{
+    if (!old || !out)
+        return DDT_ERR_BAD_PARAM;
+    *out = clone_type(old);
+    return DDT_SUCCESS;
+}
+
+int ddt_type_create_subarray(int ndims, const size_t *sizes, const size_t *subsizes,
+                             const size_t *starts, int order, const ddt_datatype_t *old,
+                             ddt_datatype_t **out)
+{
+    // ompi_datatype_create_subarray (ompi_datatype_create_subarray.c:32-112)
+    if (!old || !out || ndims < 0 || (ndims > 0 && (!sizes || !subsizes || !starts)))
+        return DDT_ERR_BAD_PARAM;
+    int64_t extent = old->extent(), size, displ;
+    ddt_datatype_t *last = nullptr, *nt = nullptr;
+    if (ndims < 2) {
+        if (ndims == 0) {
+            *out = make_empty();
+            return DDT_SUCCESS;
+        }
+        ddt_type_create_contiguous(subsizes[0], old, &last);
+        size = int64_t(sizes[0]);
+        displ = int64_t(starts[0]);
+    } else {
+        int i, step, end_loop;
+        if (order == DDT_ORDER_C) {
+            i = ndims - 1;
+            step = -1;
+            end_loop = -1;
+        } else {
+            i = 0;
+            step = 1;
+            end_loop = ndims;
+        }
+        ddt_type_create_vector(subsizes[i + step], subsizes[i], ptrdiff_t(sizes[i]), old, &last);
+        size = int64_t(sizes[i]) * int64_t(sizes[i + step]);
+        displ = int64_t(starts[i]) + int64_t(starts[i + step]) * int64_t(sizes[i]);
+        for (i += 2 * step; i != end_loop; i += step) {
+            ddt_type_create_hvector(subsizes[i], 1, size * extent, last, &nt);
+            delete last;
+            displ += size * int64_t(starts[i]);
+            size *= int64_t(sizes[i]);
+            last = nt;
+        }
+    }
+    nt = new_type();
+    type_add(nt, last, 1, displ * extent, size * extent);
+    delete last;
+    resize_in_place(nt, 0, size * extent);
+    *out = nt;
+    return DDT_SUCCESS;
+}
+
+int ddt_type_commit(ddt_datatype_t *t)
+{
+    if (!t)
+        return DDT_ERR_BAD_PARAM;
+    return commit(t);
+}
+
+int ddt_type_destroy(ddt_datatype_t **t)
+{
+    if (!t || !*t)
+        return DDT_ERR_BAD_PARAM;
+    if (is_predefined(*t)) {
+        *t = nullptr;
+        return DDT_SUCCESS;
+    }
+    delete *t;
+    *t = nullptr;
+    return DDT_SUCCESS;
+}
+
+int ddt_type_size(const ddt_datatype_t *t, size_t *size)
+{
+    if (!t || !size)
+        return DDT_ERR_BAD_PARAM;
+    *size = size_t(t->size);
+    return DDT_SUCCESS;
+}
+
+int ddt_type_get_extent(const ddt_datatype_t *t, ptrdiff_t *lb, ptrdiff_t *extent)
+{
+    if (!t)
+        return DDT_ERR_BAD_PARAM;
+    if (lb)
+        *lb = t->lb;
+    if (extent)
+        *extent = t->ub - t->lb;
+    return DDT_SUCCESS;
+}
+
+int ddt_type_get_true_extent(const ddt_datatype_t *t, ptrdiff_t *true_lb, ptrdiff_t *true_extent)
+{
+    if (!t)
+        return DDT_ERR_BAD_PARAM;
+    if (true_lb)
+        *true_lb = t->true_lb;
+    if (true_extent)
+        *true_extent = t->true_ub - t->true_lb;
+    return DDT_SUCCESS;
+}
+
+uint32_t ddt_type_flags(const ddt_datatype_t *t) { return t ? t->flags : 0; }
+
+int ddt_type_info(const ddt_datatype_t *t, int64_t *o)
+{
+    if (!t || !o)
+        return DDT_ERR_BAD_PARAM;
+    o[0] = t->size;
+    o[1] = t->lb;
+    o[2] = t->ub;
+    o[3] = t->true_lb;
+    o[4] = t->true_ub;
+    o[5] = t->align;
+    o[6] = int64_t(t->flags);
+    o[7] = int64_t(t->nbElems);
+    return DDT_SUCCESS;
+}
+
+// ---- opal description import (opal_datatype_internal.h:119-160 layout, 32-byte entries)
+namespace {
+struct RawEntry {
+    uint16_t flags, type;
+    uint32_t a;   // DATA: count; LOOP/END_LOOP: items
+    uint32_t b;   // LOOP: loops
+    uint32_t pad;
+    uint64_t c;   // DATA: blocklen; END_LOOP: size
+    int64_t d;    // DATA: extent; LOOP: extent
+    int64_t e;    // DATA: disp; END_LOOP: first_elem_disp
+};
+
+bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<Node> &out)
+{
+    size_t i = begin;
+    while (i < end) {
+        const unsigned char *p = raw + 32 * i;
+        uint16_t flags, type;
+        std::memcpy(&flags, p, 2);
+        std::memcpy(&type, p + 2, 2);
+        if (flags & F_DATA) {
+            uint32_t count;
+            uint64_t blocklen;
+            int64_t extent, disp;
+            std::memcpy(&count, p + 4, 4);
+            std::memcpy(&blocklen, p + 8, 8);
+            std::memcpy(&extent, p + 16, 8);
+            std::memcpy(&disp, p + 24, 8);
+            if (type < 4 || type > 27)
+                return false;
+            Node n;
+            n.kind = Node::DATA;
+            n.esize = kSize[type];
+            n.count = count;
+            n.blen = blocklen * uint64_t(kSize[type]);
+            n.extent = extent;
+            n.disp = disp;
+            out.push_back(n);
+            ++i;
+        } else if (type == 0) {   // LOOP
+            uint32_t items, loops;
+            int64_t extent;
+            std::memcpy(&items, p + 4, 4);
+            std::memcpy(&loops, p + 8, 4);
+            std::memcpy(&extent, p + 24, 8);
+            size_t endi = i + items;
+            if (endi >= end + 1 || items < 1)
+                return false;
+            const unsigned char *q = raw + 32 * endi;
+            uint64_t size;
+            std::memcpy(&size, q + 16, 8);
+            Node l;
+            l.kind = Node::LOOP;
+            l.count = loops;
+            l.extent = extent;
+            l.body_size = size;
+            if (!parse_opal(raw, i + 1, endi, l.body))
+                return false;
+            out.push_back(std::move(l));
+            i = endi + 1;
+        } else {
+            return false;   // stray END_LOOP
+        }
+    }
+    return true;
+}
+}  // namespace
+
+int ddt_type_from_opal_desc(const void *desc, size_t used, size_t size, ptrdiff_t lb, ptrdiff_t ub,
+                            ptrdiff_t true_lb, ptrdiff_t true_ub, ddt_datatype_t **out)
+{
+    if (!desc || !out)
+        return DDT_ERR_BAD_PARAM;
+    ddt_datatype *t = new_type();
+    if (!parse_opal(static_cast<const unsigned char *>(desc), 0, used, t->desc)) {
+        delete t;
+        return DDT_ERR_BAD_PARAM;
+    }
+    t->size = int64_t(size);
+    t->lb = lb;
+    t->ub = ub;
+    t->true_lb = true_lb;
+    t->true_ub = true_ub;
+    t->flags = F_DATA;
+    t->nbElems = 0;
+    uint64_t s = 0;
+    for (const Node &n : t->desc)
+        s += n.packed_bytes();
+    if (s != size) {
+        delete t;
+        return DDT_ERR_BAD_PARAM;
+    }
+    commit(t);
+    *out = t;
+    return DDT_SUCCESS;
+}
+
+}  // extern "C"

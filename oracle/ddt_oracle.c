@@ -1,0 +1,648 @@
+/*
+ * ddt_oracle.c -- CPU restatement of Open MPI's derived-datatype type map and
+ * homogeneous pack/unpack, used ONLY as test infrastructure.
+ *
+ *   *** TEST INFRASTRUCTURE: only tests/, __graft_entry__.smoke() and the
+ *   *** cpu_baseline leg of bench.py may load this library.  The product
+ *   *** (ompi_amd/, libddt_hip.so) never links, calls or falls back to it.
+ *
+ * What it restates (reference = /root/reference, Open MPI 6.1 dev tree):
+ *   - bounds / size / flag bookkeeping of opal_datatype_add()
+ *       opal/datatype/opal_datatype_add.c:133-460 (LB_UB_CONT :98-116)
+ *   - the MPI constructors, call for call:
+ *       ompi/datatype/ompi_datatype_create_contiguous.c:31-44
+ *       ompi/datatype/ompi_datatype_create_vector.c:32-88   (vector, hvector)
+ *       ompi/datatype/ompi_datatype_create_indexed.c:35-183 (indexed, hindexed,
+ *                                                            indexed_block, hindexed_block)
+ *       ompi/datatype/ompi_datatype_create_struct.c:32-98
+ *       ompi/datatype/ompi_datatype_create_subarray.c:32-112
+ *       ompi/datatype/ompi_datatype.h:270-284 (create_resized) +
+ *       opal/datatype/opal_datatype_resize.c:23-41
+ *   - the packed-stream order of opal_generic_inlined_pack
+ *       (opal/datatype/opal_datatype_pack.c:372-733): type-map order, instance i
+ *       at base + i*extent (extent = ub - lb).
+ *   - pack never splits a predefined element
+ *       (opal/datatype/opal_datatype_pack_accelerator.c:52-58, pack.h:33-76);
+ *     unpack accepts arbitrary byte windows
+ *       (opal/datatype/opal_datatype_unpack_accelerator.c:344-352).
+ *
+ * Representation: a committed type is flattened to its type map, stored as
+ * maximal runs of contiguous bytes made of basic elements of one size.  This is
+ * deliberately the most literal possible form of the MPI type map (independent
+ * of the product's plan compiler) and is sized for test inputs, not for speed.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORT_FLAG_PREDEFINED 0x0002u
+#define ORT_FLAG_CONTIGUOUS 0x0010u
+#define ORT_FLAG_NO_GAPS 0x0020u
+#define ORT_FLAG_USER_LB 0x0040u
+#define ORT_FLAG_USER_UB 0x0080u
+#define ORT_FLAG_DATA 0x0100u
+
+typedef struct {
+    int64_t disp;  /* byte displacement relative to the type origin */
+    int64_t len;   /* bytes */
+    int64_t esize; /* size of the basic elements the run is made of */
+} ort_run;
+
+typedef struct ort_type {
+    int id; /* OPAL predefined id, 0 for derived */
+    uint32_t flags;
+    int64_t size, lb, ub, true_lb, true_ub;
+    int64_t align;
+    int64_t nbElems;
+    ort_run *runs;
+    int64_t nruns, cap;
+    int64_t *pref; /* packed offset of each run (built lazily at first pack) */
+} ort_type;
+
+/* OPAL predefined ids (opal/datatype/opal_datatype_internal.h:71-99) and the
+ * LP64 x86-64 sizes of opal_datatype_module.c:143-180 (alignment = natural). */
+static const int64_t ort_basic_size[29] = {
+    0, 0, 0, 0, 1, 2, 4, 8, 16, 1, 2, 4, 8, 16, 2, 4, 8, 16, 16, 4, 8, 16, 32, 1, 4, 8, 8, 32, 0};
+static const int64_t ort_basic_align[29] = {
+    0, 0, 0, 0, 1, 2, 4, 8, 16, 1, 2, 4, 8, 16, 2, 4, 8, 16, 16, 2, 4, 8, 16, 1, 4, 8, 8, 16, 0};
+
+static ort_type *ort_new(void)
+{
+    /* opal_datatype_construct (opal/datatype/opal_datatype_create.c:33-59) */
+    ort_type *t = (ort_type *) calloc(1, sizeof(ort_type));
+    t->flags = ORT_FLAG_CONTIGUOUS;
+    t->true_lb = INT64_MAX;
+    t->true_ub = INT64_MIN;
+    t->lb = INT64_MAX;
+    t->ub = INT64_MIN;
+    t->align = 1;
+    return t;
+}
+
+void ort_free(ort_type *t)
+{
+    if (!t)
+        return;
+    free(t->runs);
+    free(t->pref);
+    free(t);
+}
+
+static void ort_push_run(ort_type *t, int64_t disp, int64_t len, int64_t esize)
+{
+    if (len <= 0)
+        return;
+    if (t->nruns > 0) {
+        ort_run *p = &t->runs[t->nruns - 1];
+        if (p->disp + p->len == disp && p->esize == esize) {
+            p->len += len;
+            return;
+        }
+    }
+    if (t->nruns == t->cap) {
+        t->cap = t->cap ? 2 * t->cap : 16;
+        t->runs = (ort_run *) realloc(t->runs, (size_t) t->cap * sizeof(ort_run));
+    }
+    t->runs[t->nruns].disp = disp;
+    t->runs[t->nruns].len = len;
+    t->runs[t->nruns].esize = esize;
+    t->nruns++;
+}
+
+ort_type *ort_basic(int id)
+{
+    if (id < 4 || id > 27 || ort_basic_size[id] == 0)
+        return NULL;
+    ort_type *t = ort_new();
+    t->id = id;
+    t->size = ort_basic_size[id];
+    t->lb = 0;
+    t->ub = t->size;
+    t->true_lb = 0;
+    t->true_ub = t->size;
+    t->align = ort_basic_align[id];
+    t->nbElems = 1;
+    t->flags = ORT_FLAG_PREDEFINED | ORT_FLAG_CONTIGUOUS | ORT_FLAG_NO_GAPS | ORT_FLAG_DATA;
+    ort_push_run(t, 0, t->size, t->size);
+    return t;
+}
+
+/* opal_datatype_empty (opal_datatype_constructors.h:67-75), as returned by the
+ * constructors for zero counts through ompi_datatype_duplicate(null). */
+ort_type *ort_empty(void)
+{
+    ort_type *t = ort_new();
+    t->lb = t->ub = t->true_lb = t->true_ub = 0;
+    t->align = 1;
+    t->nbElems = 1;
+    t->flags = ORT_FLAG_CONTIGUOUS | ORT_FLAG_NO_GAPS;
+    return t;
+}
+
+ort_type *ort_dup(const ort_type *o)
+{
+    /* opal_datatype_clone: copy everything, drop PREDEFINED (opal_datatype_clone.c:42-46) */
+    ort_type *t = ort_new();
+    *t = *o;
+    t->id = 0;
+    t->flags &= ~ORT_FLAG_PREDEFINED;
+    t->runs = (ort_run *) malloc((size_t) (o->nruns ? o->nruns : 1) * sizeof(ort_run));
+    memcpy(t->runs, o->runs, (size_t) o->nruns * sizeof(ort_run));
+    t->cap = o->nruns;
+    t->pref = NULL;
+    return t;
+}
+
+static inline int64_t lmin(int64_t a, int64_t b) { return a < b ? a : b; }
+static inline int64_t lmax(int64_t a, int64_t b) { return a < b ? b : a; }
+
+/* Bounds/flags of opal_datatype_add (opal_datatype_add.c:133-460) + type-map append. */
+static void ort_add(ort_type *base, const ort_type *add, int64_t count, int64_t disp, int64_t extent)
+{
+    int64_t lb, ub, true_lb, true_ub, old_true_ub, epsilon;
+    if (count == 0)
+        return;
+    if (extent == -1)
+        extent = add->ub - add->lb;
+    /* OPAL_DATATYPE_LB_UB_CONT (:98-116) */
+    {
+        int64_t upper = disp + extent * (count - 1), lower = disp;
+        if (lower < upper) {
+            lb = lower;
+            ub = upper;
+        } else {
+            lb = upper;
+            ub = lower;
+        }
+        lb += add->lb;
+        ub += add->ub;
+    }
+    true_lb = lb - (add->lb - add->true_lb);
+    true_ub = ub - (add->ub - add->true_ub);
+    if (true_lb > true_ub) {
+        int64_t tmp = true_lb;
+        true_lb = true_ub;
+        true_ub = tmp;
+    }
+    if ((add->flags ^ base->flags) & ORT_FLAG_USER_LB) {
+        if (base->flags & ORT_FLAG_USER_LB)
+            lb = base->lb;
+        base->flags |= ORT_FLAG_USER_LB;
+    } else {
+        lb = lmin(base->lb, lb);
+    }
+    if ((base->flags ^ add->flags) & ORT_FLAG_USER_UB) {
+        if (base->flags & ORT_FLAG_USER_UB)
+            ub = base->ub;
+        base->flags |= ORT_FLAG_USER_UB;
+    } else {
+        ub = lmax(base->ub, ub);
+    }
+    base->lb = lb;
+    base->ub = ub;
+    base->align = lmax(base->align, add->align);
+    if (!(base->flags & ORT_FLAG_USER_UB)) {
+        epsilon = (base->ub - base->lb) % base->align; /* C remainder, as the reference */
+        if (0 != epsilon)
+            base->ub += (base->align - epsilon);
+    }
+    base->flags |= ORT_FLAG_DATA;
+    if (0 == add->size)
+        return;
+    base->size += count * add->size;
+    old_true_ub = (0 == base->nbElems) ? disp : base->true_ub;
+    base->true_lb = lmin(true_lb, base->true_lb);
+    base->true_ub = lmax(true_ub, base->true_ub);
+    if (!(add->flags & ORT_FLAG_PREDEFINED)) {
+        base->flags |= (add->flags & ORT_FLAG_USER_LB);
+        base->flags |= (add->flags & ORT_FLAG_USER_UB);
+    }
+    /* type map: count replicas of add's map at disp + i*extent, in order */
+    for (int64_t i = 0; i < count; i++) {
+        int64_t off = disp + i * extent;
+        for (int64_t r = 0; r < add->nruns; r++)
+            ort_push_run(base, add->runs[r].disp + off, add->runs[r].len, add->runs[r].esize);
+    }
+    /* contiguity flags (:437-451) */
+    {
+        uint32_t localFlags = base->flags & add->flags;
+        base->flags &= ~(ORT_FLAG_CONTIGUOUS | ORT_FLAG_NO_GAPS);
+        if ((localFlags & ORT_FLAG_CONTIGUOUS) && ((disp + add->true_lb) == old_true_ub)
+            && ((add->size == extent) || (count < 2))) {
+            base->flags |= ORT_FLAG_CONTIGUOUS;
+            if (base->size == (base->ub - base->lb))
+                base->flags |= ORT_FLAG_NO_GAPS;
+        }
+    }
+    base->nbElems += count * add->nbElems;
+}
+
+static inline int64_t ort_extent(const ort_type *t) { return t->ub - t->lb; }
+
+ort_type *ort_contiguous(int64_t count, const ort_type *old)
+{
+    if (count == 0 || old->size == 0)
+        return ort_empty();
+    ort_type *t = ort_new();
+    ort_add(t, old, count, 0, ort_extent(old));
+    return t;
+}
+
+ort_type *ort_vector(int64_t count, int64_t blen, int64_t stride, const ort_type *old)
+{
+    int64_t extent = ort_extent(old);
+    if (count == 0 || blen == 0)
+        return ort_empty();
+    ort_type *t = ort_new();
+    if (blen == stride || count <= 1) {
+        ort_add(t, old, count * blen, 0, extent);
+    } else if (blen == 1) {
+        ort_add(t, old, count, 0, extent * stride);
+    } else {
+        ort_add(t, old, blen, 0, extent);
+        ort_type *t2 = ort_new();
+        ort_add(t2, t, count, 0, extent * stride);
+        ort_free(t);
+        t = t2;
+    }
+    return t;
+}
+
+ort_type *ort_hvector(int64_t count, int64_t blen, int64_t stride, const ort_type *old)
+{
+    int64_t extent = ort_extent(old);
+    if (count == 0 || blen == 0)
+        return ort_empty();
+    ort_type *t = ort_new();
+    if (extent * blen == stride || count <= 1) {
+        ort_add(t, old, count * blen, 0, extent);
+    } else if (blen == 1) {
+        ort_add(t, old, count, 0, stride);
+    } else {
+        ort_add(t, old, blen, 0, extent);
+        ort_type *t2 = ort_new();
+        ort_add(t2, t, count, 0, stride);
+        ort_free(t);
+        t = t2;
+    }
+    return t;
+}
+
+/* indexed (scale=extent) and hindexed (scale=1), ompi_datatype_create_indexed.c:35-114 */
+static ort_type *ort_indexed_any(int64_t count, const int64_t *blens, const int64_t *disps,
+                                 const ort_type *old, int bytes)
+{
+    int64_t i, extent = ort_extent(old), disp, dlen, endat;
+    for (i = 0; i < count && blens[i] == 0; i++)
+        ;
+    if (i == count || old->size == 0)
+        return ort_empty();
+    ort_type *t = ort_new();
+    disp = disps[i];
+    dlen = blens[i];
+    endat = bytes ? disp + dlen * extent : disp + dlen;
+    for (i += 1; i < count; i++) {
+        if (blens[i] == 0)
+            continue;
+        if (endat == disps[i]) {
+            dlen += blens[i];
+            endat += bytes ? blens[i] * extent : blens[i];
+        } else {
+            ort_add(t, old, dlen, bytes ? disp : disp * extent, extent);
+            disp = disps[i];
+            dlen = blens[i];
+            endat = bytes ? disp + dlen * extent : disp + dlen;
+        }
+    }
+    ort_add(t, old, dlen, bytes ? disp : disp * extent, extent);
+    return t;
+}
+
+ort_type *ort_indexed(int64_t count, const int64_t *blens, const int64_t *disps, const ort_type *old)
+{
+    return ort_indexed_any(count, blens, disps, old, 0);
+}
+
+ort_type *ort_hindexed(int64_t count, const int64_t *blens, const int64_t *disps, const ort_type *old)
+{
+    return ort_indexed_any(count, blens, disps, old, 1);
+}
+
+/* ompi_datatype_create_indexed.c:117-183 */
+static ort_type *ort_indexed_block_any(int64_t count, int64_t blen, const int64_t *disps,
+                                       const ort_type *old, int bytes)
+{
+    int64_t extent = ort_extent(old), disp, dlen, endat;
+    if (count == 0 || blen == 0)
+        return ort_empty();
+    ort_type *t = ort_new();
+    disp = disps[0];
+    dlen = blen;
+    endat = bytes ? disp + dlen * extent : disp + dlen;
+    for (int64_t i = 1; i < count; i++) {
+        if (endat == disps[i]) {
+            dlen += blen;
+            endat += bytes ? blen * extent : blen;
+        } else {
+            ort_add(t, old, dlen, bytes ? disp : disp * extent, extent);
+            disp = disps[i];
+            dlen = blen;
+            endat = bytes ? disp + blen * extent : disp + blen;
+        }
+    }
+    ort_add(t, old, dlen, bytes ? disp : disp * extent, extent);
+    return t;
+}
+
+ort_type *ort_indexed_block(int64_t count, int64_t blen, const int64_t *disps, const ort_type *old)
+{
+    return ort_indexed_block_any(count, blen, disps, old, 0);
+}
+
+ort_type *ort_hindexed_block(int64_t count, int64_t blen, const int64_t *disps, const ort_type *old)
+{
+    return ort_indexed_block_any(count, blen, disps, old, 1);
+}
+
+/* ompi_datatype_create_struct.c:32-98 (the same-type/adjacent merge included) */
+ort_type *ort_struct(int64_t count, const int64_t *blens, const int64_t *disps,
+                     const ort_type *const *types)
+{
+    int64_t i, start;
+    for (i = 0; i < count && blens[i] == 0; i++)
+        ;
+    if (i == count)
+        return ort_empty();
+    start = i;
+    const ort_type *lastType = types[start];
+    int64_t lastBlock = blens[start];
+    int64_t lastExtent = ort_extent(lastType);
+    int64_t lastDisp = disps[start];
+    int64_t endto = lastDisp + lastExtent * lastBlock;
+    ort_type *t = ort_new();
+    for (i = start + 1; i < count; i++) {
+        if (types[i] == lastType && disps[i] == endto) {
+            lastBlock += blens[i];
+            endto = lastDisp + lastBlock * lastExtent;
+        } else {
+            ort_add(t, lastType, lastBlock, lastDisp, lastExtent);
+            lastType = types[i];
+            lastExtent = ort_extent(lastType);
+            lastBlock = blens[i];
+            lastDisp = disps[i];
+            endto = lastDisp + lastExtent * lastBlock;
+        }
+    }
+    ort_add(t, lastType, lastBlock, lastDisp, lastExtent);
+    return t;
+}
+
+ort_type *ort_resized(const ort_type *old, int64_t lb, int64_t extent)
+{
+    /* ompi_datatype_create_resized = duplicate + opal_datatype_resize (resize.c:23-41) */
+    ort_type *t = ort_dup(old);
+    t->lb = lb;
+    t->ub = lb + extent;
+    t->flags &= ~ORT_FLAG_NO_GAPS;
+    t->flags |= ORT_FLAG_USER_LB | ORT_FLAG_USER_UB;
+    if (extent == t->size && (t->flags & ORT_FLAG_CONTIGUOUS))
+        t->flags |= ORT_FLAG_NO_GAPS;
+    return t;
+}
+
+/* ompi_datatype_create_subarray.c:32-112; order 0 = MPI_ORDER_C, 1 = MPI_ORDER_FORTRAN */
+ort_type *ort_subarray(int ndims, const int64_t *sizes, const int64_t *subsizes,
+                       const int64_t *starts, int order, const ort_type *old)
+{
+    int64_t extent = ort_extent(old), size, displ;
+    ort_type *last, *nt;
+    int i, step, end_loop;
+    if (ndims < 2) {
+        if (ndims == 0)
+            return ort_empty();
+        last = ort_contiguous(subsizes[0], old);
+        size = sizes[0];
+        displ = starts[0];
+    } else {
+        if (order == 0) {
+            i = ndims - 1;
+            step = -1;
+            end_loop = -1;
+        } else {
+            i = 0;
+            step = 1;
+            end_loop = ndims;
+        }
+        last = ort_vector(subsizes[i + step], subsizes[i], sizes[i], old);
+        size = sizes[i] * sizes[i + step];
+        displ = starts[i] + starts[i + step] * sizes[i];
+        for (i += 2 * step; i != end_loop; i += step) {
+            nt = ort_hvector(subsizes[i], 1, size * extent, last);
+            ort_free(last);
+            displ += size * starts[i];
+            size *= sizes[i];
+            last = nt;
+        }
+    }
+    nt = ort_new();
+    ort_add(nt, last, 1, displ * extent, size * extent);
+    ort_free(last);
+    nt->lb = 0;
+    nt->ub = size * extent;
+    nt->flags &= ~ORT_FLAG_NO_GAPS;
+    nt->flags |= ORT_FLAG_USER_LB | ORT_FLAG_USER_UB;
+    if (size * extent == nt->size && (nt->flags & ORT_FLAG_CONTIGUOUS))
+        nt->flags |= ORT_FLAG_NO_GAPS;
+    return nt;
+}
+
+/* out[0..7] = size, lb, ub, true_lb, true_ub, align, flags, nruns */
+void ort_info(const ort_type *t, int64_t *out)
+{
+    out[0] = t->size;
+    out[1] = t->lb;
+    out[2] = t->ub;
+    out[3] = t->true_lb;
+    out[4] = t->true_ub;
+    out[5] = t->align;
+    out[6] = t->flags;
+    out[7] = t->nruns;
+}
+
+/* run i of the flattened map: disp, len, esize */
+void ort_run_at(const ort_type *t, int64_t i, int64_t *out)
+{
+    out[0] = t->runs[i].disp;
+    out[1] = t->runs[i].len;
+    out[2] = t->runs[i].esize;
+}
+
+static void ort_prefix(ort_type *t)
+{
+    if (t->pref)
+        return;
+    t->pref = (int64_t *) malloc((size_t) (t->nruns + 1) * sizeof(int64_t));
+    int64_t acc = 0;
+    for (int64_t r = 0; r < t->nruns; r++) {
+        t->pref[r] = acc;
+        acc += t->runs[r].len;
+    }
+    t->pref[t->nruns] = acc;
+}
+
+/* Locate packed position p (< count*size): instance and run index, offset within run. */
+static void ort_locate(const ort_type *t, int64_t p, int64_t *inst, int64_t *run, int64_t *within)
+{
+    *inst = p / t->size;
+    int64_t q = p - *inst * t->size;
+    int64_t lo = 0, hi = t->nruns - 1;
+    while (lo < hi) { /* last run with pref <= q */
+        int64_t mid = (lo + hi + 1) / 2;
+        if (t->pref[mid] <= q)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    *run = lo;
+    *within = q - t->pref[lo];
+}
+
+/*
+ * Pack the window [position, position+len) of the packed stream of `count`
+ * instances at `base` into `out`.  Stops early rather than split a basic element
+ * (opal_datatype_pack_accelerator.c:52-58).  Returns the bytes produced.
+ */
+int64_t ort_pack(ort_type *t, int64_t count, const void *base, int64_t position, void *out,
+                 int64_t len)
+{
+    const int64_t total = count * t->size;
+    if (t->size == 0 || position >= total || len <= 0)
+        return 0;
+    ort_prefix(t);
+    const int64_t ext = ort_extent(t);
+    int64_t inst, run, within, done = 0;
+    ort_locate(t, position, &inst, &run, &within);
+    const char *b = (const char *) base;
+    char *o = (char *) out;
+    while (done < len && position + done < total) {
+        const ort_run *r = &t->runs[run];
+        int64_t avail = r->len - within;
+        int64_t space = len - done;
+        int64_t n = avail;
+        if (n > space) {
+            /* never split a basic element: keep whole elements (plus the tail of a
+             * partially packed element we are finishing) */
+            int64_t head = (r->esize - (within % r->esize)) % r->esize;
+            if (head > space)
+                n = 0;
+            else
+                n = head + ((space - head) / r->esize) * r->esize;
+            if (n == 0)
+                break;
+        }
+        memcpy(o + done, b + inst * ext + r->disp + within, (size_t) n);
+        done += n;
+        within += n;
+        if (within == r->len) {
+            within = 0;
+            if (++run == t->nruns) {
+                run = 0;
+                inst++;
+            }
+        } else {
+            break; /* window exhausted mid-run */
+        }
+    }
+    return done;
+}
+
+/* Byte-exact transfer of the packed window [position, position+len): dir 0 packs
+ * (user -> stream), dir 1 unpacks (stream -> user).  Returns bytes moved. */
+static int64_t ort_xfer(ort_type *t, int64_t count, char *user, int64_t position, char *stream,
+                        int64_t len, int dir)
+{
+    const int64_t total = count * t->size;
+    if (t->size == 0 || position >= total || len <= 0)
+        return 0;
+    ort_prefix(t);
+    const int64_t ext = ort_extent(t);
+    int64_t inst, run, within, done = 0;
+    if (len > total - position)
+        len = total - position;
+    ort_locate(t, position, &inst, &run, &within);
+    while (done < len) {
+        const ort_run *r = &t->runs[run];
+        int64_t n = r->len - within;
+        if (n > len - done)
+            n = len - done;
+        char *u = user + inst * ext + r->disp + within;
+        if (dir)
+            memcpy(u, stream + done, (size_t) n);
+        else
+            memcpy(stream + done, u, (size_t) n);
+        done += n;
+        within += n;
+        if (within == r->len) {
+            within = 0;
+            if (++run == t->nruns) {
+                run = 0;
+                inst++;
+            }
+        }
+    }
+    return done;
+}
+
+/* Unpack a byte-exact window (unpack accepts split elements). Returns bytes consumed. */
+int64_t ort_unpack(ort_type *t, int64_t count, void *base, int64_t position, const void *in,
+                   int64_t len)
+{
+    return ort_xfer(t, count, (char *) base, position, (char *) in, len, 1);
+}
+
+/* Byte-exact pack window (used for position-sharded baselines). */
+int64_t ort_pack_bytes(ort_type *t, int64_t count, const void *base, int64_t position, void *out,
+                       int64_t len)
+{
+    return ort_xfer(t, count, (char *) base, position, (char *) out, len, 0);
+}
+
+/* ---- multi-threaded full pack/unpack, sharded by packed position (the
+ *      8-thread set_position split of SURVEY.md §6).  Used as cpu_baseline. ---- */
+typedef struct {
+    ort_type *t;
+    int64_t count;
+    void *base;
+    void *buf;
+    int64_t pos, len;
+    int unpack;
+} ort_job;
+
+static void *ort_worker(void *arg)
+{
+    ort_job *j = (ort_job *) arg;
+    ort_xfer(j->t, j->count, (char *) j->base, j->pos, (char *) j->buf + j->pos, j->len, j->unpack);
+    return NULL;
+}
+
+int64_t ort_run_mt(ort_type *t, int64_t count, void *base, void *buf, int nthreads, int unpack)
+{
+    int64_t total = count * t->size;
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > 256)
+        nthreads = 256;
+    ort_prefix(t); /* build lazy state before threading (SURVEY.md §5 ptypes race) */
+    pthread_t th[256];
+    ort_job jobs[256];
+    int64_t per = (total + nthreads - 1) / nthreads;
+    for (int k = 0; k < nthreads; k++) {
+        int64_t p0 = lmin((int64_t) k * per, total), p1 = lmin(p0 + per, total);
+        jobs[k] = (ort_job){t, count, base, buf, p0, p1 - p0, unpack};
+        pthread_create(&th[k], NULL, ort_worker, &jobs[k]);
+    }
+    for (int k = 0; k < nthreads; k++)
+        pthread_join(th[k], NULL);
+    return total;
+}

@@ -1,0 +1,185 @@
+"""ctypes wrapper of the CPU oracle (oracle/ddt_oracle.c) -- test infrastructure only.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load this.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "_build", "libddt_oracle.so")
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+    return ORACLE_LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        src = os.path.join(ORACLE_DIR, "ddt_oracle.c")
+        if not os.path.exists(ORACLE_LIB) or (
+                os.path.exists(src) and os.path.getmtime(src) > os.path.getmtime(ORACLE_LIB)):
+            build()
+        L = ctypes.CDLL(ORACLE_LIB)
+        vp, i64, i = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+        sig = {
+            "ort_basic": (vp, [i]), "ort_empty": (vp, []), "ort_dup": (vp, [vp]),
+            "ort_free": (None, [vp]),
+            "ort_contiguous": (vp, [i64, vp]),
+            "ort_vector": (vp, [i64, i64, i64, vp]), "ort_hvector": (vp, [i64, i64, i64, vp]),
+            "ort_indexed": (vp, [i64, vp, vp, vp]), "ort_hindexed": (vp, [i64, vp, vp, vp]),
+            "ort_indexed_block": (vp, [i64, i64, vp, vp]),
+            "ort_hindexed_block": (vp, [i64, i64, vp, vp]),
+            "ort_struct": (vp, [i64, vp, vp, vp]),
+            "ort_subarray": (vp, [i, vp, vp, vp, i, vp]),
+            "ort_resized": (vp, [vp, i64, i64]),
+            "ort_info": (None, [vp, vp]), "ort_run_at": (None, [vp, i64, vp]),
+            "ort_pack": (i64, [vp, i64, vp, i64, vp, i64]),
+            "ort_pack_bytes": (i64, [vp, i64, vp, i64, vp, i64]),
+            "ort_unpack": (i64, [vp, i64, vp, i64, vp, i64]),
+            "ort_run_mt": (i64, [vp, i64, vp, vp, i, i]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _arr(a, dt):
+    a = np.ascontiguousarray(np.asarray(a, dtype=dt))
+    return a, a.ctypes.data_as(ctypes.c_void_p)
+
+
+class OType:
+    """An oracle type (flattened MPI type map)."""
+
+    def __init__(self, h):
+        if not h:
+            raise ValueError("oracle returned null")
+        self.h = ctypes.c_void_p(h)
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().ort_free(self.h)
+        except Exception:
+            pass
+
+    def info(self) -> dict:
+        out = (ctypes.c_int64 * 8)()
+        lib().ort_info(self.h, out)
+        keys = ("size", "lb", "ub", "true_lb", "true_ub", "align", "flags", "nruns")
+        return dict(zip(keys, list(out)))
+
+    def runs(self):
+        n = self.info()["nruns"]
+        out = (ctypes.c_int64 * 3)()
+        res = []
+        for r in range(n):
+            lib().ort_run_at(self.h, r, out)
+            res.append((out[0], out[1], out[2]))
+        return res
+
+    @property
+    def size(self):
+        return self.info()["size"]
+
+    @property
+    def extent(self):
+        i = self.info()
+        return i["ub"] - i["lb"]
+
+    # --- data movement (numpy byte arrays; base = address of the type origin) ---
+    def pack(self, count: int, user: np.ndarray, origin: int, position: int, length: int,
+             element_granular: bool = True) -> bytes:
+        out = np.zeros(max(length, 1), dtype=np.uint8)
+        base = user.ctypes.data + origin
+        fn = lib().ort_pack if element_granular else lib().ort_pack_bytes
+        n = fn(self.h, count, ctypes.c_void_p(base), position, out.ctypes.data_as(ctypes.c_void_p),
+               length)
+        return out[:n].tobytes()
+
+    def unpack(self, count: int, user: np.ndarray, origin: int, position: int, data: bytes) -> int:
+        src = np.frombuffer(data, dtype=np.uint8).copy()
+        base = user.ctypes.data + origin
+        return lib().ort_unpack(self.h, count, ctypes.c_void_p(base), position,
+                                src.ctypes.data_as(ctypes.c_void_p), len(data))
+
+    def pack_all(self, count: int, user: np.ndarray, origin: int) -> bytes:
+        total = count * self.size
+        return self.pack(count, user, origin, 0, total, element_granular=False)
+
+    def run_mt(self, count, user_ptr: int, buf_ptr: int, nthreads: int, unpack: bool) -> int:
+        return lib().ort_run_mt(self.h, count, ctypes.c_void_p(user_ptr), ctypes.c_void_p(buf_ptr),
+                                nthreads, int(unpack))
+
+
+def basic(type_id: int) -> OType:
+    return OType(lib().ort_basic(type_id))
+
+
+def contiguous(count, old):
+    return OType(lib().ort_contiguous(count, old.h))
+
+
+def vector(count, blen, stride, old):
+    return OType(lib().ort_vector(count, blen, stride, old.h))
+
+
+def hvector(count, blen, stride, old):
+    return OType(lib().ort_hvector(count, blen, stride, old.h))
+
+
+def indexed(blens, disps, old):
+    b, bp = _arr(blens, np.int64)
+    d, dp = _arr(disps, np.int64)
+    return OType(lib().ort_indexed(len(b), bp, dp, old.h))
+
+
+def hindexed(blens, disps, old):
+    b, bp = _arr(blens, np.int64)
+    d, dp = _arr(disps, np.int64)
+    return OType(lib().ort_hindexed(len(b), bp, dp, old.h))
+
+
+def indexed_block(blen, disps, old):
+    d, dp = _arr(disps, np.int64)
+    return OType(lib().ort_indexed_block(len(d), blen, dp, old.h))
+
+
+def hindexed_block(blen, disps, old):
+    d, dp = _arr(disps, np.int64)
+    return OType(lib().ort_hindexed_block(len(d), blen, dp, old.h))
+
+
+def struct(blens, disps, types):
+    b, bp = _arr(blens, np.int64)
+    d, dp = _arr(disps, np.int64)
+    arr = (ctypes.c_void_p * len(types))(*[t.h.value for t in types])
+    return OType(lib().ort_struct(len(b), bp, dp, ctypes.cast(arr, ctypes.c_void_p)))
+
+
+def subarray(sizes, subsizes, starts, order, old):
+    s, sp = _arr(sizes, np.int64)
+    ss, ssp = _arr(subsizes, np.int64)
+    st, stp = _arr(starts, np.int64)
+    return OType(lib().ort_subarray(len(s), sp, ssp, stp, order, old.h))
+
+
+def resized(old, lb, extent):
+    return OType(lib().ort_resized(old.h, lb, extent))
+
+
+def dup(old):
+    return OType(lib().ort_dup(old.h))
