@@ -108,6 +108,8 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         }
         assign_tasks(S->items);
         S->ntasks = total_tasks(S->items);
+        for (const Item &it : S->items)
+            S->has_lists = S->has_lists || it.kind == ITEM_LIST_UNI || it.kind == ITEM_LIST_VAR;
         if (!S->items.empty()) {
             size_t bytes = S->items.size() * sizeof(Item);
             Item *h = nullptr;
@@ -122,22 +124,27 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             if (e != hipSuccess)
                 return fail(DDT_ERR_HIP, std::string("item upload: ") + hipGetErrorString(e));
         }
-        HIPCHK(hipEventCreateWithFlags(&S->last_use, hipEventDisableTiming));
-        std::shared_ptr<ItemSet> evicted;
+        bool drain = false;
         {
             std::lock_guard<std::mutex> g(P.mu);
             P.cache.insert(P.cache.begin(), S);
             if (P.cache.size() > kCacheEntries) {
-                evicted = P.cache.back();
+                // an evicted descriptor set may still be read by a launch in flight:
+                // park it, and free parked sets only after the device has drained
+                P.graveyard.push_back(P.cache.back());
                 P.cache.pop_back();
+                drain = P.graveyard.size() > kCacheEntries;
             }
         }
-        evicted.reset();   // waits for its last launch
+        if (drain) {
+            HIPCHK(hipDeviceSynchronize());
+            std::lock_guard<std::mutex> g(P.mu);
+            P.graveyard.clear();
+        }
     }
     if (S->items.empty())
         return DDT_SUCCESS;
-    HIPCHK(launch_move(S->d_items, uint32_t(S->items.size()), S->ntasks, dir, stream));
-    HIPCHK(hipEventRecord(S->last_use, stream));
+    HIPCHK(launch_move(S->d_items, uint32_t(S->items.size()), S->ntasks, dir, S->has_lists, stream));
     return DDT_SUCCESS;
 }
 
@@ -258,7 +265,10 @@ int prepare(ddt_convertor *c, const ddt_datatype *t, size_t count, const void *b
     if (c->local_size == 0)
         return DDT_SUCCESS;
     // accelerator slot: check_addr must report device memory (opal_convertor.c:593-608)
-    if (classify(buf) != MEM_DEVICE)
+    // probe the first byte the type map touches (buf + true_lb): unlike the reference,
+    // which probes pUserBuf itself (opal_convertor.c:624,654), this also classifies
+    // MPI_BOTTOM-style buffers whose base lies outside the allocation
+    if (classify(static_cast<const char *>(buf) + t->true_lb) != MEM_DEVICE)
         return fail(DDT_ERR_NOT_DEVICE, "user buffer is not device memory: the HIP engine is the "
                                         "accelerator slot of the convertor");
     try {
@@ -504,7 +514,8 @@ int ddt_copy_content_same_ddt(const ddt_datatype_t *t, size_t count, void *dst, 
         return fail(DDT_ERR_NOT_COMMITTED, "datatype not committed");
     if (count == 0 || t->size == 0)
         return DDT_SUCCESS;
-    if (classify(dst) != MEM_DEVICE || classify(src) != MEM_DEVICE)
+    if (classify(static_cast<const char *>(dst) + t->true_lb) != MEM_DEVICE
+        || classify(static_cast<const char *>(src) + t->true_lb) != MEM_DEVICE)
         return fail(DDT_ERR_NOT_DEVICE, "typed copy needs device buffers");
     ddt_datatype *dt = const_cast<ddt_datatype *>(t);
     std::shared_ptr<Plan> P;

@@ -105,7 +105,7 @@ struct ItemSet {
     std::vector<Item> items;
     Item *d_items = nullptr;
     uint32_t ntasks = 0;
-    hipEvent_t last_use = nullptr;
+    bool has_lists = false;
     ~ItemSet();
 };
 
@@ -115,7 +115,8 @@ struct Plan {
     uint64_t dev_bytes = 0;       // device metadata bytes
     bool dev_ready = false;       // index lists uploaded
     std::mutex mu;
-    std::vector<std::shared_ptr<ItemSet>> cache;   // most recent first
+    std::vector<std::shared_ptr<ItemSet>> cache;      // most recent first
+    std::vector<std::shared_ptr<ItemSet>> graveyard;  // evicted, freed after a device drain
     ~Plan();
 };
 

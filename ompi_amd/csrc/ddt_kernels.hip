@@ -13,6 +13,8 @@
 // Replaces the per-block cbmemcpy loop of opal_pack_accelerator_simple /
 // opal_unpack_accelerator_simple (opal_datatype_pack_accelerator.c:161-295,
 // opal_datatype_unpack_accelerator.c:210-368).
+#include <cstdlib>
+
 #include <hip/hip_runtime.h>
 
 #include "ddt_device.h"
@@ -20,26 +22,31 @@
 
 namespace ddt {
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 template <int U> struct Vec;
-template <> struct Vec<16> { using T = uint4; };
-template <> struct Vec<8> { using T = uint2; };
+template <> struct Vec<16> { using T = u32x4; };
+template <> struct Vec<8> { using T = u32x2; };
 template <> struct Vec<4> { using T = uint32_t; };
 template <> struct Vec<2> { using T = uint16_t; };
 template <> struct Vec<1> { using T = uint8_t; };
 
-struct Nest {
+// Nest of an item, ND dims kept in registers (ND = 0: generic MAXD path).
+template <int ND> struct Nest {
+    static constexpr int N = ND > 0 ? ND : MAXD;
     uint32_t ndim;
-    uint32_t cnt[MAXD];
-    FastDiv fd[MAXD];
-    int64_t us[MAXD];
-    int64_t ps[MAXD];
+    uint32_t cnt[N];
+    FastDiv fd[N];
+    int64_t us[N];
+    int64_t ps[N];
 };
 
-__device__ __forceinline__ void load_nest(const Item *it, Nest &n)
+template <int ND>
+__device__ __forceinline__ void load_nest(const Item *it, Nest<ND> &n)
 {
-    n.ndim = it->ndim;
+    n.ndim = ND > 0 ? uint32_t(ND) : it->ndim;
 #pragma unroll
-    for (int j = 0; j < MAXD; ++j) {
+    for (int j = 0; j < Nest<ND>::N; ++j) {
         n.cnt[j] = uint32_t(it->cnt[j]);
         n.fd[j] = it->fd[j];
         n.us[j] = it->ustr[j];
@@ -48,11 +55,12 @@ __device__ __forceinline__ void load_nest(const Item *it, Nest &n)
 }
 
 // block index -> (user, packed) byte offsets over the nest (32-bit index path)
-__device__ __forceinline__ void nest_offsets32(const Nest &n, uint32_t blk, int64_t &uo, int64_t &po)
+template <int ND>
+__device__ __forceinline__ void nest_offsets32(const Nest<ND> &n, uint32_t blk, int64_t &uo, int64_t &po)
 {
 #pragma unroll
-    for (int j = MAXD - 1; j > 0; --j) {
-        if (j < int(n.ndim)) {
+    for (int j = Nest<ND>::N - 1; j > 0; --j) {
+        if (ND > 0 || j < int(n.ndim)) {
             uint32_t q = fastdiv(blk, n.fd[j]);
             uint32_t idx = blk - q * n.cnt[j];
             blk = q;
@@ -60,7 +68,7 @@ __device__ __forceinline__ void nest_offsets32(const Nest &n, uint32_t blk, int6
             po += int64_t(idx) * n.ps[j];
         }
     }
-    if (n.ndim > 0) {
+    if (ND > 0 || n.ndim > 0) {
         uo += int64_t(blk) * n.us[0];
         po += int64_t(blk) * n.ps[0];
     }
@@ -81,110 +89,146 @@ __device__ __forceinline__ void nest_offsets64(const Item *it, uint64_t blk, int
     }
 }
 
+template <int U> constexpr int unroll() { return U >= 16 ? 4 : 8; }
+
 template <int U, int DIR>
-__device__ __forceinline__ void run_affine(const Item *it, uint64_t ub, uint64_t ue)
+__device__ __noinline__ void run_affine64(const Item *it, uint64_t ub, uint64_t ue)
 {
     using T = typename Vec<U>::T;
-    constexpr int K = U >= 16 ? 4 : 8;
-    const uint64_t user = it->user, packed = it->packed;
-    if (it->idx64) {
-        const uint64_t upb = it->upb;
-        for (uint64_t u = ub + threadIdx.x; u < ue; u += THREADS) {
-            uint64_t blk = u / upb, within = u - blk * upb;
-            int64_t uo = int64_t(within) * U, po = uo;
-            nest_offsets64(it, blk, uo, po);
-            const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
-            T *dst = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
-            *dst = *src;
-        }
-        return;
+    const uint64_t user = it->user, packed = it->packed, upb = it->upb;
+    for (uint64_t u = ub + threadIdx.x; u < ue; u += THREADS) {
+        uint64_t blk = u / upb, within = u - blk * upb;
+        int64_t uo = int64_t(within) * U, po = uo;
+        nest_offsets64(it, blk, uo, po);
+        const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
+        T *dst = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
+        *dst = *src;
     }
-    Nest n;
+}
+
+template <typename T, bool NT> __device__ __forceinline__ T ld(const T *p)
+{
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <typename T, bool NT> __device__ __forceinline__ void st(T *p, T v)
+{
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <int U, int DIR, int ND, bool NT>
+__device__ __forceinline__ void run_affine(const Item *it, uint32_t ub, uint32_t ue)
+{
+    using T = typename Vec<U>::T;
+    constexpr int K = unroll<U>();
+    const uint64_t user = it->user, packed = it->packed;
+    Nest<ND> n;
     load_nest(it, n);
     const FastDiv fdu = it->fd_upb;
     const uint32_t upb = uint32_t(it->upb);
-    const uint32_t e = uint32_t(ue);
-    for (uint32_t base = uint32_t(ub) + threadIdx.x; base < e; base += THREADS * K) {
+    for (uint32_t base = ub + threadIdx.x; base < ue; base += THREADS * K) {
         T v[K];
         T *dst[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t u = base + uint32_t(k) * THREADS;
             dst[k] = nullptr;
-            if (u < e) {
+            if (u < ue) {
                 const uint32_t blk = fastdiv(u, fdu);
                 const uint32_t within = u - blk * upb;
                 int64_t uo = int64_t(within) * U, po = uo;
                 nest_offsets32(n, blk, uo, po);
                 const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
                 dst[k] = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
-                v[k] = *src;
+                v[k] = ld<T, NT>(src);
             }
         }
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (dst[k])
-                *dst[k] = v[k];
+                st<T, NT>(dst[k], v[k]);
     }
 }
 
 template <int U, int DIR>
-__device__ __forceinline__ void run_list_uni(const Item *it, uint64_t ub, uint64_t ue)
+__device__ __noinline__ void run_list_uni64(const Item *it, uint64_t ub, uint64_t ue)
 {
     using T = typename Vec<U>::T;
-    constexpr int K = U >= 16 ? 4 : 8;
-    const uint64_t user = it->user, packed = it->packed;
-    const uint64_t ulen = it->ulen;
+    const uint64_t user = it->user, packed = it->packed, ulen = it->ulen;
     const bool d32 = it->ldisp32 != 0;
     const int32_t *disp32 = reinterpret_cast<const int32_t *>(it->ldisp);
     const int64_t *disp64 = reinterpret_cast<const int64_t *>(it->ldisp);
-    if (it->idx64) {
-        const uint64_t upb = it->upb, nb = it->nblk;
-        for (uint64_t u = ub + threadIdx.x; u < ue; u += THREADS) {
-            uint64_t blk = u / upb, within = u - blk * upb;
-            uint64_t i = blk % nb, outer = blk / nb;
-            int64_t uo = 0, po = 0;
-            nest_offsets64(it, outer, uo, po);
-            int64_t d = d32 ? int64_t(disp32[i]) : disp64[i];
-            uo += d + int64_t(within) * U;
-            po += int64_t(i * ulen + within * U);
-            const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
-            T *dst = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
-            *dst = *src;
-        }
-        return;
+    const uint64_t upb = it->upb, nb = it->nblk;
+    for (uint64_t u = ub + threadIdx.x; u < ue; u += THREADS) {
+        uint64_t blk = u / upb, within = u - blk * upb;
+        uint64_t i = blk % nb, outer = blk / nb;
+        int64_t uo = 0, po = 0;
+        nest_offsets64(it, outer, uo, po);
+        int64_t d = d32 ? int64_t(disp32[i]) : disp64[i];
+        uo += d + int64_t(within) * U;
+        po += (it->same ? d : int64_t(i * ulen)) + int64_t(within) * U;
+        const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
+        T *dst = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
+        *dst = *src;
     }
-    Nest n;
+}
+
+// Index list with one block length: all K displacement loads of a round are issued
+// (coalesced) before the K dependent gathers, so each round pays two memory latencies
+// instead of 2K.
+template <int U, int DIR>
+__device__ __forceinline__ void run_list_uni(const Item *it, uint32_t ub, uint32_t ue)
+{
+    using T = typename Vec<U>::T;
+    constexpr int K = unroll<U>();
+    const uint64_t user = it->user, packed = it->packed;
+    const uint64_t ulen = it->ulen;
+    const bool d32 = it->ldisp32 != 0;
+    const bool same = it->same != 0;
+    const int32_t *disp32 = reinterpret_cast<const int32_t *>(it->ldisp);
+    const int64_t *disp64 = reinterpret_cast<const int64_t *>(it->ldisp);
+    Nest<0> n;
     load_nest(it, n);
     const FastDiv fdu = it->fd_upb, fdn = it->fd_nblk;
     const uint32_t upb = uint32_t(it->upb), nb = uint32_t(it->nblk);
-    const uint32_t e = uint32_t(ue);
-    for (uint32_t base = uint32_t(ub) + threadIdx.x; base < e; base += THREADS * K) {
-        T v[K];
-        T *dst[K];
+    for (uint32_t base = ub + threadIdx.x; base < ue; base += THREADS * K) {
+        int64_t uo[K], po[K];
+        uint32_t ii[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const uint32_t u = base + uint32_t(k) * THREADS;
-            dst[k] = nullptr;
-            if (u < e) {
-                const uint32_t blk = fastdiv(u, fdu);
-                const uint32_t within = u - blk * upb;
-                const uint32_t outer = fastdiv(blk, fdn);
-                const uint32_t i = blk - outer * nb;
-                int64_t uo = 0, po = 0;
-                nest_offsets32(n, outer, uo, po);
-                const int64_t d = d32 ? int64_t(disp32[i]) : disp64[i];
-                uo += d + int64_t(within) * U;
-                po += int64_t(uint64_t(i) * ulen) + int64_t(within) * U;
-                const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
-                dst[k] = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
-                v[k] = *src;
-            }
+            const uint32_t uu = u < ue ? u : ub;   // clamp: keeps the loads in bounds
+            const uint32_t blk = fastdiv(uu, fdu);
+            const uint32_t within = uu - blk * upb;
+            const uint32_t outer = fastdiv(blk, fdn);
+            ii[k] = blk - outer * nb;
+            uo[k] = int64_t(within) * U;
+            po[k] = int64_t(uint64_t(ii[k]) * ulen) + int64_t(within) * U;
+            nest_offsets32(n, outer, uo[k], po[k]);
         }
+        int64_t d[K];
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            if (dst[k])
-                *dst[k] = v[k];
+            d[k] = d32 ? int64_t(disp32[ii[k]]) : disp64[ii[k]];
+        if (same) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                po[k] += d[k] - int64_t(uint64_t(ii[k]) * ulen);
+        }
+        T v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo[k] + d[k] : packed + po[k]);
+            v[k] = *src;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (base + uint32_t(k) * THREADS < ue) {
+                T *dst = reinterpret_cast<T *>(DIR == 0 ? packed + po[k] : user + uo[k] + d[k]);
+                *dst = v[k];
+            }
+        }
     }
 }
 
@@ -242,14 +286,69 @@ __device__ __forceinline__ void run_list_var(const Item *it, uint64_t ub, uint64
             const int64_t d = d32 ? int64_t(disp32[i]) : disp64[i];
             const int64_t off = s0 - lx;
             uint8_t *up = reinterpret_cast<uint8_t *>(user + uo + d + off);
-            uint8_t *pp = reinterpret_cast<uint8_t *>(packed + po + int64_t(goff[g] + excl) + off);
+            uint8_t *pp = reinterpret_cast<uint8_t *>(packed + po + (it->same ? d : int64_t(goff[g] + excl)) + off);
             if (DIR == 0) copy_bytes_aligned(pp, up, uint64_t(s1 - s0), it->U);
             else copy_bytes_aligned(up, pp, uint64_t(s1 - s0), it->U);
         }
     }
 }
 
-template <int DIR>
+// Deep nests (> 4 dims) are rare: their dims are re-read from the (cached) item on every
+// unit instead of being held in registers, which keeps the kernel's SGPR budget small.
+template <int U, int DIR, bool NT>
+__device__ __forceinline__ void run_affine_deep(const Item *it, uint32_t ub, uint32_t ue)
+{
+    using T = typename Vec<U>::T;
+    const uint64_t user = it->user, packed = it->packed;
+    const FastDiv fdu = it->fd_upb;
+    const uint32_t upb = uint32_t(it->upb);
+    const int nd = int(it->ndim);
+    for (uint32_t u = ub + threadIdx.x; u < ue; u += THREADS) {
+        uint32_t blk = fastdiv(u, fdu);
+        const uint32_t within = u - blk * upb;
+        int64_t uo = int64_t(within) * U, po = uo;
+        for (int j = nd - 1; j > 0; --j) {
+            const uint32_t q = fastdiv(blk, it->fd[j]);
+            const uint32_t idx = blk - q * uint32_t(it->cnt[j]);
+            blk = q;
+            uo += int64_t(idx) * it->ustr[j];
+            po += int64_t(idx) * it->pstr[j];
+        }
+        uo += int64_t(blk) * it->ustr[0];
+        po += int64_t(blk) * it->pstr[0];
+        const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
+        T *dst = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
+        st<T, NT>(dst, ld<T, NT>(src));
+    }
+}
+
+template <int U, int DIR, bool NT>
+__device__ __forceinline__ void dispatch_affine_u(const Item *it, uint32_t ub, uint32_t ue)
+{
+    switch (it->ndim) {
+    case 1: run_affine<U, DIR, 1, NT>(it, ub, ue); break;
+    case 2: run_affine<U, DIR, 2, NT>(it, ub, ue); break;
+    case 3: run_affine<U, DIR, 3, NT>(it, ub, ue); break;
+    case 4: run_affine<U, DIR, 4, NT>(it, ub, ue); break;
+    default: run_affine_deep<U, DIR, NT>(it, ub, ue); break;
+    }
+}
+
+template <int DIR, bool NT>
+__device__ __forceinline__ void dispatch_affine(const Item *it, uint32_t ub, uint32_t ue)
+{
+    switch (it->U) {
+    case 16: dispatch_affine_u<16, DIR, NT>(it, ub, ue); break;
+    case 8: dispatch_affine_u<8, DIR, NT>(it, ub, ue); break;
+    case 4: dispatch_affine_u<4, DIR, NT>(it, ub, ue); break;
+    case 2: dispatch_affine_u<2, DIR, NT>(it, ub, ue); break;
+    default: dispatch_affine_u<1, DIR, NT>(it, ub, ue); break;
+    }
+}
+
+// LISTS = false: affine + fragment items only (vector/hvector/subarray/struct nests), a
+// lean register budget; LISTS = true adds the index-list paths.
+template <int DIR, bool NT, bool LISTS>
 __global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restrict__ items, uint32_t nitems)
 {
     const uint32_t b = blockIdx.x;
@@ -266,25 +365,40 @@ __global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restric
     if (ue > it->u1) ue = it->u1;
     switch (it->kind) {
     case ITEM_AFFINE:
-        switch (it->U) {
-        case 16: run_affine<16, DIR>(it, ub, ue); break;
-        case 8: run_affine<8, DIR>(it, ub, ue); break;
-        case 4: run_affine<4, DIR>(it, ub, ue); break;
-        case 2: run_affine<2, DIR>(it, ub, ue); break;
-        default: run_affine<1, DIR>(it, ub, ue); break;
+        if (it->idx64) {
+            switch (it->U) {
+            case 16: run_affine64<16, DIR>(it, ub, ue); break;
+            case 8: run_affine64<8, DIR>(it, ub, ue); break;
+            case 4: run_affine64<4, DIR>(it, ub, ue); break;
+            case 2: run_affine64<2, DIR>(it, ub, ue); break;
+            default: run_affine64<1, DIR>(it, ub, ue); break;
+            }
+        } else {
+            dispatch_affine<DIR, NT>(it, uint32_t(ub), uint32_t(ue));
         }
         break;
     case ITEM_LIST_UNI:
-        switch (it->U) {
-        case 16: run_list_uni<16, DIR>(it, ub, ue); break;
-        case 8: run_list_uni<8, DIR>(it, ub, ue); break;
-        case 4: run_list_uni<4, DIR>(it, ub, ue); break;
-        case 2: run_list_uni<2, DIR>(it, ub, ue); break;
-        default: run_list_uni<1, DIR>(it, ub, ue); break;
+        if (!LISTS) break;
+        if (it->idx64) {
+            switch (it->U) {
+            case 16: run_list_uni64<16, DIR>(it, ub, ue); break;
+            case 8: run_list_uni64<8, DIR>(it, ub, ue); break;
+            case 4: run_list_uni64<4, DIR>(it, ub, ue); break;
+            case 2: run_list_uni64<2, DIR>(it, ub, ue); break;
+            default: run_list_uni64<1, DIR>(it, ub, ue); break;
+            }
+        } else {
+            switch (it->U) {
+            case 16: run_list_uni<16, DIR>(it, uint32_t(ub), uint32_t(ue)); break;
+            case 8: run_list_uni<8, DIR>(it, uint32_t(ub), uint32_t(ue)); break;
+            case 4: run_list_uni<4, DIR>(it, uint32_t(ub), uint32_t(ue)); break;
+            case 2: run_list_uni<2, DIR>(it, uint32_t(ub), uint32_t(ue)); break;
+            default: run_list_uni<1, DIR>(it, uint32_t(ub), uint32_t(ue)); break;
+            }
         }
         break;
     case ITEM_LIST_VAR:
-        run_list_var<DIR>(it, ub, ue);
+        if (LISTS) run_list_var<DIR>(it, ub, ue);
         break;
     default:   // ITEM_FRAG
         if (threadIdx.x == 0) {
@@ -297,15 +411,40 @@ __global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restric
     }
 }
 
-hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir,
+static bool use_nt()
+{
+    static const bool nt = [] {
+        const char *e = std::getenv("DDT_NT");
+        return e && e[0] == '1';
+    }();
+    return nt;
+}
+
+template <int DIR, bool NT>
+static void launch_dir(const Item *d_items, uint32_t nitems, uint32_t ntasks, bool lists,
+                       hipStream_t stream)
+{
+    if (lists)
+        hipLaunchKernelGGL((ddt_move_kernel<DIR, NT, true>), dim3(ntasks), dim3(THREADS), 0, stream,
+                           d_items, nitems);
+    else
+        hipLaunchKernelGGL((ddt_move_kernel<DIR, NT, false>), dim3(ntasks), dim3(THREADS), 0, stream,
+                           d_items, nitems);
+}
+
+hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
                        hipStream_t stream)
 {
     if (ntasks == 0 || nitems == 0)
         return hipSuccess;
-    if (dir == 0)
-        hipLaunchKernelGGL(ddt_move_kernel<0>, dim3(ntasks), dim3(THREADS), 0, stream, d_items, nitems);
-    else
-        hipLaunchKernelGGL(ddt_move_kernel<1>, dim3(ntasks), dim3(THREADS), 0, stream, d_items, nitems);
+    const bool nt = use_nt();
+    if (dir == 0) {
+        if (nt) launch_dir<0, true>(d_items, nitems, ntasks, lists, stream);
+        else launch_dir<0, false>(d_items, nitems, ntasks, lists, stream);
+    } else {
+        if (nt) launch_dir<1, true>(d_items, nitems, ntasks, lists, stream);
+        else launch_dir<1, false>(d_items, nitems, ntasks, lists, stream);
+    }
     return hipGetLastError();
 }
 

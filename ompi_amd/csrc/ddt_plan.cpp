@@ -9,6 +9,7 @@
 // per block -- the reference issues one cbmemcpy per block instead
 // (opal_datatype_accelerator_copy.h:51-75).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -21,7 +22,11 @@ namespace ddt {
 
 Plan::~Plan()
 {
-    cache.clear();   // waits for the last launch that used each descriptor set
+    // launches that read these descriptors or lists may still be in flight
+    if (!cache.empty() || !graveyard.empty() || dev_ready)
+        (void) hipDeviceSynchronize();
+    cache.clear();
+    graveyard.clear();
     for (DevList &d : dev) {
         if (d.disp) (void) hipFree(d.disp);
         if (d.len) (void) hipFree(d.len);
@@ -31,12 +36,8 @@ Plan::~Plan()
 
 ItemSet::~ItemSet()
 {
-    if (last_use)
-        (void) hipEventSynchronize(last_use);
     if (d_items)
         (void) hipFree(d_items);
-    if (last_use)
-        (void) hipEventDestroy(last_use);
 }
 
 namespace {
@@ -260,9 +261,21 @@ void fill_dims(Item &it, const std::vector<LeafDim> &dims)
     }
 }
 
+// Fixed packed bytes per workgroup task (DDT_TASK_KB, tuning sweeps only); 0 = adaptive.
+uint64_t task_bytes_override()
+{
+    static const uint64_t tb = [] {
+        const char *e = std::getenv("DDT_TASK_KB");
+        long v = e ? std::atol(e) : 0;
+        return uint64_t(v > 0 ? v : 0) << 10;
+    }();
+    return tb;
+}
+
 uint64_t units_per_task(uint32_t U)
 {
-    return U >= 16 ? 2048 : (U == 8 ? 4096 : 8192);
+    uint64_t u = (32u << 10) / U;   // provisional; assign_tasks() sets the final size
+    return u < THREADS ? THREADS : u;
 }
 
 void add_frag(std::vector<Item> &items, uint64_t user, uint64_t packed, uint64_t n)
@@ -302,17 +315,16 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
         const int64_t leaf_pk = int64_t(pk) - int64_t(W0) + (same_layout ? L.src_off : L.dst_off);
         // window in leaf-local bytes (packed-stream order == type-map order)
         uint64_t f0, f1;
+        const uint64_t inner = L.kind == LEAF_AFFINE ? L.blen : L.list->total;
+        uint64_t leaf_total = inner;
+        for (const LeafDim &d : dims)
+            leaf_total *= d.cnt;
         if (same_layout) {
             f0 = 0;   // typed copy always moves whole messages
-            uint64_t tot = L.bytes_per_iter;
-            for (const LeafDim &d : dims)
-                tot *= d.cnt;
-            f1 = tot;
+            f1 = leaf_total;
         } else {
-            std::vector<LeafDim> dd = dims;
-            uint64_t inner = L.kind == LEAF_AFFINE ? L.blen : L.list->total;
-            f0 = leaf_bytes_before(dd, inner, int64_t(W0) - L.dst_off);
-            f1 = leaf_bytes_before(dd, inner, int64_t(W1) - L.dst_off);
+            f0 = leaf_bytes_before(dims, inner, int64_t(W0) - L.dst_off);
+            f1 = leaf_bytes_before(dims, inner, int64_t(W1) - L.dst_off);
         }
         if (f1 <= f0)
             continue;
@@ -361,6 +373,8 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
                 big = big || d.cnt >= 0xffffffffull;
             }
             it.idx64 = (big || total_units >= 0xffffffffull) ? 1 : 0;
+            if (u1 * U > leaf_total || total_units * U != leaf_total)
+                throw std::runtime_error("plan: affine unit range outside its leaf");
             it.u0 = u0;
             it.u1 = u1;
             it.units_per_task = units_per_task(U);
@@ -377,6 +391,8 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
         simplify(od, nullptr);
         const uint64_t nb = X.nblk();
         const int64_t ubase = int64_t(user) + L.list_shift;
+        // typed copy: destination list base mirrors the source (pk + shift + disp_base)
+        const int64_t same_pk = int64_t(pk) + L.list_shift + D.disp_base;
         if (X.len.empty()) {   // uniform block length
             uint64_t g = X.ulen | X.disp_gcd | absu(ubase) | absu(leaf_pk);
             for (const LeafDim &d : od)
@@ -407,6 +423,7 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
             Item it{};
             it.kind = ITEM_LIST_UNI;
             it.leaf = uint32_t(li);
+            it.same = same_layout ? 1 : 0;
             it.U = U;
             fill_dims(it, od);
             it.upb = X.ulen / U;
@@ -417,6 +434,8 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
             for (const LeafDim &d : od)
                 total_units *= d.cnt;
             it.idx64 = (total_units >= 0xffffffffull || it.upb >= 0xffffffffull) ? 1 : 0;
+            if (u1 * U > leaf_total || total_units * U != leaf_total)
+                throw std::runtime_error("plan: list unit range outside its leaf");
             it.ulen = X.ulen;
             it.ldisp = uint64_t(uintptr_t(D.disp));
             it.ldisp32 = D.disp32 ? 1 : 0;
@@ -424,7 +443,7 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
             it.u1 = u1;
             it.units_per_task = units_per_task(U);
             it.user = uint64_t(ubase + D.disp_base);
-            it.packed = uint64_t(leaf_pk);
+            it.packed = uint64_t(same_layout ? same_pk : leaf_pk);
             items.push_back(it);
             continue;
         }
@@ -445,6 +464,7 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
         Item it{};
         it.kind = ITEM_LIST_VAR;
         it.leaf = uint32_t(li);
+        it.same = same_layout ? 1 : 0;
         it.U = pick_unit(g);
         fill_dims(it, od);
         it.nblk = nb;
@@ -460,7 +480,7 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
         it.u1 = unit_of(f1, true);
         it.units_per_task = 16;
         it.user = uint64_t(ubase + D.disp_base);
-        it.packed = uint64_t(leaf_pk);
+        it.packed = uint64_t(same_layout ? same_pk : leaf_pk);
         it.w0 = int64_t(f0);   // clip window in leaf-local packed bytes
         it.w1 = int64_t(f1);
         items.push_back(it);
@@ -469,13 +489,29 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
 
 void assign_tasks(std::vector<Item> &items)
 {
-    uint32_t tb = 0;
+    // Size tasks so the launch has ~6 K workgroups (24 per CU: enough waves in flight to
+    // cover HBM latency) but never tasks below 4 KiB or above 64 KiB of packed bytes.
+    uint64_t total = 0;
+    for (const Item &it : items)
+        if (it.kind == ITEM_AFFINE || it.kind == ITEM_LIST_UNI)
+            total += (it.u1 - it.u0) * it.U;
+    uint64_t tb = task_bytes_override();
+    if (tb == 0) {
+        tb = 4096;
+        while (tb < (64u << 10) && total / (tb * 2) >= 6144)
+            tb *= 2;
+    }
+    uint32_t b = 0;
     for (Item &it : items) {
+        if (it.kind == ITEM_AFFINE || it.kind == ITEM_LIST_UNI) {
+            uint64_t u = tb / it.U;
+            it.units_per_task = u < THREADS ? THREADS : u;
+        }
         uint64_t units = it.u1 - it.u0;
         uint64_t nt = (units + it.units_per_task - 1) / it.units_per_task;
-        it.task_begin = tb;
+        it.task_begin = b;
         it.ntasks = uint32_t(nt);
-        tb += uint32_t(nt);
+        b += uint32_t(nt);
     }
 }
 

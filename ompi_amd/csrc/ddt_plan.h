@@ -16,7 +16,7 @@ void assign_tasks(std::vector<Item> &items);
 uint32_t total_tasks(const std::vector<Item> &items);
 
 // ddt_kernels.hip: dir 0 = pack / typed copy (user side -> packed side), 1 = unpack.
-hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir,
+hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
                        hipStream_t stream);
 
 }  // namespace ddt

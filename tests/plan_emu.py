@@ -35,6 +35,7 @@ class Item(ctypes.Structure):
         ("ldisp", ctypes.c_uint64), ("llen", ctypes.c_uint64), ("lgoff", ctypes.c_uint64),
         ("nblk", ctypes.c_uint64), ("fd_nblk", FastDiv), ("ulen", ctypes.c_uint64),
         ("ldisp32", ctypes.c_uint32), ("leaf", ctypes.c_uint32),
+        ("same", ctypes.c_uint32), ("pad1", ctypes.c_uint32),
         ("w0", ctypes.c_int64), ("w1", ctypes.c_int64), ("nbytes", ctypes.c_uint64),
     ]
 
@@ -204,7 +205,7 @@ def emulate(its, user_arr, user_addr, packed_arr, packed_addr, direction, lists=
                 uo, po = _nest(it, outer)
                 dd = d[i] - base if it.ldisp32 else d[i]
                 ua = it.user + uo + dd + within * U
-                pa = it.packed + po + i * it.ulen + within * U
+                pa = it.packed + po + (dd if it.same else i * it.ulen) + within * U
             mv(ua, pa, U)
             continue
         # LIST_VAR: one wave per 64-block group, inclusive scan, clip
@@ -225,6 +226,6 @@ def emulate(its, user_arr, user_addr, packed_arr, packed_addr, direction, lists=
                     off = s0[k] - lx[k]
                     dd = d[i[k]] - base if it.ldisp32 else d[i[k]]
                     ua = it.user + uo[0] + dd + off
-                    pa = it.packed + po[0] + goff + excl[k] + off
+                    pa = it.packed + po[0] + (dd if it.same else goff + excl[k]) + off
                     mv(np.array([ua]), np.array([pa]), int(s1[k] - s0[k]))
     return cover

@@ -111,3 +111,47 @@ def test_extent_minus_one_quirk():
     b = R.Built(("vector", 4, 3, -1, ("basic", 4)))
     assert b.o.info()["lb"] == 0 and b.engine().info()["lb"] == 0
     assert b.engine().info()["ub"] == 12
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_typed_copy_items_match_oracle(seed):
+    """Same-layout descriptors (opal_datatype_copy_content_same_ddt) move every byte of
+    the type map once, from the source layout to the same offsets of the destination."""
+    rng = random.Random(500 + seed)
+    for n in range(80):
+        b = R.Built(R.random_recipe(rng))
+        oi = b.o.info()
+        if oi["size"] == 0:
+            continue
+        count = rng.choice([1, 2, 5])
+        span, origin = R.layout(oi, count)
+        src = R.fill(span, n)
+        dst = np.full(span, 0xA5, dtype=np.uint8)
+        UA, PA = (1 << 40), (1 << 41)
+        its = E.items(b.engine(), count, UA + origin, PA + origin, 0, oi["size"] * count,
+                      same_layout=True)
+        for it in its:
+            if it.kind == E.ITEM_AFFINE:
+                tot = it.upb
+                for j in range(it.ndim):
+                    tot *= it.cnt[j]
+                assert it.u1 <= tot
+        E.emulate(its, src, UA, dst, PA, 0, E.list_tables(b.engine()))
+        exp = np.full(span, 0xA5, dtype=np.uint8)
+        stream = b.o.pack(count, src, origin, 0, oi["size"] * count, element_granular=False)
+        b.o.unpack(count, exp, origin, 0, stream)
+        if not _overlap(b.o, count):
+            np.testing.assert_array_equal(dst, exp, err_msg=str(b.recipe))
+
+
+def _overlap(o, count):
+    info = o.info()
+    ext = info["ub"] - info["lb"]
+    seen = set()
+    for i in range(count):
+        for d, n, _ in o.runs():
+            for x in range(d + i * ext, d + i * ext + n):
+                if x in seen:
+                    return True
+                seen.add(x)
+    return False
