@@ -175,6 +175,7 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--faces", action="store_true", help="also time each face type alone")
+    ap.add_argument("--no-graph", action="store_true", help="skip the HIP-graph replay measurement")
     args = ap.parse_args()
 
     import torch
@@ -253,6 +254,31 @@ def main():
     tp = float(np.mean([a.elapsed_time(b) for a, b, _ in ev])) / 1e3
     tu = float(np.mean([b.elapsed_time(c) for _, b, c in ev])) / 1e3
 
+    # The same K steps captured once into a HIP graph and replayed: the launch-bound
+    # regime a persistent halo exchange runs in (reported beside the eager value).
+    graph_step = None
+    if not args.no_graph:
+        gs = torch.cuda.Stream(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=gs, capture_error_mode="relaxed"):
+            cs = torch.cuda.current_stream(dev)
+            cp.set_stream(cs, True)
+            cu.set_stream(cs, True)
+            for _ in range(args.steps):
+                pack()
+                unpack()
+        cp.set_stream(stream, True)
+        cu.set_stream(stream, True)
+        with torch.cuda.stream(gs):
+            g.replay()
+            torch.cuda.synchronize()
+            g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            g0.record(gs)
+            g.replay()
+            g1.record(gs)
+        torch.cuda.synchronize()
+        graph_step = g0.elapsed_time(g1) / 1e3 / args.steps
+
     result = None
     if rank == 0:
         ms_per_step = wall / args.steps * 1e3
@@ -268,6 +294,7 @@ def main():
                            parallelism=f"replicas x{world} (fields sharded by count, no collective)"),
             "per_gpu_GiBs": round(2.0 * S / (tp + tu) / GiB, 3),
             "kernel_ms": {"pack": round(tp * 1e3, 4), "unpack": round(tu * 1e3, 4)},
+            "graph_replay_GiBs_per_gpu": (round(2.0 * S / graph_step / GiB, 3) if graph_step else None),
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 2), "peak": 8000.0,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": None},
         }

@@ -229,3 +229,56 @@ def test_large_index_list(device):
     for rec in [("indexed_block", 1, disps.tolist(), ("basic", 15)),
                 ("indexed", rng.integers(0, 4, n).tolist(), (disps * 4).tolist(), ("basic", 4))]:
         _roundtrip(R.Built(rec), 2, device, 17)
+
+
+# ---------------------------------------------------------------- reference corpus
+from . import corpus as _corpus  # noqa: E402
+import hashlib as _hashlib  # noqa: E402
+import json as _json  # noqa: E402
+import os as _os  # noqa: E402
+
+_GOLD = _json.load(open(_os.path.join(_os.path.dirname(__file__), "golden", "corpus_sha256.json")))
+
+
+@pytest.mark.parametrize("name", sorted(_corpus.CORPUS))
+def test_corpus_on_gpu(device, name):
+    """Every datatype of ompi/test/datatype/datatype_corpus.c: GPU pack == the reference's
+    by-hand stream (golden SHA-256), for the whole message and the opt_desc_equiv.c:63
+    fragment matrix; GPU unpack == the by-hand unpack (gaps keep their 0xA5 sentinel)."""
+    import torch
+    import ompi_amd
+    rec, byhand = _corpus.CORPUS[name]()
+    b = R.Built(rec)
+    g = _GOLD[name]
+    count = g["count"]
+    info = b.o.info()
+    size = count * info["size"]
+    span, origin = R.layout(info, count)
+    host = R.fill(span, 0x5A)
+    user = _dev(host, device)
+    e = b.engine()
+    packed = torch.zeros(size, dtype=torch.uint8, device=device)
+    assert ompi_amd.pack(user.data_ptr() + origin, count, e, packed, size, 0) == size
+    assert _hashlib.sha256(_host(packed).tobytes()).hexdigest() == g["sha256"]
+    for frag in (12, 16, 40, 4096):
+        packed.zero_()
+        conv = ompi_amd.Convertor().prepare_for_send(e, count, user.data_ptr() + origin)
+        pos, rc = 0, 0
+        while rc == 0:
+            rc, _, md = conv.pack([(packed.data_ptr() + pos, min(frag, size - pos))])
+            if md == 0:
+                rc, _, md = conv.pack([(packed.data_ptr() + pos, size - pos)])
+            pos += md
+        assert pos == size
+        assert _hashlib.sha256(_host(packed).tobytes()).hexdigest() == g["sha256"], frag
+    if _overlapping(b.o, count):
+        return
+    ref = _host(packed)
+    out = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
+    ompi_amd.unpack(packed, size, 0, out.data_ptr() + origin, count, e)
+    exp = np.full(span, 0xA5, dtype=np.uint8)
+    p = 0
+    for off, n in byhand(count):          # the reference's unpack_byhand_* regions
+        exp[origin + off: origin + off + n] = ref[p:p + n]
+        p += n
+    np.testing.assert_array_equal(_host(out), exp)
