@@ -79,7 +79,7 @@ struct Item {
     uint32_t ldisp32;       // displacement array is int32
     uint32_t leaf;          // plan leaf this item belongs to (diagnostics)
     uint32_t same;          // typed copy: the packed side uses the user-side layout too
-    uint32_t pad1;
+    uint32_t nt;            // user-side accesses non-temporal (sparse gathers over > MALL spans)
     int64_t w0, w1;         // LIST_VAR / FRAG: window [w0, w1) in packed-stream coordinates
     uint64_t nbytes;        // FRAG: bytes
 };

@@ -272,6 +272,26 @@ uint64_t task_bytes_override()
     return tb;
 }
 
+// Non-temporal user-side LOADS (pack) for sparse, narrow blocks spread over more than
+// the 256 MiB Infinity Cache (x-face-like gathers): the 6-face halo pack went from 112 to
+// 68 us (scripts/ubench*.hip, bench.py).  Stores stay temporal: non-temporal scattered
+// stores made the halo unpack slower (82 -> 108 us).  DDT_NT=0/1 forces it off/on.
+bool use_nt(uint32_t U, uint64_t blen, const std::vector<LeafDim> &dims)
+{
+    static const int force = [] {
+        const char *e = std::getenv("DDT_NT");
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
+    }();
+    if (force >= 0)
+        return force == 1;
+    if (U > 8 || blen > 64)
+        return false;
+    uint64_t span = blen;
+    for (const LeafDim &d : dims)
+        span += (d.cnt - 1) * absu(d.sstr);
+    return span > (192ull << 20);
+}
+
 uint64_t units_per_task(uint32_t U)
 {
     uint64_t u = (32u << 10) / U;   // provisional; assign_tasks() sets the final size
@@ -375,6 +395,7 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
             it.idx64 = (big || total_units >= 0xffffffffull) ? 1 : 0;
             if (u1 * U > leaf_total || total_units * U != leaf_total)
                 throw std::runtime_error("plan: affine unit range outside its leaf");
+            it.nt = use_nt(U, blen, sd) ? 1 : 0;
             it.u0 = u0;
             it.u1 = u1;
             it.units_per_task = units_per_task(U);

@@ -1,0 +1,76 @@
+"""Multi-GPU sharding of one datatype message.
+
+For a homogeneous type the packed offset of top-level instance i is exactly i*size, so
+shard k of G owns instances [first_k, first_k + n_k) and writes packed bytes
+[first_k*size, (first_k+n_k)*size) -- no exchange is needed to pack.  This is the
+same partition the reference applies with opal_convertor_set_position for multi-BTL
+scheduling (pml_ob1_sendreq.c:1184-1194).  A consumer that needs the whole packed
+stream on one device gets it with one all-gather of equal-size shards (RCCL over
+xGMI on GPUs; gloo in the CPU tests).
+"""
+from __future__ import annotations
+
+from typing import List, Tuple
+
+
+def count_shards(count: int, world: int) -> List[Tuple[int, int]]:
+    """Balanced split of `count` top-level instances: [(first, n)] per rank."""
+    if world <= 0:
+        raise ValueError("world must be positive")
+    base, rem = divmod(count, world)
+    out, first = [], 0
+    for r in range(world):
+        n = base + (1 if r < rem else 0)
+        out.append((first, n))
+        first += n
+    return out
+
+
+def position_shards(total: int, world: int, granule: int = 1) -> List[Tuple[int, int]]:
+    """Split the packed stream [0, total) into `world` byte ranges on `granule` boundaries
+    (opal_convertor_set_position-style sharding of a count-1 type)."""
+    per = -(-total // world)
+    per = -(-per // granule) * granule
+    out = []
+    for r in range(world):
+        a = min(r * per, total)
+        b = min(a + per, total)
+        out.append((a, b - a))
+    return out
+
+
+def shard_of(count: int, size: int, extent: int, rank: int, world: int):
+    """(first instance, n instances, user byte offset, packed byte offset) of `rank`."""
+    first, n = count_shards(count, world)[rank]
+    return first, n, first * extent, first * size
+
+
+def pack_shard(dt, count: int, buf, rank: int, world: int, out, stream=None) -> int:
+    """Pack this rank's instances of a `count`-instance message at `buf` into `out`
+    (a buffer of n*size bytes).  Returns the bytes packed."""
+    from .convertor import addr, pack_window
+    info = dt.info()
+    size, extent = info["size"], info["ub"] - info["lb"]
+    first, n, uoff, poff = shard_of(count, size, extent, rank, world)
+    if n == 0:
+        return 0
+    return pack_window(dt, n, addr(buf) + uoff, 0, out, n * size, stream=stream)
+
+
+def gather_packed(local, group=None):
+    """All-gather equal-size packed shards into the full stream (torch.distributed;
+    backend 'nccl' is RCCL on ROCm).  `local` is a 1-D uint8 tensor; shards are padded to
+    the largest one and trimmed by the caller with `count_shards`."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    n = torch.tensor([local.numel()], device=local.device, dtype=torch.int64)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    mx = int(max(int(s.item()) for s in sizes))
+    buf = torch.zeros(mx, dtype=local.dtype, device=local.device)
+    buf[:local.numel()] = local
+    out = torch.empty(world * mx, dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    parts = [out[r * mx: r * mx + int(sizes[r].item())] for r in range(world)]
+    return torch.cat(parts)

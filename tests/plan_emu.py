@@ -35,7 +35,7 @@ class Item(ctypes.Structure):
         ("ldisp", ctypes.c_uint64), ("llen", ctypes.c_uint64), ("lgoff", ctypes.c_uint64),
         ("nblk", ctypes.c_uint64), ("fd_nblk", FastDiv), ("ulen", ctypes.c_uint64),
         ("ldisp32", ctypes.c_uint32), ("leaf", ctypes.c_uint32),
-        ("same", ctypes.c_uint32), ("pad1", ctypes.c_uint32),
+        ("same", ctypes.c_uint32), ("nt", ctypes.c_uint32),
         ("w0", ctypes.c_int64), ("w1", ctypes.c_int64), ("nbytes", ctypes.c_uint64),
     ]
 
