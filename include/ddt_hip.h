@@ -205,6 +205,10 @@ int ddt_debug_items(const ddt_datatype_t *type, size_t count, uint64_t user, uin
                     size_t *nitems, size_t *item_size);
 int64_t ddt_type_plan_list(const ddt_datatype_t *type, size_t leaf, int64_t *disp, uint64_t *len,
                            size_t cap);
+/* Tuning knobs for A/B measurements (affect descriptor sets built afterwards):
+ * "nt" = user-side non-temporal gathers (-1 auto, 0 off, 1 on); "task_kb" = packed KiB per
+ * workgroup (0 adaptive).  Environment: DDT_NT, DDT_TASK_KB. */
+int ddt_tune(const char *key, long value);
 /* Library self-check of host-side index arithmetic (fast division); returns 0 on success. */
 int ddt_selftest(void);
 const char *ddt_version(void);

@@ -110,7 +110,13 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         S->ntasks = total_tasks(S->items);
         for (const Item &it : S->items)
             S->has_lists = S->has_lists || it.kind == ITEM_LIST_UNI || it.kind == ITEM_LIST_VAR;
-        if (!S->items.empty()) {
+        if (S->items.size() <= INLINE_ITEMS) {
+            // small sets travel in the kernel-argument segment: no device allocation
+            S->inline_ok = true;
+            S->blk.n = uint32_t(S->items.size());
+            for (size_t i = 0; i < S->items.size(); ++i)
+                S->blk.items[i] = S->items[i];
+        } else if (!S->items.empty()) {
             size_t bytes = S->items.size() * sizeof(Item);
             Item *h = nullptr;
             HIPCHK(hipHostMalloc((void **) &h, bytes, hipHostMallocDefault));
@@ -131,7 +137,8 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             if (P.cache.size() > kCacheEntries) {
                 // an evicted descriptor set may still be read by a launch in flight:
                 // park it, and free parked sets only after the device has drained
-                P.graveyard.push_back(P.cache.back());
+                if (!P.cache.back()->inline_ok)
+                    P.graveyard.push_back(P.cache.back());
                 P.cache.pop_back();
                 drain = P.graveyard.size() > kCacheEntries;
             }
@@ -144,7 +151,10 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     }
     if (S->items.empty())
         return DDT_SUCCESS;
-    HIPCHK(launch_move(S->d_items, uint32_t(S->items.size()), S->ntasks, dir, S->has_lists, stream));
+    if (S->inline_ok)
+        HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, stream));
+    else
+        HIPCHK(launch_move(S->d_items, uint32_t(S->items.size()), S->ntasks, dir, S->has_lists, stream));
     return DDT_SUCCESS;
 }
 
@@ -664,6 +674,20 @@ int ddt_selftest(void)
             return 2;
     }
     return 0;
+}
+
+int ddt_tune(const char *key, long value)
+{
+    if (!key)
+        return DDT_ERR_BAD_PARAM;
+    std::string k(key);
+    if (k == "nt")
+        tuning().nt = value < 0 ? -1 : (value ? 1 : 0);
+    else if (k == "task_kb")
+        tuning().task_kb = value;
+    else
+        return fail(DDT_ERR_BAD_PARAM, "unknown tuning key " + k);
+    return DDT_SUCCESS;
 }
 
 const char *ddt_version(void) { return "ddt-hip 0.1 (gfx950)"; }

@@ -106,6 +106,8 @@ struct ItemSet {
     Item *d_items = nullptr;
     uint32_t ntasks = 0;
     bool has_lists = false;
+    bool inline_ok = false;       // <= INLINE_ITEMS: launched from the kernarg segment
+    ItemBlock blk{};
     ~ItemSet();
 };
 

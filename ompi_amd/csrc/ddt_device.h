@@ -82,6 +82,17 @@ struct Item {
     uint32_t nt;            // user-side accesses non-temporal (sparse gathers over > MALL spans)
     int64_t w0, w1;         // LIST_VAR / FRAG: window [w0, w1) in packed-stream coordinates
     uint64_t nbytes;        // FRAG: bytes
+    uint64_t pad2;          // keeps sizeof(Item) == 512
 };
+
+// Descriptors passed by value in the kernel-argument segment (<= 4 KiB).
+constexpr uint32_t INLINE_ITEMS = 7;
+struct ItemBlock {
+    uint32_t n;
+    uint32_t pad[3];
+    Item items[INLINE_ITEMS];
+};
+static_assert(sizeof(Item) == 512, "Item layout is shared with tests/plan_emu.py");
+static_assert(sizeof(ItemBlock) <= 4096, "kernel argument segment limit");
 
 }  // namespace ddt

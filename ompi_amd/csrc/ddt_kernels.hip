@@ -349,7 +349,7 @@ __device__ __forceinline__ void dispatch_affine(const Item *it, uint32_t ub, uin
 // LISTS = false: affine + fragment items only (vector/hvector/subarray/struct nests), a
 // lean register budget; LISTS = true adds the index-list paths.
 template <int DIR, bool LISTS>
-__global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restrict__ items, uint32_t nitems)
+__device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32_t nitems)
 {
     const uint32_t b = blockIdx.x;
     uint32_t lo = 0, hi = nitems - 1;
@@ -412,6 +412,24 @@ __global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restric
     }
 }
 
+template <int DIR, bool LISTS>
+__global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restrict__ items, uint32_t nitems)
+{
+    move_body<DIR, LISTS>(items, nitems);
+}
+
+// Small launches carry their descriptors in the kernel-argument segment: no device
+// buffer, no upload, no cache entry (fragment pipelines, windows, one-off messages).
+template <int DIR, bool LISTS>
+__global__ __launch_bounds__(THREADS) void ddt_move_inline_kernel(ItemBlock blk)
+{
+    // read the block in place from the kernarg segment (taking the address of `blk`
+    // would copy 3.6 KB to scratch)
+    const ItemBlock *kb = reinterpret_cast<const ItemBlock *>(
+        (const void *) __builtin_amdgcn_kernarg_segment_ptr());
+    move_body<DIR, LISTS>(kb->items, kb->n);
+}
+
 template <int DIR>
 static void launch_dir(const Item *d_items, uint32_t nitems, uint32_t ntasks, bool lists,
                        hipStream_t stream)
@@ -422,6 +440,21 @@ static void launch_dir(const Item *d_items, uint32_t nitems, uint32_t ntasks, bo
     else
         hipLaunchKernelGGL((ddt_move_kernel<DIR, false>), dim3(ntasks), dim3(THREADS), 0, stream,
                            d_items, nitems);
+}
+
+hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists,
+                              hipStream_t stream)
+{
+    if (ntasks == 0 || blk.n == 0)
+        return hipSuccess;
+    if (dir == 0) {
+        if (lists) hipLaunchKernelGGL((ddt_move_inline_kernel<0, true>), dim3(ntasks), dim3(THREADS), 0, stream, blk);
+        else hipLaunchKernelGGL((ddt_move_inline_kernel<0, false>), dim3(ntasks), dim3(THREADS), 0, stream, blk);
+    } else {
+        if (lists) hipLaunchKernelGGL((ddt_move_inline_kernel<1, true>), dim3(ntasks), dim3(THREADS), 0, stream, blk);
+        else hipLaunchKernelGGL((ddt_move_inline_kernel<1, false>), dim3(ntasks), dim3(THREADS), 0, stream, blk);
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,

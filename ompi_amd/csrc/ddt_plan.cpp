@@ -20,6 +20,19 @@
 
 namespace ddt {
 
+Tuning &tuning()
+{
+    static Tuning t = [] {
+        Tuning v;
+        if (const char *e = std::getenv("DDT_NT"))
+            v.nt = e[0] == '1' ? 1 : 0;
+        if (const char *e = std::getenv("DDT_TASK_KB"))
+            v.task_kb = std::atol(e);
+        return v;
+    }();
+    return t;
+}
+
 Plan::~Plan()
 {
     // launches that read these descriptors or lists may still be in flight
@@ -261,15 +274,10 @@ void fill_dims(Item &it, const std::vector<LeafDim> &dims)
     }
 }
 
-// Fixed packed bytes per workgroup task (DDT_TASK_KB, tuning sweeps only); 0 = adaptive.
+// Fixed packed bytes per workgroup task (tuning sweeps only); 0 = adaptive.
 uint64_t task_bytes_override()
 {
-    static const uint64_t tb = [] {
-        const char *e = std::getenv("DDT_TASK_KB");
-        long v = e ? std::atol(e) : 0;
-        return uint64_t(v > 0 ? v : 0) << 10;
-    }();
-    return tb;
+    return uint64_t(tuning().task_kb > 0 ? tuning().task_kb : 0) << 10;
 }
 
 // Non-temporal user-side LOADS (pack) for sparse, narrow blocks spread over more than
@@ -278,10 +286,7 @@ uint64_t task_bytes_override()
 // stores made the halo unpack slower (82 -> 108 us).  DDT_NT=0/1 forces it off/on.
 bool use_nt(uint32_t U, uint64_t blen, const std::vector<LeafDim> &dims)
 {
-    static const int force = [] {
-        const char *e = std::getenv("DDT_NT");
-        return e ? (e[0] == '1' ? 1 : 0) : -1;
-    }();
+    const int force = tuning().nt;
     if (force >= 0)
         return force == 1;
     if (U > 8 || blen > 64)

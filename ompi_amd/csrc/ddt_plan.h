@@ -10,12 +10,21 @@
 
 namespace ddt {
 
+// Tuning knobs (environment DDT_NT / DDT_TASK_KB, or ddt_tune()): for A/B sweeps.
+struct Tuning {
+    int nt = -1;       // user-side non-temporal loads: -1 auto, 0 off, 1 on
+    long task_kb = 0;  // packed KiB per workgroup task: 0 = adaptive
+};
+Tuning &tuning();
+
 void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t user, uint64_t pk,
                  uint64_t W0, uint64_t W1, bool same_layout, std::vector<Item> &items);
 void assign_tasks(std::vector<Item> &items);
 uint32_t total_tasks(const std::vector<Item> &items);
 
 // ddt_kernels.hip: dir 0 = pack / typed copy (user side -> packed side), 1 = unpack.
+hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists,
+                              hipStream_t stream);
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
                        hipStream_t stream);
 

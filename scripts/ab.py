@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of engine tuning variants in ONE process (cdna guide §5.4 rule 24):
+per variant and round, a fresh committed type, then pack and unpack timed separately
+with HIP events.  Usage: python scripts/ab.py --config cfg2 --variants nt=-1,nt=0,nt=1"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import ompi_amd  # noqa: E402
+from ompi_amd import recipe as ER  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--variants", default="nt=-1,nt=0,nt=1")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    recipe, count, _ = bench.make_workload(args.config)
+    variants = [dict(kv.split("=") for kv in v.split(";")) for v in args.variants.split(",")]
+    probe = ER.build_committed(recipe)
+    info = probe.info()
+    S = info["size"] * count
+    span, origin = bench.layout(info, count)
+    user = torch.randint(1, 255, (span,), dtype=torch.uint8, device=dev)
+    packed = torch.empty(S, dtype=torch.uint8, device=dev)
+    uptr = user.data_ptr() + origin
+    L = ompi_amd.lib()
+    res = {json.dumps(v): {"pack": [], "unpack": []} for v in variants}
+    for _ in range(args.rounds):
+        for v in variants:
+            for k, val in v.items():
+                L.ddt_tune(k.encode(), int(val))
+            dt = ER.build_committed(recipe)
+            cp, cu = ompi_amd.Convertor(), ompi_amd.Convertor()
+            st = torch.cuda.current_stream(dev)
+            cp.set_stream(st, True)
+            cu.set_stream(st, True)
+            evs = []
+            for i in range(args.steps + 3):
+                a, b, c = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                a.record()
+                cp.prepare_for_send(dt, count, uptr)
+                cp.pack([(packed, S)])
+                b.record()
+                cu.prepare_for_recv(dt, count, uptr)
+                cu.unpack([(packed, S)])
+                c.record()
+                if i >= 3:
+                    evs.append((a, b, c))
+            torch.cuda.synchronize()
+            r = res[json.dumps(v)]
+            r["pack"].append(statistics.median(a.elapsed_time(b) for a, b, _ in evs) * 1e3)
+            r["unpack"].append(statistics.median(b.elapsed_time(c) for _, b, c in evs) * 1e3)
+    for k, r in res.items():
+        p, u = statistics.median(r["pack"]), statistics.median(r["unpack"])
+        print(json.dumps({"config": args.config, "variant": json.loads(k), "pack_us": round(p, 1),
+                          "unpack_us": round(u, 1), "step_us": round(p + u, 1),
+                          "frac": round(4 * S / ((p + u) * 1e-6) / 8e12, 4),
+                          "pack_rounds": [round(x, 1) for x in r["pack"]],
+                          "unpack_rounds": [round(x, 1) for x in r["unpack"]]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
