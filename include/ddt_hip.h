@@ -207,7 +207,9 @@ int64_t ddt_type_plan_list(const ddt_datatype_t *type, size_t leaf, int64_t *dis
                            size_t cap);
 /* Tuning knobs for A/B measurements (affect descriptor sets built afterwards):
  * "nt" = user-side non-temporal gathers (-1 auto, 0 off, 1 on); "task_kb" = packed KiB per
- * workgroup (0 adaptive).  Environment: DDT_NT, DDT_TASK_KB. */
+ * workgroup (0 adaptive); "policy" = task sizing (0 v0, 1 per-leaf passes); "interleave" =
+ * reorder items in runs of this many tasks (0 off); "reset" = restore the defaults.
+ * Environment: DDT_NT, DDT_TASK_KB. */
 int ddt_tune(const char *key, long value);
 /* Library self-check of host-side index arithmetic (fast division); returns 0 on success. */
 int ddt_selftest(void);

@@ -685,6 +685,12 @@ int ddt_tune(const char *key, long value)
         tuning().nt = value < 0 ? -1 : (value ? 1 : 0);
     else if (k == "task_kb")
         tuning().task_kb = value;
+    else if (k == "interleave")
+        tuning().interleave = value;
+    else if (k == "policy")
+        tuning().policy = int(value);
+    else if (k == "reset")
+        tuning() = Tuning{};
     else
         return fail(DDT_ERR_BAD_PARAM, "unknown tuning key " + k);
     return DDT_SUCCESS;

@@ -14,6 +14,8 @@ namespace ddt {
 
 constexpr int MAXD = 8;             // affine dims per item, instance dim included
 constexpr int THREADS = 256;        // workgroup size (4 wave64)
+// units each thread loads before storing, per pass of the affine loop
+constexpr int unroll_of(uint32_t U) { return U >= 16 ? 4 : 8; }
 
 enum LeafKind : int { LEAF_AFFINE = 0, LEAF_LIST = 1 };
 

@@ -89,7 +89,7 @@ __device__ __forceinline__ void nest_offsets64(const Item *it, uint64_t blk, int
     }
 }
 
-template <int U> constexpr int unroll() { return U >= 16 ? 4 : 8; }
+template <int U> constexpr int unroll() { return unroll_of(U); }
 
 template <int U, int DIR>
 __device__ __noinline__ void run_affine64(const Item *it, uint64_t ub, uint64_t ue)

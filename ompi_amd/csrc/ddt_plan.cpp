@@ -515,24 +515,77 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
 
 void assign_tasks(std::vector<Item> &items)
 {
-    // Size tasks so the launch has ~6 K workgroups (24 per CU: enough waves in flight to
-    // cover HBM latency) but never tasks below 4 KiB or above 64 KiB of packed bytes.
     uint64_t total = 0;
     for (const Item &it : items)
         if (it.kind == ITEM_AFFINE || it.kind == ITEM_LIST_UNI)
             total += (it.u1 - it.u0) * it.U;
-    uint64_t tb = task_bytes_override();
-    if (tb == 0) {
-        tb = 4096;
-        while (tb < (64u << 10) && total / (tb * 2) >= 6144)
+    const uint64_t over = task_bytes_override();
+    if (tuning().policy == 0 || over) {
+        // v0 policy: ~6 K workgroups, tasks of 4..64 KiB of packed bytes.
+        uint64_t tb = over;
+        if (tb == 0) {
+            tb = 4096;
+            while (tb < (64u << 10) && total / (tb * 2) >= 6144)
+                tb *= 2;
+        }
+        for (Item &it : items)
+            if (it.kind == ITEM_AFFINE || it.kind == ITEM_LIST_UNI) {
+                uint64_t u = tb / it.U;
+                it.units_per_task = u < THREADS ? THREADS : u;
+            }
+    } else {
+        // ~1024 tasks (4 per CU) for the whole launch, 4..64 KiB each; a sparse affine
+        // leaf (blocks <= 64 B: one DRAM burst per unit) caps its task at ONE unrolled
+        // pass of the workgroup (THREADS*K units), a streaming leaf at four passes.
+        // Measured on the 6-face halo: 8 KiB tasks 99/82 us, 64 KiB 92/78 us, and the
+        // x-face alone is best at one pass (scripts/ab.py).
+        uint64_t tb = 4096;
+        while (tb < (64u << 10) && tb * 1024 < total)
             tb *= 2;
+        for (Item &it : items) {
+            if (it.kind != ITEM_AFFINE && it.kind != ITEM_LIST_UNI)
+                continue;
+            uint64_t cap = tb;
+            if (it.kind == ITEM_AFFINE) {
+                const uint64_t pass = uint64_t(THREADS) * unroll_of(it.U) * it.U;
+                const bool sparse = it.upb * it.U <= 64;
+                cap = pass * (sparse ? 1 : 4);
+            }
+            const uint64_t b = tb < cap ? tb : cap;
+            uint64_t u = b / it.U;
+            it.units_per_task = u < THREADS ? THREADS : u;
+        }
+    }
+    const long chunk = tuning().interleave;
+    if (chunk > 0 && items.size() > 1) {
+        // Split items into runs of `chunk` tasks and order the runs by their fractional
+        // position inside their item, so gather-bound and streaming leaves share the chip
+        // instead of running back to back.
+        struct Piece { double key; size_t seq; Item it; };
+        std::vector<Piece> pieces;
+        size_t seq = 0;
+        for (const Item &it : items) {
+            const uint64_t units = it.u1 - it.u0;
+            const uint64_t nt = (units + it.units_per_task - 1) / it.units_per_task;
+            const bool split = (it.kind == ITEM_AFFINE || it.kind == ITEM_LIST_UNI) && nt > uint64_t(chunk);
+            const uint64_t np = split ? (nt + chunk - 1) / chunk : 1;
+            for (uint64_t p = 0; p < np; ++p) {
+                Item c = it;
+                if (split) {
+                    c.u0 = it.u0 + p * chunk * it.units_per_task;
+                    c.u1 = std::min<uint64_t>(it.u1, c.u0 + chunk * it.units_per_task);
+                }
+                pieces.push_back({(p + 0.5) / double(np), seq++, c});
+            }
+        }
+        std::stable_sort(pieces.begin(), pieces.end(),
+                         [](const Piece &a, const Piece &b) { return a.key < b.key; });
+        items.clear();
+        for (Piece &p : pieces)
+            items.push_back(p.it);
     }
     uint32_t b = 0;
     for (Item &it : items) {
-        if (it.kind == ITEM_AFFINE || it.kind == ITEM_LIST_UNI) {
-            uint64_t u = tb / it.U;
-            it.units_per_task = u < THREADS ? THREADS : u;
-        }
         uint64_t units = it.u1 - it.u0;
         uint64_t nt = (units + it.units_per_task - 1) / it.units_per_task;
         it.task_begin = b;

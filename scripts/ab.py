@@ -26,9 +26,21 @@ def main():
     ap.add_argument("--variants", default="nt=-1,nt=0,nt=1")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--mode", default="pair", choices=["pair", "pack", "unpack"],
+                    help="pair = pack then unpack per step; pack/unpack = that direction only")
+    ap.add_argument("--prewarm", type=float, default=0.0, help="seconds of HBM copies first")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    recipe, count, _ = bench.make_workload(args.config)
+    faces = bench.face_recipes()
+    n, field = 256, 256 ** 3 * 8
+    xf, yf = faces["x"][1], faces["y"][1]
+    faces["xx"] = ("resized", ("struct", [1, 1], [0, (n - 1) * 8], [xf, xf]), 0, field)
+    faces["yz"] = ("resized", ("struct", [1, 1, 1, 1], [0, (n - 1) * n * 8, 0, (n - 1) * n * n * 8],
+                               [yf, yf, faces["z"][1], faces["z"][1]]), 0, field)
+    if args.config in faces:
+        recipe, count = faces[args.config], 16
+    else:
+        recipe, count, _ = bench.make_workload(args.config)
     variants = [dict(kv.split("=") for kv in v.split(";")) for v in args.variants.split(",")]
     probe = ER.build_committed(recipe)
     info = probe.info()
@@ -38,9 +50,19 @@ def main():
     packed = torch.empty(S, dtype=torch.uint8, device=dev)
     uptr = user.data_ptr() + origin
     L = ompi_amd.lib()
+    if args.prewarm > 0:
+        import time
+        a = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+        b = torch.empty_like(a)
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < args.prewarm:
+            b.copy_(a)
+            torch.cuda.synchronize()
+        del a, b
     res = {json.dumps(v): {"pack": [], "unpack": []} for v in variants}
     for _ in range(args.rounds):
         for v in variants:
+            L.ddt_tune(b"reset", 0)
             for k, val in v.items():
                 L.ddt_tune(k.encode(), int(val))
             dt = ER.build_committed(recipe)
@@ -52,11 +74,13 @@ def main():
             for i in range(args.steps + 3):
                 a, b, c = (torch.cuda.Event(enable_timing=True) for _ in range(3))
                 a.record()
-                cp.prepare_for_send(dt, count, uptr)
-                cp.pack([(packed, S)])
+                if args.mode != "unpack":
+                    cp.prepare_for_send(dt, count, uptr)
+                    cp.pack([(packed, S)])
                 b.record()
-                cu.prepare_for_recv(dt, count, uptr)
-                cu.unpack([(packed, S)])
+                if args.mode != "pack":
+                    cu.prepare_for_recv(dt, count, uptr)
+                    cu.unpack([(packed, S)])
                 c.record()
                 if i >= 3:
                     evs.append((a, b, c))

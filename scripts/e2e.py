@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""End-to-end rate with a HOST-resident packed stream (SURVEY.md §8d "End-to-end"):
+pack e2e = pack kernel + D2H into pinned host memory; unpack e2e = H2D from pinned host
++ unpack kernel.  Two schedules:
+  serialized -- whole-message kernel into an HBM buffer, then one hipMemcpy (and reverse);
+  overlapped -- the convertor's own host-iovec path: 16 MiB chunks double-buffered through
+                two HBM staging slots on a copy stream (ddt_convertor.cpp, ensure_staging).
+Also prints the plain pinned copy rates, the PCIe ceiling both schedules sit under."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import ompi_amd  # noqa: E402
+from ompi_amd import recipe as ER  # noqa: E402
+import bench  # noqa: E402
+
+GiB = float(1 << 30)
+
+
+def timed(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    recipe, count, desc = bench.make_workload(args.config)
+    dt = ER.build_committed(recipe)
+    info = dt.info()
+    S = info["size"] * count
+    span, origin = bench.layout(info, count)
+    user = torch.randint(1, 255, (span,), dtype=torch.uint8, device=dev)
+    uptr = user.data_ptr() + origin
+    dpk = torch.empty(S, dtype=torch.uint8, device=dev)
+    hpk = torch.empty(S, dtype=torch.uint8, pin_memory=True)
+    st = torch.cuda.current_stream(dev)
+    cp, cu = ompi_amd.Convertor(), ompi_amd.Convertor()
+    for c in (cp, cu):
+        c.set_stream(st, True)
+
+    def pack_dev():
+        cp.prepare_for_send(dt, count, uptr)
+        cp.pack([(dpk, S)])
+
+    def unpack_dev():
+        cu.prepare_for_recv(dt, count, uptr)
+        cu.unpack([(dpk, S)])
+
+    def pack_ser():
+        pack_dev()
+        hpk.copy_(dpk, non_blocking=True)
+
+    def unpack_ser():
+        dpk.copy_(hpk, non_blocking=True)
+        unpack_dev()
+
+    def pack_ovl():
+        cp.prepare_for_send(dt, count, uptr)
+        cp.pack([(hpk.data_ptr(), S)])
+
+    def unpack_ovl():
+        cu.prepare_for_recv(dt, count, uptr)
+        cu.unpack([(hpk.data_ptr(), S)])
+
+    r = args.reps
+    t = {k: timed(f, r) for k, f in (("pack_kernel", pack_dev), ("unpack_kernel", unpack_dev),
+                                     ("pack_serialized", pack_ser), ("unpack_serialized", unpack_ser),
+                                     ("pack_overlapped", pack_ovl), ("unpack_overlapped", unpack_ovl),
+                                     ("d2h_copy", lambda: hpk.copy_(dpk, non_blocking=True)),
+                                     ("h2d_copy", lambda: dpk.copy_(hpk, non_blocking=True)))}
+    # the overlapped path must produce the same stream as the device path
+    pack_dev()
+    ref = dpk.clone()
+    pack_ovl()
+    torch.cuda.synchronize()
+    same = bool(torch.equal(ref.cpu(), hpk))
+    out = {"config": args.config, "workload": desc["workload"], "packed_bytes": S,
+           "overlapped_matches_device_path": same,
+           "GiBs": {k: round(S / v / GiB, 2) for k, v in t.items()},
+           "us": {k: round(v * 1e6, 1) for k, v in t.items()},
+           "pack+unpack_GiBs": {
+               "device_resident": round(2 * S / (t["pack_kernel"] + t["unpack_kernel"]) / GiB, 2),
+               "serialized": round(2 * S / (t["pack_serialized"] + t["unpack_serialized"]) / GiB, 2),
+               "overlapped": round(2 * S / (t["pack_overlapped"] + t["unpack_overlapped"]) / GiB, 2)}}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -155,3 +155,23 @@ def _overlap(o, count):
                     return True
                 seen.add(x)
     return False
+
+
+@pytest.mark.parametrize("chunk", [1, 3])
+def test_interleaved_task_order_matches_oracle(chunk):
+    """ddt_tune("interleave") splits items into task runs and reorders them; every byte
+    must still move exactly once to the oracle's packed position."""
+    from ompi_amd import lib
+    L = lib()
+    L.ddt_tune(b"interleave", chunk)
+    L.ddt_tune(b"task_kb", 1)
+    try:
+        rng = random.Random(900 + chunk)
+        for n in range(60):
+            b = R.Built(R.random_recipe(rng))
+            if b.o.info()["size"] == 0:
+                continue
+            _check_windows(b, rng, seed=n)
+    finally:
+        L.ddt_tune(b"interleave", 0)
+        L.ddt_tune(b"task_kb", 0)
