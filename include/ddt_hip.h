@@ -144,6 +144,33 @@ int ddt_convertor_prepare_for_send(ddt_convertor_t *conv, const ddt_datatype_t *
 /* opal_convertor_prepare_for_recv (opal_convertor.c:616-646) */
 int ddt_convertor_prepare_for_recv(ddt_convertor_t *conv, const ddt_datatype_t *type, size_t count,
                                    void *buf);
+/* external32 data representation: MPI_Pack_external / MPI_Unpack_external /
+ * MPI_Pack_external_size (ompi_datatype_external.c:33-135 over the external32 convertor
+ * of ompi_datatype_external32.c:35-38).  Big-endian elements; MPI_LONG / MPI_UNSIGNED_LONG
+ * travel as 4 bytes; long double types are refused (DDT_ERR_NOT_SUPPORTED).  The user
+ * buffer must be device memory; the external buffer may be device or host memory.
+ * `datarep` is accepted and ignored, as in the reference.  Synchronous. */
+int ddt_pack_external_size(const char *datarep, size_t incount, const ddt_datatype_t *type,
+                           ptrdiff_t *size);
+int ddt_pack_external(const char *datarep, const void *inbuf, size_t incount,
+                      const ddt_datatype_t *type, void *outbuf, ptrdiff_t outsize,
+                      ptrdiff_t *position);
+int ddt_unpack_external(const char *datarep, const void *inbuf, ptrdiff_t insize,
+                        ptrdiff_t *position, void *outbuf, size_t outcount,
+                        const ddt_datatype_t *type);
+
+/* Raw iovec export: opal_convertor_raw (opal_convertor_raw.c:65-283, prototype
+ * opal_convertor.h:352-354).  Fills iov[0..*iov_count) with the user-memory regions of the
+ * type map in type-map order from the current position, merging adjacent regions
+ * (opal_convertor_merge_iov :41-58); stops before a region that needs one more iovec.
+ * *length = bytes described.  Returns 1 when the whole message has been described, else 0.
+ * No data moves, so the buffer may be host, device or NULL (the reference's callers prepare
+ * on NULL: ddt_raw2.c:45).  ddt_convertor_prepare_for_raw is prepare_for_send without the
+ * accelerator check. */
+int ddt_convertor_prepare_for_raw(ddt_convertor_t *conv, const ddt_datatype_t *type, size_t count,
+                                  const void *buf);
+int32_t ddt_convertor_raw(ddt_convertor_t *conv, struct iovec *iov, uint32_t *iov_count,
+                          size_t *length);
 /* opal_convertor_pack (opal_convertor.c:255-305): fAdvance slot = opal_pack_accelerator_simple
  * (opal_datatype_pack_accelerator.c:161-295).  Never splits a predefined element. */
 int32_t ddt_convertor_pack(ddt_convertor_t *conv, struct iovec *iov, uint32_t *out_size,

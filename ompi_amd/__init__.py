@@ -7,7 +7,9 @@ datatype + convertor interface.  This package is the Python mirror of that inter
 from ._lib import DDTError, LIB_PATH, lib  # noqa: F401
 from . import datatype, convertor  # noqa: F401
 from .datatype import MPI, Datatype  # noqa: F401
-from .convertor import Convertor, pack, unpack, pack_size  # noqa: F401
+from .convertor import (Convertor, pack, unpack, pack_size, pack_external,  # noqa: F401
+                        unpack_external, pack_external_size)
 
 __all__ = ["lib", "LIB_PATH", "DDTError", "datatype", "convertor", "MPI", "Datatype",
-           "Convertor", "pack", "unpack", "pack_size"]
+           "Convertor", "pack", "unpack", "pack_size", "pack_external", "unpack_external",
+           "pack_external_size"]

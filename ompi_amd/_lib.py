@@ -55,6 +55,13 @@ SIGNATURES = {
     "ddt_convertor_prepare_for_recv": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "ddt_convertor_pack": (c_int32, [c_void_p, P(IOVec), P(c_uint32), P(c_size_t)]),
     "ddt_convertor_unpack": (c_int32, [c_void_p, P(IOVec), P(c_uint32), P(c_size_t)]),
+    "ddt_pack_external_size": (c_int, [ctypes.c_char_p, c_size_t, c_void_p, P(c_ssize_t)]),
+    "ddt_pack_external": (c_int, [ctypes.c_char_p, c_void_p, c_size_t, c_void_p, c_void_p,
+                                  c_ssize_t, P(c_ssize_t)]),
+    "ddt_unpack_external": (c_int, [ctypes.c_char_p, c_void_p, c_ssize_t, P(c_ssize_t), c_void_p,
+                                    c_size_t, c_void_p]),
+    "ddt_convertor_prepare_for_raw": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "ddt_convertor_raw": (c_int32, [c_void_p, P(IOVec), P(c_uint32), P(c_size_t)]),
     "ddt_convertor_set_position": (c_int, [c_void_p, P(c_size_t)]),
     "ddt_convertor_get_packed_size": (c_int, [c_void_p, P(c_size_t)]),
     "ddt_convertor_get_position": (c_int, [c_void_p, P(c_size_t)]),

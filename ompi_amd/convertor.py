@@ -60,6 +60,23 @@ class Convertor:
               "ddt_convertor_prepare_for_recv")
         return self
 
+    def prepare_for_raw(self, dt: Datatype, count: int, buf) -> "Convertor":
+        """prepare_for_send without the device check: raw export needs no data."""
+        check(lib().ddt_convertor_prepare_for_raw(self.h, dt.handle, count, addr(buf)),
+              "ddt_convertor_prepare_for_raw")
+        return self
+
+    def raw(self, max_iov: int):
+        """opal_convertor_raw: (1 if the whole message is described else 0,
+        [(address, length)] of user memory in type-map order, bytes described)."""
+        arr = (IOVec * max(max_iov, 1))()
+        n = ctypes.c_uint32(max_iov)
+        length = ctypes.c_size_t(0)
+        rc = check(lib().ddt_convertor_raw(self.h, arr, ctypes.byref(n), ctypes.byref(length)),
+                   "ddt_convertor_raw")
+        return rc, [(int(arr[i].iov_base or 0), int(arr[i].iov_len)) for i in range(n.value)], \
+            int(length.value)
+
     def set_stream(self, stream, async_: bool = True) -> None:
         check(lib().ddt_convertor_set_stream(self.h, stream_handle(stream), int(async_)),
               "ddt_convertor_set_stream")
@@ -146,3 +163,30 @@ def copy_content_same_ddt(dt: Datatype, count: int, dst, src, stream=None) -> No
     """opal_datatype_copy_content_same_ddt: typed device-to-device copy in one launch."""
     check(lib().ddt_copy_content_same_ddt(dt.handle, count, addr(dst), addr(src),
                                           stream_handle(stream)), "ddt_copy_content_same_ddt")
+
+
+# ------------------------------------------------------------------ external32
+def pack_external_size(incount: int, dt: Datatype, datarep: str = "external32") -> int:
+    """MPI_Pack_external_size."""
+    s = ctypes.c_ssize_t()
+    check(lib().ddt_pack_external_size(datarep.encode(), incount, dt.handle, ctypes.byref(s)),
+          "ddt_pack_external_size")
+    return int(s.value)
+
+
+def pack_external(inbuf, incount: int, dt: Datatype, outbuf, outsize: int, position: int = 0,
+                  datarep: str = "external32") -> int:
+    """MPI_Pack_external (big-endian external32 stream): returns the new position."""
+    p = ctypes.c_ssize_t(position)
+    check(lib().ddt_pack_external(datarep.encode(), addr(inbuf), incount, dt.handle, addr(outbuf),
+                                  outsize, ctypes.byref(p)), "ddt_pack_external")
+    return int(p.value)
+
+
+def unpack_external(inbuf, insize: int, position: int, outbuf, outcount: int, dt: Datatype,
+                    datarep: str = "external32") -> int:
+    """MPI_Unpack_external: returns the new position."""
+    p = ctypes.c_ssize_t(position)
+    check(lib().ddt_unpack_external(datarep.encode(), addr(inbuf), insize, ctypes.byref(p),
+                                    addr(outbuf), outcount, dt.handle), "ddt_unpack_external")
+    return int(p.value)

@@ -386,6 +386,146 @@ int ddt_convertor_set_position(ddt_convertor_t *c, size_t *position)
     return DDT_SUCCESS;
 }
 
+namespace {
+
+// opal_convertor_merge_iov (opal_convertor_raw.c:41-58): extend the current iovec when the
+// piece starts where it ends, otherwise open the next one; a piece that needs an iovec
+// beyond the caller's array is not consumed.
+struct RawOut {
+    struct iovec *iov;
+    uint32_t cap;
+    uint32_t idx = 0;
+    uint64_t total = 0;
+    bool piece(uint64_t addr, uint64_t len)
+    {
+        if (len == 0)
+            return true;
+        struct iovec &cur = iov[idx];
+        if (cur.iov_len != 0) {
+            if (addr == uint64_t(uintptr_t(cur.iov_base)) + cur.iov_len) {
+                cur.iov_len += len;
+                total += len;
+                return true;
+            }
+            if (++idx == cap)
+                return false;
+        }
+        iov[idx].iov_base = reinterpret_cast<void *>(uintptr_t(addr));
+        iov[idx].iov_len = len;
+        total += len;
+        return true;
+    }
+};
+
+// Emit the user-memory pieces of `nodes` (one type-map level at `base`) in type-map order,
+// starting `skip` packed bytes in.  Returns false once the iovec array is full.
+bool raw_walk(const std::vector<Node> &nodes, uint64_t base, uint64_t skip, RawOut &o)
+{
+    for (const Node &n : nodes) {
+        const uint64_t sz = n.packed_bytes();
+        if (skip >= sz) {
+            skip -= sz;
+            continue;
+        }
+        switch (n.kind) {
+        case Node::DATA: {
+            uint64_t k = skip / n.blen, off = skip % n.blen;
+            for (; k < n.count; ++k, off = 0)
+                if (!o.piece(base + uint64_t(n.disp + int64_t(k) * n.extent) + off, n.blen - off))
+                    return false;
+            break;
+        }
+        case Node::LOOP: {
+            uint64_t k = skip / n.body_size, rem = skip % n.body_size;
+            for (; k < n.count; ++k, rem = 0)
+                if (!raw_walk(n.body, base + uint64_t(int64_t(k) * n.extent), rem, o))
+                    return false;
+            break;
+        }
+        case Node::LIST: {
+            const IndexList &X = *n.list;
+            const size_t nb = X.nblk();
+            size_t b;
+            uint64_t off;
+            if (X.len.empty()) {
+                b = size_t(skip / X.ulen);
+                off = skip % X.ulen;
+            } else {
+                b = size_t(std::upper_bound(X.poff.begin(), X.poff.begin() + long(nb), skip) - X.poff.begin()) - 1;
+                off = skip - X.poff[b];
+            }
+            for (; b < nb; ++b, off = 0) {
+                const uint64_t len = X.len.empty() ? X.ulen : X.len[b];
+                if (off >= len)
+                    continue;
+                if (!o.piece(base + uint64_t(n.disp + X.disp[b]) + off, len - off))
+                    return false;
+            }
+            break;
+        }
+        }
+        skip = 0;
+    }
+    return true;
+}
+
+}  // namespace
+
+int ddt_convertor_prepare_for_raw(ddt_convertor_t *c, const ddt_datatype_t *t, size_t count,
+                                  const void *buf)
+{
+    // the reference prepares a send convertor on a NULL or host base for raw export
+    // (ddt_raw2.c:45, common_ompio_file_open.c:860-873): address arithmetic only, so no
+    // device check and no plan
+    if (!c || !t)
+        return fail(DDT_ERR_BAD_PARAM, "null convertor or datatype");
+    if (!(t->flags & F_COMMITTED))
+        return fail(DDT_ERR_NOT_COMMITTED, "datatype not committed");
+    c->dt = const_cast<ddt_datatype *>(t);
+    c->count = count;
+    c->base = uint64_t(uintptr_t(buf));
+    c->send = true;
+    c->local_size = uint64_t(t->size) * count;
+    c->bConverted = 0;
+    c->completed = (c->local_size == 0);
+    c->prepared = true;
+    return DDT_SUCCESS;
+}
+
+int32_t ddt_convertor_raw(ddt_convertor_t *c, struct iovec *iov, uint32_t *iov_count, size_t *length)
+{
+    // opal_convertor_raw (opal_convertor_raw.c:65-283)
+    if (!c || !c->prepared || !iov_count || !length || (*iov_count && !iov))
+        return fail(DDT_ERR_BAD_PARAM, "convertor not prepared or bad iovec");
+    if (c->completed || *iov_count == 0) {
+        if (*iov_count) {
+            iov[0].iov_base = nullptr;
+            iov[0].iov_len = 0;
+        }
+        *iov_count = 0;
+        *length = 0;
+        return c->completed ? 1 : 0;
+    }
+    const ddt_datatype *t = c->dt;
+    RawOut o{iov, *iov_count};
+    iov[0].iov_len = 0;
+    const uint64_t size = uint64_t(t->size);
+    const int64_t ext = t->extent();
+    bool room = true;
+    for (uint64_t i = c->bConverted / size; room && i < c->count; ++i) {
+        const uint64_t skip = i == c->bConverted / size ? c->bConverted % size : 0;
+        room = raw_walk(t->opt, c->base + uint64_t(int64_t(i) * ext), skip, o);
+    }
+    c->bConverted += o.total;
+    *length = size_t(o.total);
+    *iov_count = room ? (iov[o.idx].iov_len ? o.idx + 1 : o.idx) : o.cap;
+    if (c->bConverted == c->local_size) {
+        c->completed = true;
+        return 1;
+    }
+    return 0;
+}
+
 int ddt_convertor_get_packed_size(const ddt_convertor_t *c, size_t *size)
 {
     if (!c || !size)
@@ -468,6 +608,127 @@ int ddt_unpack(const void *inbuf, size_t insize, size_t *position, void *outbuf,
     if (r < 0)
         return r;
     *position += max_data;
+    return DDT_SUCCESS;
+}
+
+// ---------------------------------------------------------------- external32
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    ~DevBuf() { if (p) (void) hipFree(p); }
+};
+
+int ext_plan_for(const ddt_datatype_t *t, std::shared_ptr<ExtPlan> &X)
+{
+    if (!t)
+        return fail(DDT_ERR_BAD_PARAM, "null datatype");
+    if (!(t->flags & F_COMMITTED))
+        return fail(DDT_ERR_NOT_COMMITTED, "datatype not committed");
+    X = get_ext_plan(const_cast<ddt_datatype *>(t));
+    if (X->error)
+        return fail(X->error, X->what);
+    return DDT_SUCCESS;
+}
+
+}  // namespace
+
+int ddt_pack_external_size(const char *datarep, size_t incount, const ddt_datatype_t *t,
+                           ptrdiff_t *size)
+{
+    // ompi_datatype_pack_external_size (ompi_datatype_external.c:115-135)
+    (void) datarep;
+    if (!size)
+        return fail(DDT_ERR_BAD_PARAM, "null size");
+    std::shared_ptr<ExtPlan> X;
+    int rc = ext_plan_for(t, X);
+    if (rc != DDT_SUCCESS)
+        return rc;
+    *size = ptrdiff_t(incount * X->Se);
+    return DDT_SUCCESS;
+}
+
+int ddt_pack_external(const char *datarep, const void *inbuf, size_t incount,
+                      const ddt_datatype_t *t, void *outbuf, ptrdiff_t outsize, ptrdiff_t *position)
+{
+    // ompi_datatype_pack_external (ompi_datatype_external.c:33-70): native pack into HBM,
+    // then one conversion launch into the external32 stream
+    (void) datarep;
+    if (!position || *position < 0 || outsize < 0 || (!outbuf && outsize))
+        return fail(DDT_ERR_BAD_PARAM, "bad argument");
+    std::shared_ptr<ExtPlan> X;
+    int rc = ext_plan_for(t, X);
+    if (rc != DDT_SUCCESS)
+        return rc;
+    const uint64_t need = incount * X->Se, native = incount * uint64_t(t->size);
+    if (uint64_t(*position) + need > uint64_t(outsize))
+        return fail(DDT_ERR_TRUNCATE, "output buffer too small");
+    if (need == 0)
+        return DDT_SUCCESS;
+    if ((rc = ext_upload(*X)) != DDT_SUCCESS)
+        return fail(rc, "external32 table upload");
+    DevBuf tn, te;
+    HIPCHK(hipMalloc(&tn.p, native));
+    ddt_convertor c;
+    if ((rc = prepare(&c, t, incount, inbuf, true)) != DDT_SUCCESS)
+        return rc;
+    struct iovec iov{tn.p, native};
+    uint32_t n = 1;
+    size_t md = 0;
+    if ((rc = advance(&c, &iov, &n, &md, 0)) < 0)
+        return rc;
+    char *dst = static_cast<char *>(outbuf) + *position;
+    const bool dev_out = classify(dst) == MEM_DEVICE;
+    if (!dev_out)
+        HIPCHK(hipMalloc(&te.p, need));
+    HIPCHK(launch_ext(X->d_segs, uint32_t(X->segs.size()), X->d_runs, X->E, incount,
+                      uint64_t(t->size), X->Se, tn.p, dev_out ? dst : te.p, 0, nullptr));
+    if (!dev_out)
+        HIPCHK(hipMemcpy(dst, te.p, need, hipMemcpyDeviceToHost));
+    HIPCHK(hipStreamSynchronize(nullptr));
+    *position += ptrdiff_t(need);
+    return DDT_SUCCESS;
+}
+
+int ddt_unpack_external(const char *datarep, const void *inbuf, ptrdiff_t insize,
+                        ptrdiff_t *position, void *outbuf, size_t outcount, const ddt_datatype_t *t)
+{
+    // ompi_datatype_unpack_external (ompi_datatype_external.c:72-113)
+    (void) datarep;
+    if (!position || *position < 0 || insize < 0 || (!inbuf && insize))
+        return fail(DDT_ERR_BAD_PARAM, "bad argument");
+    std::shared_ptr<ExtPlan> X;
+    int rc = ext_plan_for(t, X);
+    if (rc != DDT_SUCCESS)
+        return rc;
+    const uint64_t need = outcount * X->Se, native = outcount * uint64_t(t->size);
+    if (uint64_t(*position) + need > uint64_t(insize))
+        return fail(DDT_ERR_TRUNCATE, "input buffer too small");
+    if (need == 0)
+        return DDT_SUCCESS;
+    if ((rc = ext_upload(*X)) != DDT_SUCCESS)
+        return fail(rc, "external32 table upload");
+    ddt_convertor c;
+    if ((rc = prepare(&c, t, outcount, outbuf, false)) != DDT_SUCCESS)
+        return rc;
+    const char *src = static_cast<const char *>(inbuf) + *position;
+    DevBuf tn, te;
+    const bool dev_in = classify(src) == MEM_DEVICE;
+    if (!dev_in) {
+        HIPCHK(hipMalloc(&te.p, need));
+        HIPCHK(hipMemcpy(te.p, src, need, hipMemcpyHostToDevice));
+    }
+    HIPCHK(hipMalloc(&tn.p, native));
+    HIPCHK(launch_ext(X->d_segs, uint32_t(X->segs.size()), X->d_runs, X->E, outcount,
+                      uint64_t(t->size), X->Se, tn.p, dev_in ? const_cast<char *>(src) : te.p, 1,
+                      nullptr));
+    HIPCHK(hipStreamSynchronize(nullptr));
+    struct iovec iov{tn.p, native};
+    uint32_t n = 1;
+    size_t md = 0;
+    if ((rc = advance(&c, &iov, &n, &md, 1)) < 0)
+        return rc;
+    *position += ptrdiff_t(need);
     return DDT_SUCCESS;
 }
 

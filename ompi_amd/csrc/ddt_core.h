@@ -57,6 +57,7 @@ struct IndexList {
 struct Node {
     enum Kind : uint8_t { DATA, LOOP, LIST } kind = DATA;
     int64_t esize = 1;      // DATA/LIST: basic element size
+    uint16_t tid = 0;       // DATA/LIST: OPAL id of the elements (0 = mixed, after commit merges)
     uint64_t count = 1;     // DATA: blocks; LOOP: iterations
     uint64_t blen = 0;      // DATA: bytes per block
     int64_t extent = 0;     // DATA: block stride; LOOP: iteration stride
@@ -111,6 +112,8 @@ struct ItemSet {
     ~ItemSet();
 };
 
+struct ExtPlan;
+
 struct Plan {
     std::vector<Leaf> leaves;
     std::vector<DevList> dev;     // one per LIST leaf (index in Leaf order, others empty)
@@ -137,6 +140,7 @@ struct ddt_datatype {
     std::vector<uint64_t> opt_prefix;  // packed offset of each top-level opt node
     std::mutex plan_mu;
     std::shared_ptr<ddt::Plan> plan;
+    std::shared_ptr<ddt::ExtPlan> ext;   // external32 signature (lazy)
     int64_t extent() const { return ub - lb; }
 };
 

@@ -97,4 +97,25 @@ struct ItemBlock {
 static_assert(sizeof(Item) == 512, "Item layout is shared with tests/plan_emu.py");
 static_assert(sizeof(ItemBlock) <= 4096, "kernel argument segment limit");
 
+// ---- external32 conversion (ddt_external.cpp, ddt_ext_kernel) ----
+enum ConvKind : uint32_t { CONV_COPY = 0, CONV_SWAP = 1, CONV_LONG = 2, CONV_ULONG = 3 };
+
+// `n` consecutive elements of one basic type inside a segment body.
+struct ConvRun {
+    uint64_t e0;            // index of the first element within the body
+    uint64_t noff, eoff;    // byte offset of the first element in the body: native / external
+    uint32_t nsz, esz;      // element bytes: native / external
+    uint32_t comp;          // byte-swap unit (component size for complex types)
+    uint32_t kind;          // ConvKind
+};
+
+// `reps` repetitions of a body of runs, consecutive in both streams.
+struct ConvSeg {
+    uint64_t e0;            // index of the first element within one instance
+    uint64_t reps, body_elems;
+    uint64_t nbase, ebase;  // byte offset of the segment within one instance
+    uint64_t nbody, ebody;  // bytes per repetition
+    uint32_t run0, nruns;
+};
+
 }  // namespace ddt

@@ -469,4 +469,104 @@ hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, in
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- external32
+// One thread per basic element of the type signature: locate the element's segment and
+// run (binary searches over tiny tables), then move it between the native packed stream
+// and the big-endian external32 stream (opal_copy_functions_heterogeneous.c semantics,
+// see ddt_external.cpp).  DIR 0 = native -> external (pack), 1 = external -> native.
+template <typename T> __device__ __forceinline__ T bswap(T v);
+template <> __device__ __forceinline__ uint16_t bswap(uint16_t v) { return __builtin_bswap16(v); }
+template <> __device__ __forceinline__ uint32_t bswap(uint32_t v) { return __builtin_bswap32(v); }
+template <> __device__ __forceinline__ uint64_t bswap(uint64_t v) { return __builtin_bswap64(v); }
+
+template <typename T>
+__device__ __forceinline__ bool swap_words(const uint8_t *from, uint8_t *to, uint32_t n)
+{
+    if ((reinterpret_cast<uintptr_t>(from) | reinterpret_cast<uintptr_t>(to)) % sizeof(T))
+        return false;
+    for (uint32_t b = 0; b < n; b += sizeof(T))
+        *reinterpret_cast<T *>(to + b) = bswap(*reinterpret_cast<const T *>(from + b));
+    return true;
+}
+
+template <int DIR>
+__device__ __forceinline__ void convert_elem(const ConvRun &r, const uint8_t *from, uint8_t *to)
+{
+    if (r.kind == CONV_LONG || r.kind == CONV_ULONG) {
+        // external 4 big-endian bytes <-> native 8 little-endian bytes
+        for (int k = 0; k < 4; ++k)
+            to[k] = from[3 - k];
+        if (DIR == 1) {
+            const uint8_t fill = (r.kind == CONV_LONG && (from[0] & 0x80)) ? 0xFF : 0x00;
+            for (int k = 4; k < 8; ++k)
+                to[k] = fill;
+        }
+        return;
+    }
+    const uint32_t n = r.nsz;
+    if (r.kind == CONV_COPY || r.comp == 1) {
+        for (uint32_t b = 0; b < n; ++b)
+            to[b] = from[b];
+        return;
+    }
+    const uint32_t c = r.comp;
+    if (c == 8 && swap_words<uint64_t>(from, to, n)) return;
+    if (c == 4 && swap_words<uint32_t>(from, to, n)) return;
+    if (c == 2 && swap_words<uint16_t>(from, to, n)) return;
+    for (uint32_t base = 0; base < n; base += c)
+        for (uint32_t k = 0; k < c; ++k)
+            to[base + k] = from[base + c - 1 - k];
+}
+
+template <int DIR>
+__global__ __launch_bounds__(THREADS) void ddt_ext_kernel(const ConvSeg *__restrict__ segs, uint32_t nseg,
+                                                          const ConvRun *__restrict__ runs,
+                                                          uint64_t E, uint64_t total, uint64_t Sn,
+                                                          uint64_t Se, uint8_t *native, uint8_t *ext)
+{
+    const uint64_t stride = uint64_t(gridDim.x) * THREADS;
+    for (uint64_t g = uint64_t(blockIdx.x) * THREADS + threadIdx.x; g < total; g += stride) {
+        const uint64_t inst = g / E, r = g - inst * E;
+        uint32_t lo = 0, hi = nseg - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (segs[mid].e0 <= r) lo = mid; else hi = mid - 1;
+        }
+        const ConvSeg &s = segs[lo];
+        const uint64_t local = r - s.e0;
+        const uint64_t rep = local / s.body_elems, k = local - rep * s.body_elems;
+        uint32_t a = s.run0, b = s.run0 + s.nruns - 1;
+        while (a < b) {
+            const uint32_t mid = (a + b + 1) >> 1;
+            if (runs[mid].e0 <= k) a = mid; else b = mid - 1;
+        }
+        const ConvRun ru = runs[a];
+        const uint64_t j = k - ru.e0;
+        uint8_t *np = native + inst * Sn + s.nbase + rep * s.nbody + ru.noff + j * ru.nsz;
+        uint8_t *ep = ext + inst * Se + s.ebase + rep * s.ebody + ru.eoff + j * ru.esz;
+        if (DIR == 0) convert_elem<0>(ru, np, ep);
+        else convert_elem<1>(ru, ep, np);
+    }
+}
+
+hipError_t launch_ext(const ConvSeg *segs, uint32_t nseg, const ConvRun *runs, uint64_t E,
+                      uint64_t count, uint64_t Sn, uint64_t Se, void *native, void *ext, int dir,
+                      hipStream_t stream)
+{
+    const uint64_t total = E * count;
+    if (total == 0 || nseg == 0)
+        return hipSuccess;
+    uint64_t blocks = (total + THREADS - 1) / THREADS;
+    if (blocks > (1u << 16))
+        blocks = 1u << 16;   // grid-stride beyond 16 M threads (64 waves per CU)
+    uint8_t *n8 = static_cast<uint8_t *>(native), *e8 = static_cast<uint8_t *>(ext);
+    if (dir == 0)
+        hipLaunchKernelGGL((ddt_ext_kernel<0>), dim3(uint32_t(blocks)), dim3(THREADS), 0, stream,
+                           segs, nseg, runs, E, total, Sn, Se, n8, e8);
+    else
+        hipLaunchKernelGGL((ddt_ext_kernel<1>), dim3(uint32_t(blocks)), dim3(THREADS), 0, stream,
+                           segs, nseg, runs, E, total, Sn, Se, n8, e8);
+    return hipGetLastError();
+}
+
 }  // namespace ddt

@@ -2,6 +2,8 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
+#include <string>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -29,5 +31,25 @@ hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bo
                               hipStream_t stream);
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
                        hipStream_t stream);
+
+// external32 conversion between a native packed stream and its big-endian form.
+hipError_t launch_ext(const ConvSeg *segs, uint32_t nseg, const ConvRun *runs, uint64_t E,
+                      uint64_t count, uint64_t Sn, uint64_t Se, void *native, void *ext, int dir,
+                      hipStream_t stream);
+
+// ddt_external.cpp: the external32 signature of a committed type (built once, cached).
+struct ExtPlan {
+    std::vector<ConvSeg> segs;
+    std::vector<ConvRun> runs;
+    uint64_t E = 0;      // elements per instance
+    uint64_t Se = 0;     // external bytes per instance
+    ConvSeg *d_segs = nullptr;
+    ConvRun *d_runs = nullptr;
+    int error = 0;       // DDT_ERR_* when the type has no external32 form
+    std::string what;
+    ~ExtPlan();
+};
+std::shared_ptr<ExtPlan> get_ext_plan(ddt_datatype *t);
+int ext_upload(ExtPlan &X);
 
 }  // namespace ddt

@@ -45,6 +45,7 @@ void init_predefined()
         Node n;
         n.kind = Node::DATA;
         n.esize = kSize[id];
+        n.tid = uint16_t(id);
         n.count = 1;
         n.blen = uint64_t(kSize[id]);
         n.extent = kSize[id];
@@ -170,6 +171,7 @@ void type_add(ddt_datatype *base, const ddt_datatype *add, uint64_t count, int64
         Node n;
         n.kind = Node::DATA;
         n.esize = add->size;
+        n.tid = add->id;
         n.disp = disp;
         if (extent == add->size) {
             n.count = 1;
@@ -332,6 +334,7 @@ ddt_datatype *build_indexed(const std::vector<Block> &blocks, const ddt_datatype
         Node n;
         n.kind = Node::LIST;
         n.esize = L->esize;
+        n.tid = old->desc[0].tid;
         n.list = finish_list(L);
         t->desc.push_back(std::move(n));
     } else {
@@ -391,9 +394,11 @@ bool try_merge(Node &a, const Node &b)
         return false;
     if (a.disp + int64_t(a.blen) != b.disp)
         return false;
+    const uint16_t tid = a.tid == b.tid ? a.tid : 0;
     if (!a.pat && !b.pat && a.esize == b.esize) {
         a.blen += b.blen;
         a.extent = int64_t(a.blen);
+        a.tid = tid;
         return true;
     }
     std::vector<uint32_t> sa, sb;
@@ -407,6 +412,7 @@ bool try_merge(Node &a, const Node &b)
     a.blen += b.blen;
     a.extent = int64_t(a.blen);
     a.esize = std::min(a.esize, b.esize);
+    a.tid = tid;
     a.pat = p;
     return true;
 }
@@ -904,6 +910,7 @@ bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<
             Node n;
             n.kind = Node::DATA;
             n.esize = kSize[type];
+            n.tid = type;
             n.count = count;
             n.blen = blocklen * uint64_t(kSize[type]);
             n.extent = extent;

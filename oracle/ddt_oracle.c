@@ -47,6 +47,7 @@ typedef struct {
     int64_t disp;  /* byte displacement relative to the type origin */
     int64_t len;   /* bytes */
     int64_t esize; /* size of the basic elements the run is made of */
+    int64_t tid;   /* OPAL id of those elements (external32 conversion) */
 } ort_run;
 
 typedef struct ort_type {
@@ -89,13 +90,13 @@ void ort_free(ort_type *t)
     free(t);
 }
 
-static void ort_push_run(ort_type *t, int64_t disp, int64_t len, int64_t esize)
+static void ort_push_run(ort_type *t, int64_t disp, int64_t len, int64_t esize, int64_t tid)
 {
     if (len <= 0)
         return;
     if (t->nruns > 0) {
         ort_run *p = &t->runs[t->nruns - 1];
-        if (p->disp + p->len == disp && p->esize == esize) {
+        if (p->disp + p->len == disp && p->esize == esize && p->tid == tid) {
             p->len += len;
             return;
         }
@@ -107,6 +108,7 @@ static void ort_push_run(ort_type *t, int64_t disp, int64_t len, int64_t esize)
     t->runs[t->nruns].disp = disp;
     t->runs[t->nruns].len = len;
     t->runs[t->nruns].esize = esize;
+    t->runs[t->nruns].tid = tid;
     t->nruns++;
 }
 
@@ -124,7 +126,7 @@ ort_type *ort_basic(int id)
     t->align = ort_basic_align[id];
     t->nbElems = 1;
     t->flags = ORT_FLAG_PREDEFINED | ORT_FLAG_CONTIGUOUS | ORT_FLAG_NO_GAPS | ORT_FLAG_DATA;
-    ort_push_run(t, 0, t->size, t->size);
+    ort_push_run(t, 0, t->size, t->size, id);
     return t;
 }
 
@@ -222,7 +224,8 @@ static void ort_add(ort_type *base, const ort_type *add, int64_t count, int64_t 
     for (int64_t i = 0; i < count; i++) {
         int64_t off = disp + i * extent;
         for (int64_t r = 0; r < add->nruns; r++)
-            ort_push_run(base, add->runs[r].disp + off, add->runs[r].len, add->runs[r].esize);
+            ort_push_run(base, add->runs[r].disp + off, add->runs[r].len, add->runs[r].esize,
+                         add->runs[r].tid);
     }
     /* contiguity flags (:437-451) */
     {
@@ -645,4 +648,140 @@ int64_t ort_run_mt(ort_type *t, int64_t count, void *base, void *buf, int nthrea
     for (int k = 0; k < nthreads; k++)
         pthread_join(th[k], NULL);
     return total;
+}
+
+/*
+ * opal_convertor_raw (opal/datatype/opal_convertor_raw.c:65-283) on the flat type map:
+ * the user-memory regions of `count` instances at `base`, in type-map order, from packed
+ * position `position`.  A region starting where the previous one ends extends it
+ * (opal_convertor_merge_iov, :41-58); a region that would need iovec number `cap`+1 is
+ * left for the next call.  Writes *n iovecs to addr[]/len[] and returns the bytes they
+ * describe.
+ */
+int64_t ort_raw(ort_type *t, int64_t count, int64_t base, int64_t position, int64_t cap,
+                int64_t *addr, int64_t *len, int64_t *n)
+{
+    const int64_t total = count * t->size;
+    int64_t idx = 0, described = 0;
+    *n = 0;
+    if (t->size == 0 || position >= total || cap <= 0)
+        return 0;
+    ort_prefix(t);
+    int64_t inst, run, within;
+    ort_locate(t, position, &inst, &run, &within);
+    len[0] = 0;
+    for (; inst < count; inst++, run = 0) {
+        const int64_t ibase = base + inst * (t->ub - t->lb);
+        for (; run < t->nruns; run++, within = 0) {
+            const int64_t a = ibase + t->runs[run].disp + within;
+            const int64_t l = t->runs[run].len - within;
+            if (l <= 0)
+                continue;
+            if (len[idx] != 0) {
+                if (a == addr[idx] + len[idx]) {
+                    len[idx] += l;
+                    described += l;
+                    continue;
+                }
+                if (++idx == cap) {
+                    *n = cap;
+                    return described;
+                }
+            }
+            addr[idx] = a;
+            len[idx] = l;
+            described += l;
+        }
+    }
+    *n = len[idx] ? idx + 1 : idx;
+    return described;
+}
+
+/*
+ * external32 (MPI_Pack_external / MPI_Unpack_external, ompi_datatype_external.c:33-135):
+ * the convertor of the external32 architecture (ompi_datatype_external32.c:35-38: big
+ * endian, bool 1 byte, long 4 bytes) applies opal_copy_functions_heterogeneous.c element
+ * by element in type-map order:
+ *   - 1-byte types (INT1, UINT1, BOOL): copied (the byte-swap mask skips them,
+ *     opal_convertor.c:191-203; copy_cxx_bool_heterogeneous :918-970 is a memcpy when
+ *     sizeof(bool) matches);
+ *   - LONG / UNSIGNED_LONG: 8 local bytes <-> 4 big-endian bytes (copy_long_heterogeneous
+ *     :1094-1223, unsigned :1225-1360): pack keeps the low 32 bits, unpack sign- (LONG) or
+ *     zero- (UNSIGNED_LONG) extends;
+ *   - complex types: each component byte-swapped (COPY_2SAMETYPE_HETEROGENEOUS :776-842);
+ *   - every other type: byte-swapped whole (opal_dt_swap_bytes :49-70).
+ * Long double types (FLOAT12, FLOAT16, LONG_DOUBLE_COMPLEX, FLOAT128_COMPLEX) depend on the
+ * reference's build (HAVE_IEEE754_H, :121-230): refused (-1).
+ */
+static const int64_t ort_ext_size[29] = {
+    0, 0, 0, 0, 1, 2, 4, 8, 16, 1, 2, 4, 8, 16, 2, 4, 8, -1, -1, 4, 8, 16, -1, 1, 4, 4, 4, -1, 0};
+
+static int64_t ort_ext_comp(int64_t tid)
+{
+    switch (tid) {
+    case 19: return 2;  /* short float complex */
+    case 20: return 4;  /* float complex */
+    case 21: return 8;  /* double complex */
+    default: return ort_basic_size[tid];
+    }
+}
+
+int64_t ort_external_size(const ort_type *t)
+{
+    int64_t s = 0;
+    for (int64_t r = 0; r < t->nruns; r++) {
+        const int64_t tid = t->runs[r].tid;
+        if (tid < 4 || tid > 27 || ort_ext_size[tid] < 0)
+            return -1;
+        s += t->runs[r].len / t->runs[r].esize * ort_ext_size[tid];
+    }
+    return s;
+}
+
+static void ort_ext_elem(int64_t tid, const unsigned char *from, unsigned char *to, int pack)
+{
+    const int64_t ls = ort_basic_size[tid];
+    if (tid == 25 || tid == 26) {
+        if (pack) {
+            for (int k = 0; k < 4; k++)
+                to[k] = from[3 - k];
+        } else {
+            for (int k = 0; k < 4; k++)
+                to[k] = from[3 - k];
+            const unsigned char fill = (tid == 25 && (from[0] & 0x80)) ? 0xFF : 0x00;
+            for (int k = 4; k < 8; k++)
+                to[k] = fill;
+        }
+        return;
+    }
+    const int64_t c = ort_ext_comp(tid);
+    for (int64_t base = 0; base < ls; base += c)
+        for (int64_t k = 0; k < c; k++)
+            to[base + k] = from[base + c - 1 - k];
+}
+
+/* Whole-message conversion between `count` instances at `base` and the external32
+ * stream `ext`.  Returns the external bytes, or -1 for an unsupported type. */
+int64_t ort_external(ort_type *t, int64_t count, void *base, void *ext, int pack)
+{
+    const int64_t es = ort_external_size(t);
+    if (es < 0)
+        return -1;
+    unsigned char *e = (unsigned char *) ext;
+    for (int64_t i = 0; i < count; i++) {
+        unsigned char *ib = (unsigned char *) base + i * (t->ub - t->lb);
+        for (int64_t r = 0; r < t->nruns; r++) {
+            const ort_run *R = &t->runs[r];
+            const int64_t n = R->len / R->esize, xs = ort_ext_size[R->tid];
+            for (int64_t k = 0; k < n; k++) {
+                unsigned char *u = ib + R->disp + k * R->esize;
+                if (pack)
+                    ort_ext_elem(R->tid, u, e, 1);
+                else
+                    ort_ext_elem(R->tid, e, u, 0);
+                e += xs;
+            }
+        }
+    }
+    return es * count;
 }

@@ -47,6 +47,9 @@ def lib():
             "ort_pack_bytes": (i64, [vp, i64, vp, i64, vp, i64]),
             "ort_unpack": (i64, [vp, i64, vp, i64, vp, i64]),
             "ort_run_mt": (i64, [vp, i64, vp, vp, i, i]),
+            "ort_raw": (i64, [vp, i64, i64, i64, i64, vp, vp, vp]),
+            "ort_external": (i64, [vp, i64, vp, vp, i]),
+            "ort_external_size": (i64, [vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -119,6 +122,34 @@ class OType:
     def pack_all(self, count: int, user: np.ndarray, origin: int) -> bytes:
         total = count * self.size
         return self.pack(count, user, origin, 0, total, element_granular=False)
+
+    def raw(self, count: int, base: int, position: int, cap: int):
+        """opal_convertor_raw from `position`: ([(addr, len)], bytes described)."""
+        addr = np.zeros(max(cap, 1), dtype=np.int64)
+        ln = np.zeros(max(cap, 1), dtype=np.int64)
+        n = ctypes.c_int64()
+        got = lib().ort_raw(self.h, count, base, position, cap, addr.ctypes.data, ln.ctypes.data,
+                            ctypes.byref(n))
+        return [(int(addr[i]), int(ln[i])) for i in range(n.value)], int(got)
+
+    def external_size(self) -> int:
+        """external32 bytes of one instance, -1 if a type has no fixed external form."""
+        return int(lib().ort_external_size(self.h))
+
+    def pack_external(self, count: int, user: np.ndarray, origin: int):
+        """MPI_Pack_external of `count` instances (bytes), or None when unsupported."""
+        es = self.external_size()
+        if es < 0:
+            return None
+        out = np.zeros(max(es * count, 1), dtype=np.uint8)
+        lib().ort_external(self.h, count, ctypes.c_void_p(user.ctypes.data + origin),
+                           out.ctypes.data, 1)
+        return out[:es * count].tobytes()
+
+    def unpack_external(self, count: int, user: np.ndarray, origin: int, data: bytes) -> int:
+        buf = np.frombuffer(data, dtype=np.uint8).copy()
+        return int(lib().ort_external(self.h, count, ctypes.c_void_p(user.ctypes.data + origin),
+                                      buf.ctypes.data, 0))
 
     def run_mt(self, count, user_ptr: int, buf_ptr: int, nthreads: int, unpack: bool) -> int:
         return lib().ort_run_mt(self.h, count, ctypes.c_void_p(user_ptr), ctypes.c_void_p(buf_ptr),

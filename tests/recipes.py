@@ -25,6 +25,10 @@ from . import oracle as O
 
 # (opal id, size) of the basic types the fuzzer draws from
 BASICS = [(4, 1), (5, 2), (6, 4), (15, 4), (16, 8), (7, 8), (21, 16), (11, 4), (9, 1)]
+# every type with an external32 form: adds INT16, FLOAT2, the complex types, BOOL, WCHAR,
+# LONG and UNSIGNED_LONG (size-changing)
+EXT_BASICS = BASICS + [(8, 16), (14, 2), (19, 4), (20, 8), (23, 1), (24, 4), (25, 8), (26, 8),
+                       (12, 8), (10, 2)]
 
 
 def build_oracle(recipe, memo=None):
@@ -121,13 +125,14 @@ def fill(n: int, seed: int) -> np.ndarray:
 
 
 # ------------------------------------------------------------------ fuzzing
-def random_recipe(rng: random.Random, depth: int = 0) -> Any:
+def random_recipe(rng: random.Random, depth: int = 0, basics=None) -> Any:
+    basics = basics or BASICS
     if depth >= 3 or rng.random() < 0.25:
-        return ("basic", rng.choice(BASICS)[0])
+        return ("basic", rng.choice(basics)[0])
     k = rng.choice(["contig", "vector", "vector", "hvector", "indexed", "hindexed",
                     "indexed_block", "hindexed_block", "struct", "struct", "subarray",
                     "resized", "dup"])
-    sub = random_recipe(rng, depth + 1)
+    sub = random_recipe(rng, depth + 1, basics)
     if k == "contig":
         return ("contig", rng.randint(1, 5), sub)
     if k == "vector":
@@ -150,7 +155,7 @@ def random_recipe(rng: random.Random, depth: int = 0) -> Any:
         return (k, rng.randint(0, 3), ds, sub)
     if k == "struct":
         n = rng.randint(1, 4)
-        subs = [sub] + [random_recipe(rng, depth + 1) for _ in range(n - 1)]
+        subs = [sub] + [random_recipe(rng, depth + 1, basics) for _ in range(n - 1)]
         if n > 1 and rng.random() < 0.3:
             subs[1] = subs[0]   # same handle: exercises the struct merge
         return ("struct", [rng.randint(0, 3) for _ in range(n)],

@@ -1,0 +1,156 @@
+"""Raw iovec export (opal_convertor_raw, opal_convertor_raw.c:65-283).
+
+The engine's ddt_convertor_raw walks its committed type map; the oracle (ort_raw) walks
+the flat type map.  Both must give the same iovec lists for every position and iovec
+budget.  The reference's own raw test (ddt_raw2.c) is replayed on its hand-written
+description: 300, 10 and 1 iovecs per call give the same list, covering `size` bytes.
+No data moves, so these run on CPU (the base address is never dereferenced).
+"""
+from __future__ import annotations
+
+import json
+import os
+import random
+import struct
+
+import pytest
+
+import ompi_amd
+from ompi_amd import datatype as D
+from tests import recipes as R
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BASE = 1 << 40
+
+
+def engine_raw_all(dt, count, base, cap, position=0):
+    c = ompi_amd.Convertor()
+    c.prepare_for_raw(dt, count, base)
+    if position:
+        c.set_position(position)
+    out, calls, total = [], 0, 0
+    while True:
+        rc, iovs, n = c.raw(cap)
+        assert len(iovs) <= cap
+        assert sum(ln for _, ln in iovs) == n
+        out.append(iovs)
+        total += n
+        calls += 1
+        if rc == 1:
+            return out, total
+        assert iovs, "no progress"
+        assert calls < 10 ** 6
+
+
+def stitched(chunks):
+    """Concatenate per-call lists, merging a region split across two calls."""
+    flat = []
+    for ch in chunks:
+        for a, n in ch:
+            if flat and flat[-1][0] + flat[-1][1] == a:
+                flat[-1] = (flat[-1][0], flat[-1][1] + n)
+            else:
+                flat.append((a, n))
+    return flat
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_raw_matches_oracle_fuzz(seed):
+    rng = random.Random(4100 + seed)
+    for n in range(80):
+        b = R.Built(R.random_recipe(rng))
+        oi = b.o.info()
+        count = rng.choice([1, 2, 5])
+        total = oi["size"] * count
+        e = b.engine()
+        base = BASE + R.layout(oi, count)[1]
+        full, got = b.o.raw(count, base, 0, 1 << 20)
+        assert got == total
+        for cap in (1, 2, 7, 1 << 20):
+            chunks, tot = engine_raw_all(e, count, base, cap)
+            assert tot == total, (b.recipe, cap)
+            assert stitched(chunks) == full, (b.recipe, cap)
+        if total == 0:
+            continue
+        # every call from a random position equals the oracle's call there
+        c = ompi_amd.Convertor()
+        c.prepare_for_raw(e, count, base)
+        for _ in range(4):
+            pos = rng.randrange(total)
+            cap = rng.choice([1, 3, 16])
+            c.set_position(pos)
+            rc, iovs, nb = c.raw(cap)
+            ref, rb = b.o.raw(count, base, pos, cap)
+            assert iovs == ref and nb == rb, (b.recipe, pos, cap)
+            assert rc == (1 if pos + nb == total else 0)
+            assert c.position == pos + nb
+
+
+def test_raw_contiguous_is_one_iovec():
+    dt = D.create_contiguous(1000, D.predefined(D.FLOAT8)).commit()
+    chunks, tot = engine_raw_all(dt, 3, BASE, 4)
+    assert chunks == [[(BASE, 24000)]] and tot == 24000
+
+
+def test_raw_vector_regions():
+    # vector(3, 2, 4) double (partial.c): blocks of 16 B every 32 B
+    dt = D.create_vector(3, 2, 4, D.predefined(D.FLOAT8)).commit()
+    chunks, _ = engine_raw_all(dt, 2, BASE, 100)
+    ext = 2 * 32 + 16
+    want = [(BASE + i * ext + k * 32, 16) for i in range(2) for k in range(3)]
+    # instance 0's last block ends at 80 == instance 1's first block: merged
+    want = stitched([want])
+    assert chunks == [want]
+
+
+def test_raw_completed_and_empty():
+    c = ompi_amd.Convertor()
+    dt = D.create_contiguous(0, D.predefined(D.INT4)).commit()
+    c.prepare_for_raw(dt, 4, BASE)
+    assert c.raw(8) == (1, [], 0)
+
+
+def _opal_desc_bytes(rows):
+    out = b""
+    for kind, flags, typ, a, b_, c, d in rows:
+        if kind == "elem":
+            out += struct.pack("<HHIQqq", flags, typ, a, b_, c, d)
+        else:  # loop: items, loops, unused, extent; end: items, unused, size, first_elem_disp
+            out += struct.pack("<HHII4xQq", flags, typ, a, b_ & 0xFFFFFFFF, c & (2 ** 64 - 1), d)
+    return out
+
+
+def _walk_desc(rows, i, end, base, out):
+    """Literal walk of an opal description (opal_convertor_raw.c:148-262): DATA blocks of
+    blocklen elements every extent bytes; LOOP bodies repeated every loop extent."""
+    size1 = {9: 1}
+    while i < end:
+        kind, flags, typ, a, b_, c, d = rows[i]
+        if kind == "elem":
+            for k in range(a):
+                out.append((base + d + k * c, b_ * size1[typ]))
+            i += 1
+        else:
+            items, loops, extent = a, b_, d
+            for it in range(loops):
+                _walk_desc(rows, i + 1, i + items, base + it * extent, out)
+            i += items + 1
+
+
+def test_raw_reference_ddt_raw2_description():
+    """ddt_raw2.c:104-211 replayed: the reference's committed description, imported as-is,
+    exported with 300, 10 and 1 iovecs per call."""
+    fx = json.load(open(os.path.join(HERE, "golden", "ddt_raw2_desc.json")))
+    rows, used, bd = fx["desc"], fx["used"], fx["bounds"]
+    dt = D.from_opal_desc(_opal_desc_bytes(rows[:used]), bd["size"], bd["lb"], bd["ub"],
+                          bd["true_lb"], bd["true_ub"])
+    lists = {}
+    for cap in (300, 10, 1):
+        chunks, tot = engine_raw_all(dt, 1, BASE, cap)
+        assert tot == bd["size"]
+        lists[cap] = [iov for ch in chunks for iov in ch]
+    assert lists[300] == lists[10] == lists[1]
+    pieces = []
+    _walk_desc(rows, 0, used, BASE, pieces)
+    assert stitched([pieces]) == lists[300]
+    assert sum(n for _, n in pieces) == bd["size"]
