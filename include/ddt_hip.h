@@ -75,6 +75,11 @@ extern "C" {
 
 #define DDT_ORDER_C 0
 #define DDT_ORDER_FORTRAN 1
+/* MPI_DISTRIBUTE_* (mpi.h.in:595-598) */
+#define DDT_DISTRIBUTE_BLOCK 0
+#define DDT_DISTRIBUTE_CYCLIC 1
+#define DDT_DISTRIBUTE_NONE 2
+#define DDT_DISTRIBUTE_DFLT_DARG (-1)
 
 typedef struct ddt_datatype ddt_datatype_t;
 typedef struct ddt_convertor ddt_convertor_t;
@@ -108,6 +113,12 @@ int ddt_type_create_struct(size_t count, const size_t *blocklens, const ptrdiff_
 int ddt_type_create_subarray(int ndims, const size_t *sizes, const size_t *subsizes,
                              const size_t *starts, int order, const ddt_datatype_t *oldtype,
                              ddt_datatype_t **newtype);
+/* ompi_datatype_create_darray (ompi_datatype_create_darray.c:187-312): the block / cyclic /
+ * none distribution of a `ndims`-dimensional global array over a process grid, for `rank`
+ * of `size`; gsizes are counts (big-count form). */
+int ddt_type_create_darray(int size, int rank, int ndims, const size_t *gsizes, const int *distribs,
+                           const int *dargs, const int *psizes, int order,
+                           const ddt_datatype_t *oldtype, ddt_datatype_t **newtype);
 /* ompi_datatype_create_resized (ompi_datatype.h:270-284) */
 int ddt_type_create_resized(const ddt_datatype_t *oldtype, ptrdiff_t lb, ptrdiff_t extent,
                             ddt_datatype_t **newtype);

@@ -38,6 +38,8 @@ SIGNATURES = {
     "ddt_type_create_struct": (c_int, [c_size_t, c_void_p, c_void_p, c_void_p, P(c_void_p)]),
     "ddt_type_create_subarray": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                          P(c_void_p)]),
+    "ddt_type_create_darray": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_int, c_void_p, P(c_void_p)]),
     "ddt_type_create_resized": (c_int, [c_void_p, c_ssize_t, c_ssize_t, P(c_void_p)]),
     "ddt_type_dup": (c_int, [c_void_p, P(c_void_p)]),
     "ddt_type_commit": (c_int, [c_void_p]),

@@ -763,6 +763,169 @@ int ddt_type_dup(const ddt_datatype_t *old, ddt_datatype_t **out)
     return DDT_SUCCESS;
 }
 
+// ---- darray (ompi_datatype_create_darray.c), the same constructor calls in the same order
+namespace {
+
+int64_t gsize_prod(const size_t *g, int from, int to)   // product of g[from..to]
+{
+    int64_t p = 1;
+    for (int i = from; i <= to; ++i)
+        p *= int64_t(g[i]);
+    return p;
+}
+
+// block() (ompi_datatype_create_darray.c:34-98)
+int darray_block(const size_t *gsizes, int dim, int ndims, int nprocs, int rank, int darg, int order,
+                 int64_t orig_extent, const ddt_datatype *old, ddt_datatype **out, int64_t *st_offset)
+{
+    const int64_t global_size = int64_t(gsizes[dim]);
+    const int64_t blksize = darg == DDT_DISTRIBUTE_DFLT_DARG
+                                ? global_size / nprocs + (global_size % nprocs != 0)
+                                : int64_t(darg);
+    const int64_t j = global_size - blksize * rank;
+    int64_t mysize = blksize < j ? blksize : j;
+    if (mysize < 0)
+        mysize = 0;
+    const int start_loop = order == DDT_ORDER_C ? ndims - 1 : 0;
+    const int step = order == DDT_ORDER_C ? -1 : 1;
+    int rc;
+    if (dim == start_loop) {
+        rc = ddt_type_create_contiguous(size_t(mysize), old, out);
+    } else {
+        int64_t stride = orig_extent;
+        for (int i = start_loop; i != dim; i += step)
+            stride *= int64_t(gsizes[i]);
+        rc = ddt_type_create_hvector(size_t(mysize), 1, stride, old, out);
+    }
+    if (rc != DDT_SUCCESS)
+        return rc;
+    *st_offset = mysize == 0 ? 0 : blksize * rank;
+    const int64_t ub = orig_extent * (order == DDT_ORDER_FORTRAN ? gsize_prod(gsizes, 0, dim)
+                                                                 : gsize_prod(gsizes, dim, ndims - 1));
+    resize_in_place(*out, 0, ub);
+    return DDT_SUCCESS;
+}
+
+// cyclic() (ompi_datatype_create_darray.c:101-184)
+int darray_cyclic(const size_t *gsizes, int dim, int ndims, int nprocs, int rank, int darg, int order,
+                  int64_t orig_extent, const ddt_datatype *old, ddt_datatype **out, int64_t *st_offset)
+{
+    const int64_t blksize = darg == DDT_DISTRIBUTE_DFLT_DARG ? 1 : int64_t(darg);
+    const int64_t st_index = int64_t(rank) * blksize;
+    const int64_t end_index = int64_t(gsizes[dim]) - 1;
+    int64_t local_size = 0;
+    if (end_index >= st_index) {
+        local_size = ((end_index - st_index + 1) / (int64_t(nprocs) * blksize)) * blksize;
+        const int64_t rem = (end_index - st_index + 1) % (int64_t(nprocs) * blksize);
+        local_size += rem < blksize ? rem : blksize;
+    }
+    const int64_t count = local_size / blksize, rem = local_size % blksize;
+    int64_t stride = int64_t(nprocs) * blksize * orig_extent;
+    if (order == DDT_ORDER_FORTRAN)
+        stride *= gsize_prod(gsizes, 0, dim - 1);
+    else
+        stride *= gsize_prod(gsizes, dim + 1, ndims - 1);
+    int rc = ddt_type_create_hvector(size_t(count), size_t(blksize), stride, old, out);
+    if (rc != DDT_SUCCESS)
+        return rc;
+    if (rem) {
+        // trailing partial block through a struct (:150-165)
+        const ddt_datatype *types[2] = {*out, old};
+        const ptrdiff_t disps[2] = {0, ptrdiff_t(count * stride)};
+        const size_t blens[2] = {1, size_t(rem)};
+        ddt_datatype *tmp = nullptr;
+        rc = ddt_type_create_struct(2, blens, disps, types, &tmp);
+        delete *out;
+        *out = tmp;
+        if (rc != DDT_SUCCESS)
+            return rc;
+    }
+    const int64_t ub = orig_extent * (order == DDT_ORDER_FORTRAN ? gsize_prod(gsizes, 0, dim)
+                                                                 : gsize_prod(gsizes, dim, ndims - 1));
+    resize_in_place(*out, 0, ub);
+    *st_offset = local_size == 0 ? 0 : int64_t(rank) * blksize;
+    return DDT_SUCCESS;
+}
+
+}  // namespace
+
+int ddt_type_create_darray(int size, int rank, int ndims, const size_t *gsizes, const int *distribs,
+                           const int *dargs, const int *psizes, int order, const ddt_datatype_t *old,
+                           ddt_datatype_t **out)
+{
+    // ompi_datatype_create_darray (ompi_datatype_create_darray.c:187-312)
+    if (!old || !out || (ndims > 0 && (!gsizes || !distribs || !dargs || !psizes)) || size < 1
+        || rank < 0 || rank >= size)
+        return DDT_ERR_BAD_PARAM;
+    if (ndims < 1) {
+        *out = make_empty();
+        return DDT_SUCCESS;
+    }
+    for (int i = 0; i < ndims; ++i)
+        if (psizes[i] < 1)
+            return DDT_ERR_BAD_PARAM;
+    const int64_t orig_extent = old->extent();
+    std::vector<int> coords(static_cast<size_t>(ndims), 0);
+    int64_t ub = orig_extent;
+    {
+        int tmp_rank = rank, procs = size;
+        for (int i = 0; i < ndims; ++i) {
+            procs /= psizes[i];
+            if (procs < 1)
+                return DDT_ERR_BAD_PARAM;
+            coords[size_t(i)] = tmp_rank / procs;
+            tmp_rank %= procs;
+            ub *= int64_t(gsizes[i]);
+        }
+    }
+    std::vector<int64_t> st(static_cast<size_t>(ndims), 0);
+    ddt_datatype *last = clone_type(old);
+    const int start_loop = order == DDT_ORDER_C ? ndims - 1 : 0;
+    const int step = order == DDT_ORDER_C ? -1 : 1;
+    const int end_loop = order == DDT_ORDER_C ? -1 : ndims;
+    for (int i = start_loop; i != end_loop; i += step) {
+        ddt_datatype *nt = nullptr;
+        int rc;
+        switch (distribs[i]) {
+        case DDT_DISTRIBUTE_BLOCK:
+            rc = darray_block(gsizes, i, ndims, psizes[i], coords[size_t(i)], dargs[i], order,
+                              orig_extent, last, &nt, &st[size_t(i)]);
+            break;
+        case DDT_DISTRIBUTE_CYCLIC:
+            rc = darray_cyclic(gsizes, i, ndims, psizes[i], coords[size_t(i)], dargs[i], order,
+                               orig_extent, last, &nt, &st[size_t(i)]);
+            break;
+        case DDT_DISTRIBUTE_NONE:
+            // a block distribution on one process (:264-274)
+            rc = darray_block(gsizes, i, ndims, order == DDT_ORDER_C ? psizes[i] : 1,
+                              order == DDT_ORDER_C ? coords[size_t(i)] : 0, DDT_DISTRIBUTE_DFLT_DARG,
+                              order, orig_extent, last, &nt, &st[size_t(i)]);
+            break;
+        default:
+            rc = DDT_ERR_BAD_PARAM;
+        }
+        delete last;
+        if (rc != DDT_SUCCESS) {
+            delete nt;
+            return rc;
+        }
+        last = nt;
+    }
+    // move the data to its displacement: a fresh type + one add (:288-306)
+    int64_t disp = st[size_t(start_loop)], tmp_size = 1;
+    for (int i = start_loop + step; i != end_loop; i += step) {
+        tmp_size *= int64_t(gsizes[i - step]);
+        disp += tmp_size * st[size_t(i)];
+    }
+    disp *= orig_extent;
+    ddt_datatype *nt = new_type();
+    type_add(nt, last, 1, disp, ub);
+    delete last;
+    resize_in_place(nt, 0, ub);
+    *out = nt;
+    return DDT_SUCCESS;
+}
+
 int ddt_type_create_subarray(int ndims, const size_t *sizes, const size_t *subsizes,
                              const size_t *starts, int order, const ddt_datatype_t *old,
                              ddt_datatype_t **out)

@@ -176,6 +176,20 @@ def create_subarray(sizes: Sequence[int], subsizes: Sequence[int], starts: Seque
     return _new("ddt_type_create_subarray", len(s), _ptr(s), _ptr(ss), _ptr(st), order, old.handle)
 
 
+DISTRIBUTE_BLOCK, DISTRIBUTE_CYCLIC, DISTRIBUTE_NONE, DISTRIBUTE_DFLT_DARG = 0, 1, 2, -1
+
+
+def create_darray(size: int, rank: int, gsizes: Sequence[int], distribs: Sequence[int],
+                  dargs: Sequence[int], psizes: Sequence[int], order: int, old: Datatype) -> Datatype:
+    """MPI_Type_create_darray (ompi_datatype_create_darray.c:187-312)."""
+    g = _sizes(gsizes)
+    di = np.ascontiguousarray(np.asarray(distribs, dtype=np.int32))
+    da = np.ascontiguousarray(np.asarray(dargs, dtype=np.int32))
+    ps = np.ascontiguousarray(np.asarray(psizes, dtype=np.int32))
+    return _new("ddt_type_create_darray", size, rank, len(g), _ptr(g), _ptr(di), _ptr(da), _ptr(ps),
+                order, old.handle)
+
+
 def create_resized(old: Datatype, lb: int, extent: int) -> Datatype:
     return _new("ddt_type_create_resized", old.handle, lb, extent)
 

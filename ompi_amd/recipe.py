@@ -5,6 +5,7 @@
     ("hindexed", blens, disps, sub) | ("indexed_block", blen, disps, sub)
     ("hindexed_block", blen, disps, sub) | ("struct", blens, disps, [subs])
     ("subarray", sizes, subsizes, starts, order, sub) | ("resized", sub, lb, extent)
+  | ("darray", size, rank, gsizes, distribs, dargs, psizes, order, sub)
     ("dup", sub)
 
 Each constructor maps 1:1 to ompi_datatype_create_* (ompi/datatype/ompi_datatype.h:217-284).
@@ -45,6 +46,8 @@ def build(recipe, memo=None):
         t = D.create_struct(recipe[1], recipe[2], [sub(r) for r in recipe[3]])
     elif k == "subarray":
         t = D.create_subarray(recipe[1], recipe[2], recipe[3], recipe[4], sub(recipe[5]))
+    elif k == "darray":
+        t = D.create_darray(*recipe[1:8], sub(recipe[8]))
     elif k == "resized":
         t = D.create_resized(sub(recipe[1]), recipe[2], recipe[3])
     elif k == "dup":

@@ -460,6 +460,123 @@ ort_type *ort_subarray(int ndims, const int64_t *sizes, const int64_t *subsizes,
     return nt;
 }
 
+/* opal_datatype_resize in place (opal_datatype_resize.c:23-41) */
+static void ort_resize_inplace(ort_type *t, int64_t lb, int64_t extent)
+{
+    t->lb = lb;
+    t->ub = lb + extent;
+    t->flags &= ~ORT_FLAG_NO_GAPS;
+    t->flags |= ORT_FLAG_USER_LB | ORT_FLAG_USER_UB;
+    if (extent == t->size && (t->flags & ORT_FLAG_CONTIGUOUS))
+        t->flags |= ORT_FLAG_NO_GAPS;
+}
+
+static int64_t ort_gprod(const int64_t *g, int from, int to)
+{
+    int64_t p = 1;
+    for (int i = from; i <= to; i++)
+        p *= g[i];
+    return p;
+}
+
+/* block() of ompi_datatype_create_darray.c:34-98 */
+static ort_type *ort_darray_block(const int64_t *g, int dim, int ndims, int nprocs, int rank,
+                                  int darg, int order, int64_t oext, const ort_type *old,
+                                  int64_t *st)
+{
+    int64_t blk = darg == -1 ? g[dim] / nprocs + (g[dim] % nprocs != 0) : darg;
+    int64_t j = g[dim] - blk * rank;
+    int64_t mysize = blk < j ? blk : j;
+    if (mysize < 0)
+        mysize = 0;
+    int start_loop = order == 0 ? ndims - 1 : 0, step = order == 0 ? -1 : 1;
+    ort_type *t;
+    if (dim == start_loop) {
+        t = ort_contiguous(mysize, old);
+    } else {
+        int64_t stride = oext;
+        for (int i = start_loop; i != dim; i += step)
+            stride *= g[i];
+        t = ort_hvector(mysize, 1, stride, old);
+    }
+    *st = mysize == 0 ? 0 : blk * rank;
+    ort_resize_inplace(t, 0, oext * (order == 1 ? ort_gprod(g, 0, dim) : ort_gprod(g, dim, ndims - 1)));
+    return t;
+}
+
+/* cyclic() of ompi_datatype_create_darray.c:101-184 */
+static ort_type *ort_darray_cyclic(const int64_t *g, int dim, int ndims, int nprocs, int rank,
+                                   int darg, int order, int64_t oext, const ort_type *old,
+                                   int64_t *st)
+{
+    int64_t blk = darg == -1 ? 1 : darg;
+    int64_t st_index = (int64_t) rank * blk, end_index = g[dim] - 1, local = 0;
+    if (end_index >= st_index) {
+        local = ((end_index - st_index + 1) / ((int64_t) nprocs * blk)) * blk;
+        int64_t rem = (end_index - st_index + 1) % ((int64_t) nprocs * blk);
+        local += rem < blk ? rem : blk;
+    }
+    int64_t count = local / blk, rem = local % blk;
+    int64_t stride = (int64_t) nprocs * blk * oext;
+    stride *= order == 1 ? ort_gprod(g, 0, dim - 1) : ort_gprod(g, dim + 1, ndims - 1);
+    ort_type *t = ort_hvector(count, blk, stride, old);
+    if (rem) {
+        int64_t bl[2] = {1, rem}, dp[2] = {0, count * stride};
+        const ort_type *ty[2] = {t, old};
+        ort_type *s2 = ort_struct(2, bl, dp, ty);
+        ort_free(t);
+        t = s2;
+    }
+    ort_resize_inplace(t, 0, oext * (order == 1 ? ort_gprod(g, 0, dim) : ort_gprod(g, dim, ndims - 1)));
+    *st = local == 0 ? 0 : (int64_t) rank * blk;
+    return t;
+}
+
+/* ompi_datatype_create_darray (ompi_datatype_create_darray.c:187-312);
+ * distribs: 0 block, 1 cyclic, 2 none; darg -1 = default; order 0 = C. */
+ort_type *ort_darray(int size, int rank, int ndims, const int64_t *g, const int *distribs,
+                     const int *dargs, const int *psizes, int order, const ort_type *old)
+{
+    if (ndims < 1)
+        return ort_empty();
+    int64_t oext = ort_extent(old), ub = oext;
+    int coords[32];
+    int64_t st[32];
+    int tmp_rank = rank, procs = size;
+    for (int i = 0; i < ndims; i++) {
+        procs /= psizes[i];
+        coords[i] = tmp_rank / procs;
+        tmp_rank %= procs;
+        ub *= g[i];
+    }
+    ort_type *last = ort_dup(old);
+    int start_loop = order == 0 ? ndims - 1 : 0, step = order == 0 ? -1 : 1;
+    int end_loop = order == 0 ? -1 : ndims;
+    for (int i = start_loop; i != end_loop; i += step) {
+        ort_type *nt;
+        if (distribs[i] == 0)
+            nt = ort_darray_block(g, i, ndims, psizes[i], coords[i], dargs[i], order, oext, last, &st[i]);
+        else if (distribs[i] == 1)
+            nt = ort_darray_cyclic(g, i, ndims, psizes[i], coords[i], dargs[i], order, oext, last, &st[i]);
+        else
+            nt = ort_darray_block(g, i, ndims, order == 0 ? psizes[i] : 1, order == 0 ? coords[i] : 0,
+                                  -1, order, oext, last, &st[i]);
+        ort_free(last);
+        last = nt;
+    }
+    int64_t disp = st[start_loop], tmp = 1;
+    for (int i = start_loop + step; i != end_loop; i += step) {
+        tmp *= g[i - step];
+        disp += tmp * st[i];
+    }
+    disp *= oext;
+    ort_type *nt = ort_new();
+    ort_add(nt, last, 1, disp, ub);
+    ort_free(last);
+    ort_resize_inplace(nt, 0, ub);
+    return nt;
+}
+
 /* out[0..7] = size, lb, ub, true_lb, true_ub, align, flags, nruns */
 void ort_info(const ort_type *t, int64_t *out)
 {

@@ -41,6 +41,7 @@ def lib():
             "ort_hindexed_block": (vp, [i64, i64, vp, vp]),
             "ort_struct": (vp, [i64, vp, vp, vp]),
             "ort_subarray": (vp, [i, vp, vp, vp, i, vp]),
+            "ort_darray": (vp, [i, i, i, vp, vp, vp, vp, i, vp]),
             "ort_resized": (vp, [vp, i64, i64]),
             "ort_info": (None, [vp, vp]), "ort_run_at": (None, [vp, i64, vp]),
             "ort_pack": (i64, [vp, i64, vp, i64, vp, i64]),
@@ -199,6 +200,14 @@ def struct(blens, disps, types):
     d, dp = _arr(disps, np.int64)
     arr = (ctypes.c_void_p * len(types))(*[t.h.value for t in types])
     return OType(lib().ort_struct(len(b), bp, dp, ctypes.cast(arr, ctypes.c_void_p)))
+
+
+def darray(size, rank, gsizes, distribs, dargs, psizes, order, old):
+    g, gp = _arr(gsizes, np.int64)
+    di, dip = _arr(distribs, np.int32)
+    da, dap = _arr(dargs, np.int32)
+    ps, psp = _arr(psizes, np.int32)
+    return OType(lib().ort_darray(size, rank, len(g), gp, dip, dap, psp, order, old.h))
 
 
 def subarray(sizes, subsizes, starts, order, old):

@@ -64,6 +64,8 @@ def build_oracle(recipe, memo=None):
         t = O.struct(recipe[1], recipe[2], [sub(r) for r in recipe[3]])
     elif k == "subarray":
         t = O.subarray(recipe[1], recipe[2], recipe[3], recipe[4], sub(recipe[5]))
+    elif k == "darray":
+        t = O.darray(*recipe[1:8], sub(recipe[8]))
     elif k == "resized":
         t = O.resized(sub(recipe[1]), recipe[2], recipe[3])
     elif k == "dup":

@@ -372,3 +372,14 @@ def test_external32_errors(device):
     with pytest.raises(ompi_amd.DDTError) as ei:
         ompi_amd.pack_external(user, 1, ld, out, 16, 0)
     assert ei.value.code == -10
+
+
+def test_darray_roundtrip(device):
+    """MPI_Type_create_darray types through the kernels (block, cyclic, none; C and
+    Fortran order), bit-exact with the oracle."""
+    from .test_cpu_darray import random_darray
+    rng = random.Random(5400)
+    for n in range(40):
+        size, gs, dist, darg, ps, order, old = random_darray(rng)
+        rec = ("darray", size, rng.randrange(size), gs, dist, darg, ps, order, old)
+        _roundtrip(R.Built(rec), rng.choice([1, 2]), device, n)
