@@ -122,48 +122,53 @@ def layout(info, count):
 
 
 # ------------------------------------------------------------------ CPU baseline
-def cpu_baseline(recipe, count, name, first=None, budget_s=12.0):
-    """Oracle (restated reference CPU convertor) pack+unpack on host cores, bounded sample.
+def sample_recipe(name, recipe, count):
+    """A bounded piece of the workload whose packed stream is a PREFIX of the full one
+    (same base pointer): about 10 s of oracle work, so the default run stays short."""
+    if name == "cfg2":
+        return recipe, 2, "2 of 16 fields"
+    if name == "cfg3":
+        return recipe, 1, "1 of 8 fields"
+    if name == "cfg4":
+        n = 1 << 20
+        return ("indexed_block", 1, recipe[2][:n], recipe[3]), 1, \
+            f"the first {n} of {len(recipe[2])} displacements (same 1 GiB base)"
+    if name == "cfg5":
+        n = 1 << 20
+        return ("hvector", n, recipe[2], recipe[3], recipe[4]), 1, \
+            f"the first {n} of {recipe[1]} records"
+    return recipe, count, "the whole message"
+
+
+def cpu_baseline(name, srec, scount, what, host_user, origin, gpu_prefix, budget_s=10.0):
+    """Oracle (restated reference CPU convertor) pack+unpack on host cores, on a bounded
+    prefix of the same workload and the GPU's own input bytes.
 
     The oracle is the checker here, never the measured product: it also re-packs the
-    first instance of the GPU's user buffer and reports whether the GPU bytes match."""
+    prefix and reports whether the GPU's packed bytes match."""
     from tests import recipes as R
-    sample_count = count
-    if name == "cfg2":
-        sample_count = 2
-    elif name == "cfg3":
-        sample_count = 1
-    elif name in ("cfg4", "cfg5"):
-        return None   # sampled separately below
-    b = R.Built(recipe)
+    b = R.Built(srec)
     info = b.o.info()
-    span, origin = layout(info, sample_count)
-    user = np.ones(span, dtype=np.uint8)
-    user[::7] = 3
-    S = info["size"] * sample_count
+    S = info["size"] * scount
     packed = np.zeros(S, dtype=np.uint8)
     threads = min(16, os.cpu_count() or 1)
-    ptr = user.ctypes.data + origin
-    b.o.run_mt(sample_count, ptr, packed.ctypes.data, threads, False)   # warm
+    ptr = host_user.ctypes.data + origin
+    b.o.run_mt(scount, ptr, packed.ctypes.data, threads, False)   # warm + reference bytes
+    match = bool(np.array_equal(packed, gpu_prefix[:S]))
+    scratch = host_user.copy()
+    sptr = scratch.ctypes.data + origin
     reps, t_tot, t0 = 0, 0.0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s and reps < 200:
+    while time.perf_counter() - t0 < budget_s:
         a = time.perf_counter()
-        b.o.run_mt(sample_count, ptr, packed.ctypes.data, threads, False)
-        b.o.run_mt(sample_count, ptr, packed.ctypes.data, threads, True)
+        b.o.run_mt(scount, sptr, packed.ctypes.data, threads, False)
+        b.o.run_mt(scount, sptr, packed.ctypes.data, threads, True)
         t_tot += time.perf_counter() - a
         reps += 1
     gibs = 2 * S * reps / t_tot / GiB
-    match = None
-    if first is not None:
-        host, sorig, gpu_bytes = first
-        ref = np.frombuffer(b.o.pack(1, host, sorig, 0, info["size"], element_granular=False),
-                            dtype=np.uint8)
-        match = bool(np.array_equal(ref, gpu_bytes))
     return {"value": round(gibs, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "gpu_matches_oracle": match,
-            "sample": f"{sample_count} of {count} instances of the same committed type, "
-                      f"{reps} pack+unpack reps, {S} packed bytes each, oracle/ddt_oracle.c "
-                      f"position-sharded over {threads} threads"}
+            "sample": f"{what} of config {name}: {reps} pack+unpack reps of {S} packed bytes, "
+                      f"oracle/ddt_oracle.c position-sharded over {threads} threads"}
 
 
 # ------------------------------------------------------------------ main
@@ -184,8 +189,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # backend "nccl" is RCCL on ROCm; DDT_BENCH_BACKEND=gloo rehearses the multi-rank path
+    # with several ranks sharing one GPU (code-path check only, not a scaling number)
+    backend = os.environ.get("DDT_BENCH_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
     if world > 1:
-        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(backend=backend)
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -222,11 +231,15 @@ def main():
     pack()
     unpack()
     torch.cuda.synchronize()
-    first = None
-    if rank == 0 and args.config in ("cfg1", "cfg2", "cfg3"):
-        sspan, sorig = layout(info, 1)
-        first = (user[origin - sorig: origin - sorig + sspan].cpu().numpy(), sorig,
-                 packed[:info["size"]].cpu().numpy())
+    base_sample = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from ompi_amd import recipe as _R
+        srec, scount, what = sample_recipe(args.config, recipe, count)
+        si = _R.build_committed(srec).info()
+        sext = si["ub"] - si["lb"]
+        hi = max(si["true_ub"], si["true_ub"] + (scount - 1) * sext) if si["size"] else 0
+        host_user = user[:min(span, origin + hi)].cpu().numpy()
+        base_sample = (srec, scount, what, host_user, packed[:si["size"] * scount].cpu().numpy())
 
     for _ in range(args.warmup):
         pack()
@@ -247,7 +260,7 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([wall], device=dev, dtype=torch.float64)
+        t = torch.tensor([wall], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.barrier()
         wall = float(t.item())
@@ -331,8 +344,12 @@ def main():
                         "pack_us": round(fp_t * 1e6, 2), "unpack_us": round(fu_t * 1e6, 2)}
         result["faces"] = faces
 
-    if rank == 0 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(recipe, count, args.config, first)
+    if rank == 0 and base_sample is not None:
+        srec, scount, what, host_user, gpu_prefix = base_sample
+        result["cpu_baseline"] = cpu_baseline(args.config, srec, scount, what, host_user, origin,
+                                              gpu_prefix)
+    elif rank == 0:
+        result["cpu_baseline"] = None   # timed on rank 0 at N = 1 only
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

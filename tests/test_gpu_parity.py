@@ -383,3 +383,89 @@ def test_darray_roundtrip(device):
         size, gs, dist, darg, ps, order, old = random_darray(rng)
         rec = ("darray", size, rng.randrange(size), gs, dist, darg, ps, order, old)
         _roundtrip(R.Built(rec), rng.choice([1, 2]), device, n)
+
+
+def _segments(total, seg):
+    """position.c create_segments + shuffle_segments (position.c:45-112)."""
+    segs = [(p, min(seg, total - p)) for p in range(0, total, seg)]
+    n = len(segs)
+    for i in range(0, n // 2, 2):
+        segs[i], segs[n - i - 1] = segs[n - i - 1], segs[i]
+    return segs
+
+
+@pytest.mark.parametrize("case", ["position", "position_noncontig"])
+def test_reference_position_tests(device, case):
+    """position.c (MPI_LONG_DOUBLE_INT x 2048) and position_noncontig.c (vector(150,1,2)
+    of int): 113-byte segments, shuffled, packed as byte windows (the UCX form) and
+    unpacked through set_position; the receive buffer must equal the send buffer (gaps of
+    the vector keep 0xdeadbeef)."""
+    import torch
+    import ompi_amd
+    from ompi_amd import datatype as D
+    if case == "position":
+        dt = D.create_struct([1, 1], [0, 16], [D.predefined(D.FLOAT16), D.predefined(D.INT4)]).commit()
+        count, nbytes = 2048, 32 * 2048
+        send = (torch.arange(nbytes, dtype=torch.int32) * 7 % 251 + 1).to(torch.uint8)
+        recv0 = torch.zeros(nbytes, dtype=torch.uint8)
+    else:
+        dt = D.create_vector(150, 1, 2, D.predefined(D.INT4)).commit()
+        count, nbytes = 1, 300 * 4
+        send = torch.arange(300, dtype=torch.int32).view(torch.uint8)
+        recv0 = torch.full((300,), 0xdeadbeef - 2 ** 32, dtype=torch.int32).view(torch.uint8)
+    send, recv = send.to(device), recv0.to(device)
+    total = ompi_amd.pack_size(count, dt)
+    segs = _segments(total, 113)
+    bufs = [torch.zeros(n, dtype=torch.uint8, device=device) for _, n in segs]
+    for (p, n), b in zip(segs, bufs):
+        assert ompi_amd.convertor.pack_window(dt, count, send, p, b, n) == n
+    conv = ompi_amd.Convertor().prepare_for_recv(dt, count, recv)
+    for (p, n), b in zip(segs, bufs):
+        assert conv.set_position(p) == p
+        rc, lens, md = conv.unpack([(b, n)])
+        assert md == n
+    got = _host(recv)
+    if case == "position":
+        want = np.zeros((count, 32), dtype=np.uint8)
+        want[:, :20] = send.cpu().numpy().reshape(count, 32)[:, :20]
+        np.testing.assert_array_equal(got, want.reshape(-1))
+    else:
+        want = np.where(np.arange(300) % 2 == 1, np.int32(0xdeadbeef - 2 ** 32),
+                        np.arange(300, dtype=np.int32))
+        np.testing.assert_array_equal(got.view(np.int32), want)
+
+
+def test_reference_partial_c(device):
+    """partial.c: contiguous(2, vector(3,2,4) double) x 3 unpacked in 28-byte chunks; after
+    every chunk all bytes received so far are in place (partial.c:95-140)."""
+    import torch
+    import ompi_amd
+    from ompi_amd import datatype as D
+    base = D.create_vector(3, 2, 4, D.predefined(D.FLOAT8))
+    vec = D.create_contiguous(2, base).commit()
+    count = 3
+    info = vec.info()
+    size, ext = info["size"], info["ub"] - info["lb"]
+    bext = base.info()["ub"] - base.info()["lb"]
+    packed = torch.tensor([float(i % 2) for i in range(size * count // 8)], dtype=torch.float64,
+                          device=device)
+    array = torch.zeros(ext * count // 8, dtype=torch.float64, device=device)
+    conv = ompi_amd.Convertor().prepare_for_recv(vec, count, array)
+    length = 0
+    pk = packed.view(torch.uint8)
+    while length < size * count:
+        n = min(28, size * count - length)
+        rc, _, md = conv.unpack([(pk[length:].data_ptr(), n)])
+        length += md
+        a = array.cpu().numpy()
+        idx = checked = 0
+        for m in range(count):
+            for k in range(2):
+                for j in range(3):
+                    for i in range(2):
+                        checked += 8
+                        if checked > length:
+                            break
+                        e = (m * ext + k * bext) // 8 + j * 4 + i
+                        assert a[e] == float(idx % 2), (length, m, k, j, i)
+                        idx += 1
