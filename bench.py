@@ -171,6 +171,45 @@ def cpu_baseline(name, srec, scount, what, host_user, origin, gpu_prefix, budget
                       f"oracle/ddt_oracle.c position-sharded over {threads} threads"}
 
 
+# ------------------------------------------------------------------ latency
+def single_face_latency(dev, stream, user, origin, reps=200):
+    """one 512 KiB face of one field is launch-bound.  Reports the
+    kernel time (HIP events) and the synchronous MPI_Pack call time (host wall clock, plan
+    cached) of packing ONE x face and ONE z face of field 0."""
+    import torch
+    import ompi_amd
+    from ompi_amd import recipe as ER
+    out = {}
+    for name, rec in (("x", face_recipes()["x"]), ("z", face_recipes()["z"])):
+        ft = ER.build_committed(rec)
+        fs = ft.info()["size"]
+        buf = torch.empty(fs, dtype=torch.uint8, device=dev)
+        c = ompi_amd.Convertor()
+        c.set_stream(stream, True)
+        for _ in range(5):
+            c.prepare_for_send(ft, 1, user.data_ptr() + origin)
+            c.pack([(buf, fs)])
+        torch.cuda.synchronize()
+        evs = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            c.prepare_for_send(ft, 1, user.data_ptr() + origin)
+            c.pack([(buf, fs)])
+            b.record(stream)
+            evs.append((a, b))
+            torch.cuda.synchronize()
+        k_us = float(np.median([a.elapsed_time(b) for a, b in evs])) * 1e3
+        walls = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            ompi_amd.pack(user.data_ptr() + origin, 1, ft, buf, fs, 0)   # synchronous MPI_Pack
+            walls.append(time.perf_counter() - t0)
+        out[name] = {"bytes": fs, "kernel_us": round(k_us, 2),
+                     "mpi_pack_call_us": round(float(np.median(walls)) * 1e6, 2)}
+    return out
+
+
 # ------------------------------------------------------------------ main
 def main():
     ap = argparse.ArgumentParser()
@@ -315,6 +354,9 @@ def main():
         if os.path.exists(tfile):
             with open(tfile) as f:
                 result["roofline"]["traffic"] = json.load(f).get("bytes_per_step")
+
+    if rank == 0 and args.config == "cfg2":
+        result["single_face_latency_us"] = single_face_latency(dev, stream, user, origin)
 
     if args.faces and rank == 0:
         faces = {}
