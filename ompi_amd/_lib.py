@@ -9,7 +9,9 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libddt_hip.so")
+# DDT_LIB_PATH selects another build of the same library (e.g. the host-ASAN build of
+# scripts/asan_cpu_tests.sh); the default is the in-tree gfx950 build.
+LIB_PATH = os.environ.get("DDT_LIB_PATH") or os.path.join(HERE, "libddt_hip.so")
 
 c_size_t = ctypes.c_size_t
 c_ssize_t = ctypes.c_ssize_t

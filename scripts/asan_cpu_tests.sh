@@ -1,0 +1,19 @@
+#!/bin/bash
+# Host-side AddressSanitizer run of the CPU test suite (type map, plan compiler, raw
+# export, external32 signature: everything that runs without a GPU).  The device code is
+# compiled normally; only host objects are instrumented (-Xarch_host -fsanitize=address).
+set -e
+cd "$(dirname "$0")/../ompi_amd/csrc"
+mkdir -p build_asan
+for f in ddt_typemap ddt_plan ddt_convertor ddt_external; do
+  /opt/rocm/bin/hipcc -std=c++17 -O1 -g -fPIC -I../../include --offload-arch=gfx950 \
+    -Xarch_host -fsanitize=address -fno-omit-frame-pointer -c $f.cpp -o build_asan/$f.o
+done
+/opt/rocm/bin/hipcc -std=c++17 -O1 -fPIC -I../../include --offload-arch=gfx950 -x hip \
+  -c ddt_kernels.hip -o build_asan/ddt_kernels.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Xarch_host -fsanitize=address \
+  -o build_asan/libddt_hip_asan.so build_asan/*.o
+cd ../..
+ASAN_RT=$(/opt/rocm/bin/hipcc -print-file-name=libclang_rt.asan-x86_64.so)
+DDT_LIB_PATH=$PWD/ompi_amd/csrc/build_asan/libddt_hip_asan.so LD_PRELOAD=$ASAN_RT \
+  ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 python -m pytest tests -q -x -m "not gpu" -p no:cacheprovider "$@"
