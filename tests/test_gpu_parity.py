@@ -469,3 +469,52 @@ def test_reference_partial_c(device):
                         e = (m * ext + k * bext) // 8 + j * 4 + i
                         assert a[e] == float(idx % 2), (length, m, k, j, i)
                         idx += 1
+
+
+def test_concurrent_streams_and_descriptor_cache_eviction(device):
+    """Four host threads, each with its own HIP stream and asynchronous convertor, pack
+    random fragments of one shared committed type.  More than 32 distinct windows force
+    descriptor-set evictions while launches are still in flight (the plan's graveyard),
+    and the per-type plan is built under contention.  Every byte must match the oracle."""
+    import threading
+    import torch
+    import ompi_amd
+    rec = ("struct", [2, 1, 3], [0, 40, 96],
+           [("vector", 5, 2, 3, ("basic", 16)), ("basic", 6), ("hvector", 4, 1, 12, ("basic", 15))])
+    b = R.Built(rec)
+    e = b.engine()
+    info = b.o.info()
+    count = 64
+    size = info["size"] * count
+    span, origin = R.layout(info, count)
+    host = R.fill(span, 99)
+    user = _dev(host, device)
+    ref = np.frombuffer(b.o.pack(count, host, origin, 0, size, element_granular=False), dtype=np.uint8)
+    outs = [torch.zeros(size, dtype=torch.uint8, device=device) for _ in range(4)]
+    errors = []
+
+    def worker(t):
+        try:
+            rng = random.Random(t)
+            s = torch.cuda.Stream(device)
+            conv = ompi_amd.Convertor()
+            conv.set_stream(s, True)
+            cuts = sorted(set([0, size] + [rng.randrange(size) for _ in range(60)]))
+            order = list(range(len(cuts) - 1))
+            rng.shuffle(order)
+            for k in order:
+                p0, p1 = cuts[k], cuts[k + 1]
+                ompi_amd.convertor.pack_window(e, count, user.data_ptr() + origin, p0,
+                                               outs[t].data_ptr() + p0, p1 - p0, stream=s)
+            s.synchronize()
+        except Exception as ex:   # surfaced below
+            errors.append(repr(ex))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors
+    for t in range(4):
+        np.testing.assert_array_equal(_host(outs[t]), ref)
