@@ -89,11 +89,15 @@ struct Item {
 
 // Descriptors passed by value in the kernel-argument segment (<= 4 KiB).
 constexpr uint32_t INLINE_ITEMS = 7;
-struct ItemBlock {
+// Kernel-argument block of NI descriptors: the launch copies only sizeof(ItemBlockN<NI>)
+// bytes of arguments, so a one-leaf type pays for 528 B, not 3.6 KB.
+template <uint32_t NI>
+struct ItemBlockN {
     uint32_t n;
     uint32_t pad[3];
-    Item items[INLINE_ITEMS];
+    Item items[NI];
 };
+using ItemBlock = ItemBlockN<INLINE_ITEMS>;
 static_assert(sizeof(Item) == 512, "Item layout is shared with tests/plan_emu.py");
 static_assert(sizeof(ItemBlock) <= 4096, "kernel argument segment limit");
 

@@ -420,14 +420,34 @@ __global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restric
 
 // Small launches carry their descriptors in the kernel-argument segment: no device
 // buffer, no upload, no cache entry (fragment pipelines, windows, one-off messages).
-template <int DIR, bool LISTS>
-__global__ __launch_bounds__(THREADS) void ddt_move_inline_kernel(ItemBlock blk)
+template <int DIR, bool LISTS, uint32_t NI>
+__global__ __launch_bounds__(THREADS) void ddt_move_inline_kernel(ItemBlockN<NI> blk)
 {
     // read the block in place from the kernarg segment (taking the address of `blk`
-    // would copy 3.6 KB to scratch)
-    const ItemBlock *kb = reinterpret_cast<const ItemBlock *>(
+    // would copy it to scratch)
+    const ItemBlockN<NI> *kb = reinterpret_cast<const ItemBlockN<NI> *>(
         (const void *) __builtin_amdgcn_kernarg_segment_ptr());
     move_body<DIR, LISTS>(kb->items, kb->n);
+}
+
+template <int DIR, bool LISTS, uint32_t NI>
+static void launch_inline_n(const ItemBlock &blk, uint32_t ntasks, hipStream_t stream)
+{
+    ItemBlockN<NI> b;
+    b.n = blk.n;
+    for (uint32_t i = 0; i < blk.n; ++i)
+        b.items[i] = blk.items[i];
+    hipLaunchKernelGGL((ddt_move_inline_kernel<DIR, LISTS, NI>), dim3(ntasks), dim3(THREADS), 0,
+                       stream, b);
+}
+
+template <int DIR, bool LISTS>
+static void launch_inline(const ItemBlock &blk, uint32_t ntasks, hipStream_t stream)
+{
+    if (blk.n == 1) launch_inline_n<DIR, LISTS, 1>(blk, ntasks, stream);
+    else if (blk.n == 2) launch_inline_n<DIR, LISTS, 2>(blk, ntasks, stream);
+    else if (blk.n <= 4) launch_inline_n<DIR, LISTS, 4>(blk, ntasks, stream);
+    else launch_inline_n<DIR, LISTS, INLINE_ITEMS>(blk, ntasks, stream);
 }
 
 template <int DIR>
@@ -448,11 +468,11 @@ hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bo
     if (ntasks == 0 || blk.n == 0)
         return hipSuccess;
     if (dir == 0) {
-        if (lists) hipLaunchKernelGGL((ddt_move_inline_kernel<0, true>), dim3(ntasks), dim3(THREADS), 0, stream, blk);
-        else hipLaunchKernelGGL((ddt_move_inline_kernel<0, false>), dim3(ntasks), dim3(THREADS), 0, stream, blk);
+        if (lists) launch_inline<0, true>(blk, ntasks, stream);
+        else launch_inline<0, false>(blk, ntasks, stream);
     } else {
-        if (lists) hipLaunchKernelGGL((ddt_move_inline_kernel<1, true>), dim3(ntasks), dim3(THREADS), 0, stream, blk);
-        else hipLaunchKernelGGL((ddt_move_inline_kernel<1, false>), dim3(ntasks), dim3(THREADS), 0, stream, blk);
+        if (lists) launch_inline<1, true>(blk, ntasks, stream);
+        else launch_inline<1, false>(blk, ntasks, stream);
     }
     return hipGetLastError();
 }
