@@ -950,6 +950,8 @@ int ddt_tune(const char *key, long value)
         tuning().interleave = value;
     else if (k == "policy")
         tuning().policy = int(value);
+    else if (k == "wt")
+        tuning().wt = value < 0 ? -1 : int(value > 2 ? 2 : value);
     else if (k == "reset")
         tuning() = Tuning{};
     else

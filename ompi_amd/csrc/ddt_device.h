@@ -84,7 +84,9 @@ struct Item {
     uint32_t nt;            // user-side accesses non-temporal (sparse gathers over > MALL spans)
     int64_t w0, w1;         // LIST_VAR / FRAG: window [w0, w1) in packed-stream coordinates
     uint64_t nbytes;        // FRAG: bytes
-    uint64_t pad2;          // keeps sizeof(Item) == 512
+    uint32_t wt;            // store policy: 1 = user-side stores (unpack) write through L2 (sc1);
+                            // 2 = every store of the launch sc1
+    uint32_t pad2;          // keeps sizeof(Item) == 512
 };
 
 // Descriptors passed by value in the kernel-argument segment (<= 4 KiB).

@@ -111,13 +111,36 @@ template <typename T, bool NT> __device__ __forceinline__ T ld(const T *p)
     if constexpr (NT) return __builtin_nontemporal_load(p);
     else return *p;
 }
-template <typename T, bool NT> __device__ __forceinline__ void st(T *p, T v)
+// Write-through store (sc1): the line is not allocated dirty in L2; the bytes go on to
+// the memory side with their byte mask (Item::wt, use_wt in ddt_plan.cpp).
+__device__ __forceinline__ void st_wt(uint8_t *p, uint8_t v)
 {
-    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    asm volatile("global_store_byte %0, %1, off sc1" ::"v"(p), "v"(uint32_t(v)) : "memory");
+}
+__device__ __forceinline__ void st_wt(uint16_t *p, uint16_t v)
+{
+    asm volatile("global_store_short %0, %1, off sc1" ::"v"(p), "v"(uint32_t(v)) : "memory");
+}
+__device__ __forceinline__ void st_wt(uint32_t *p, uint32_t v)
+{
+    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_wt(u32x2 *p, u32x2 v)
+{
+    asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_wt(u32x4 *p, u32x4 v)
+{
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+template <typename T, bool WT> __device__ __forceinline__ void st(T *p, T v)
+{
+    if constexpr (WT) st_wt(p, v);
     else *p = v;
 }
 
-template <int U, int DIR, int ND, bool NT>
+template <int U, int DIR, int ND, bool NT, bool WT>
 __device__ __forceinline__ void run_affine(const Item *it, uint32_t ub, uint32_t ue)
 {
     using T = typename Vec<U>::T;
@@ -147,7 +170,7 @@ __device__ __forceinline__ void run_affine(const Item *it, uint32_t ub, uint32_t
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (dst[k])
-                st<T, false>(dst[k], v[k]);   // NT stores measured slower (scatter 51 vs 18 us)
+                st<T, WT>(dst[k], v[k]);   // (nt stores measured slower: scatter 51 vs 18 us)
     }
 }
 
@@ -177,7 +200,7 @@ __device__ __noinline__ void run_list_uni64(const Item *it, uint64_t ub, uint64_
 // Index list with one block length: all K displacement loads of a round are issued
 // (coalesced) before the K dependent gathers, so each round pays two memory latencies
 // instead of 2K.
-template <int U, int DIR>
+template <int U, int DIR, bool WT>
 __device__ __forceinline__ void run_list_uni(const Item *it, uint32_t ub, uint32_t ue)
 {
     using T = typename Vec<U>::T;
@@ -226,7 +249,7 @@ __device__ __forceinline__ void run_list_uni(const Item *it, uint32_t ub, uint32
         for (int k = 0; k < K; ++k) {
             if (base + uint32_t(k) * THREADS < ue) {
                 T *dst = reinterpret_cast<T *>(DIR == 0 ? packed + po[k] : user + uo[k] + d[k]);
-                *dst = v[k];
+                st<T, WT>(dst, v[k]);
             }
         }
     }
@@ -295,7 +318,7 @@ __device__ __forceinline__ void run_list_var(const Item *it, uint64_t ub, uint64
 
 // Deep nests (> 4 dims) are rare: their dims are re-read from the (cached) item on every
 // unit instead of being held in registers, which keeps the kernel's SGPR budget small.
-template <int U, int DIR, bool NT>
+template <int U, int DIR, bool NT, bool WT>
 __device__ __forceinline__ void run_affine_deep(const Item *it, uint32_t ub, uint32_t ue)
 {
     using T = typename Vec<U>::T;
@@ -318,31 +341,50 @@ __device__ __forceinline__ void run_affine_deep(const Item *it, uint32_t ub, uin
         po += int64_t(blk) * it->pstr[0];
         const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
         T *dst = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
-        st<T, false>(dst, ld<T, NT && DIR == 0>(src));
+        st<T, WT>(dst, ld<T, NT && DIR == 0>(src));
     }
 }
 
-template <int U, int DIR, bool NT>
+template <int U, int DIR, bool NT, bool WT>
 __device__ __forceinline__ void dispatch_affine_u(const Item *it, uint32_t ub, uint32_t ue)
 {
     switch (it->ndim) {
-    case 1: run_affine<U, DIR, 1, NT>(it, ub, ue); break;
-    case 2: run_affine<U, DIR, 2, NT>(it, ub, ue); break;
-    case 3: run_affine<U, DIR, 3, NT>(it, ub, ue); break;
-    case 4: run_affine<U, DIR, 4, NT>(it, ub, ue); break;
-    default: run_affine_deep<U, DIR, NT>(it, ub, ue); break;
+    case 1: run_affine<U, DIR, 1, NT, WT>(it, ub, ue); break;
+    case 2: run_affine<U, DIR, 2, NT, WT>(it, ub, ue); break;
+    case 3: run_affine<U, DIR, 3, NT, WT>(it, ub, ue); break;
+    case 4: run_affine<U, DIR, 4, NT, WT>(it, ub, ue); break;
+    default: run_affine_deep<U, DIR, NT, WT>(it, ub, ue); break;
     }
 }
 
-template <int DIR, bool NT>
+template <int DIR, bool NT, bool WT>
 __device__ __forceinline__ void dispatch_affine(const Item *it, uint32_t ub, uint32_t ue)
 {
     switch (it->U) {
-    case 16: dispatch_affine_u<16, DIR, NT>(it, ub, ue); break;
-    case 8: dispatch_affine_u<8, DIR, NT>(it, ub, ue); break;
-    case 4: dispatch_affine_u<4, DIR, NT>(it, ub, ue); break;
-    case 2: dispatch_affine_u<2, DIR, NT>(it, ub, ue); break;
-    default: dispatch_affine_u<1, DIR, NT>(it, ub, ue); break;
+    case 16: dispatch_affine_u<16, DIR, NT, WT>(it, ub, ue); break;
+    case 8: dispatch_affine_u<8, DIR, NT, WT>(it, ub, ue); break;
+    case 4: dispatch_affine_u<4, DIR, NT, WT>(it, ub, ue); break;
+    case 2: dispatch_affine_u<2, DIR, NT, WT>(it, ub, ue); break;
+    default: dispatch_affine_u<1, DIR, NT, WT>(it, ub, ue); break;
+    }
+}
+
+// wt = 1 asks for write-through user-side stores (unpack); wt = 2 for every store.
+template <int DIR>
+__device__ __forceinline__ bool wt_stores(const Item *it)
+{
+    return it->wt == 2 || (DIR == 1 && it->wt == 1);
+}
+
+template <int DIR, bool WT>
+__device__ __forceinline__ void dispatch_list_uni(const Item *it, uint32_t ub, uint32_t ue)
+{
+    switch (it->U) {
+    case 16: run_list_uni<16, DIR, WT>(it, ub, ue); break;
+    case 8: run_list_uni<8, DIR, WT>(it, ub, ue); break;
+    case 4: run_list_uni<4, DIR, WT>(it, ub, ue); break;
+    case 2: run_list_uni<2, DIR, WT>(it, ub, ue); break;
+    default: run_list_uni<1, DIR, WT>(it, ub, ue); break;
     }
 }
 
@@ -374,8 +416,13 @@ __device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32
             default: run_affine64<1, DIR>(it, ub, ue); break;
             }
         } else {
-            if (it->nt) dispatch_affine<DIR, true>(it, uint32_t(ub), uint32_t(ue));
-            else dispatch_affine<DIR, false>(it, uint32_t(ub), uint32_t(ue));
+            if (wt_stores<DIR>(it)) {
+                if (DIR == 0 && it->nt) dispatch_affine<DIR, true, true>(it, uint32_t(ub), uint32_t(ue));
+                else dispatch_affine<DIR, false, true>(it, uint32_t(ub), uint32_t(ue));
+            } else {
+                if (DIR == 0 && it->nt) dispatch_affine<DIR, true, false>(it, uint32_t(ub), uint32_t(ue));
+                else dispatch_affine<DIR, false, false>(it, uint32_t(ub), uint32_t(ue));
+            }
         }
         break;
     case ITEM_LIST_UNI:
@@ -389,13 +436,8 @@ __device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32
             default: run_list_uni64<1, DIR>(it, ub, ue); break;
             }
         } else {
-            switch (it->U) {
-            case 16: run_list_uni<16, DIR>(it, uint32_t(ub), uint32_t(ue)); break;
-            case 8: run_list_uni<8, DIR>(it, uint32_t(ub), uint32_t(ue)); break;
-            case 4: run_list_uni<4, DIR>(it, uint32_t(ub), uint32_t(ue)); break;
-            case 2: run_list_uni<2, DIR>(it, uint32_t(ub), uint32_t(ue)); break;
-            default: run_list_uni<1, DIR>(it, uint32_t(ub), uint32_t(ue)); break;
-            }
+            if (wt_stores<DIR>(it)) dispatch_list_uni<DIR, true>(it, uint32_t(ub), uint32_t(ue));
+            else dispatch_list_uni<DIR, false>(it, uint32_t(ub), uint32_t(ue));
         }
         break;
     case ITEM_LIST_VAR:

@@ -28,6 +28,8 @@ Tuning &tuning()
             v.nt = e[0] == '1' ? 1 : 0;
         if (const char *e = std::getenv("DDT_TASK_KB"))
             v.task_kb = std::atol(e);
+        if (const char *e = std::getenv("DDT_WT"))
+            v.wt = std::atoi(e);
         return v;
     }();
     return t;
@@ -297,6 +299,29 @@ bool use_nt(uint32_t U, uint64_t blen, const std::vector<LeafDim> &dims)
     return span > (192ull << 20);
 }
 
+// Write-through (sc1) stores: a scattered narrow store that misses L2 is sent on to the
+// memory side at once instead of allocating a partially dirty L2 line that is evicted
+// later.  Measured (scripts/ab.py, profiles/r1_wt_ab.log): the unpack-only loop of both x
+// faces 38.3 -> 29.1 us; neutral in pack+unpack pairs (the memory-side work is the same);
+// 3 % slower on dense partial-line leaves (cfg5 records), so auto = isolated small blocks
+// only: blen <= 8 and every stride >= 128 B (one block per L2 line).  Returns Item::wt.
+// DDT_WT / ddt_tune("wt"): 0 off, 1 every sparse leaf (U <= 8, blen <= 64), 2 all stores.
+uint32_t use_wt(uint32_t U, uint64_t blen, const std::vector<LeafDim> *dims)
+{
+    const int force = tuning().wt;
+    const bool sparse = U <= 8 && blen <= 64;
+    if (force == 2)
+        return 2;
+    if (force == 1)
+        return sparse ? 1 : 0;
+    if (force == 0 || !dims || dims->empty() || blen > 8)
+        return 0;
+    for (const LeafDim &d : *dims)
+        if (d.cnt > 1 && absu(d.sstr) < 128)
+            return 0;
+    return 1;
+}
+
 uint64_t units_per_task(uint32_t U)
 {
     uint64_t u = (32u << 10) / U;   // provisional; assign_tasks() sets the final size
@@ -401,6 +426,7 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
             if (u1 * U > leaf_total || total_units * U != leaf_total)
                 throw std::runtime_error("plan: affine unit range outside its leaf");
             it.nt = use_nt(U, blen, sd) ? 1 : 0;
+            it.wt = use_wt(U, blen, &sd);
             it.u0 = u0;
             it.u1 = u1;
             it.units_per_task = units_per_task(U);
@@ -463,6 +489,7 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
             if (u1 * U > leaf_total || total_units * U != leaf_total)
                 throw std::runtime_error("plan: list unit range outside its leaf");
             it.ulen = X.ulen;
+            it.wt = use_wt(U, X.ulen, nullptr);
             it.ldisp = uint64_t(uintptr_t(D.disp));
             it.ldisp32 = D.disp32 ? 1 : 0;
             it.u0 = u0;

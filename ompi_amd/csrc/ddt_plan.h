@@ -18,6 +18,7 @@ struct Tuning {
     long task_kb = 0;  // packed KiB per workgroup task: 0 = adaptive
     long interleave = 0;  // >0: interleave items in runs of this many tasks
     int policy = 1;       // task sizing: 0 = v0 (~6 K tasks), 1 = per-leaf passes
+    int wt = -1;          // write-through (sc1) stores: -1 auto, 0 off, 1 sparse user side, 2 all
 };
 Tuning &tuning();
 
