@@ -229,6 +229,11 @@ int ddt_copy_content_same_ddt(const ddt_datatype_t *type, size_t count, void *ds
 
 /* Plan introspection for tests/benchmarks: number of leaves, device metadata bytes. */
 int ddt_type_plan_info(const ddt_datatype_t *type, int64_t *out4);
+/* Which engine whole-message moves of this type use: out4 = [state, device bytes, chunks,
+ * U slots] of the address-ordered index-list engine (ddt_sorted.hip); state 1 = built and in
+ * use, 0 = not tried yet (built at the first whole-message pack/unpack), -1 = not applicable
+ * (the per-block list kernel runs). */
+int ddt_type_engine_info(const ddt_datatype_t *type, int64_t *out4);
 /* ---- introspection for the CPU test-suite (no data movement; never used by pack/unpack) ----
  * ddt_type_plan_leaves: serialises the plan's leaf streams as int64 records
  *   [kind, blen, src_off, dst_off, ndim, list_leaf_index, (cnt, sstr, dstr) x ndim] and returns
@@ -246,8 +251,10 @@ int64_t ddt_type_plan_list(const ddt_datatype_t *type, size_t leaf, int64_t *dis
 /* Tuning knobs for A/B measurements (affect descriptor sets built afterwards):
  * "nt" = user-side non-temporal gathers (-1 auto, 0 off, 1 on); "task_kb" = packed KiB per
  * workgroup (0 adaptive); "policy" = task sizing (0 v0, 1 per-leaf passes); "interleave" =
- * reorder items in runs of this many tasks (0 off); "reset" = restore the defaults.
- * Environment: DDT_NT, DDT_TASK_KB. */
+ * reorder items in runs of this many tasks (0 off); "wt" = write-through stores (-1 auto,
+ * 0 off, 1 every sparse leaf, 2 all); "sorted" = address-ordered list engine (-1 auto from
+ * 1 Mi blocks, 0 off, n > 0 from n blocks; read when a type's plan first runs);
+ * "reset" = restore the defaults.  Environment: DDT_NT, DDT_TASK_KB, DDT_WT. */
 int ddt_tune(const char *key, long value);
 /* Library self-check of host-side index arithmetic (fast division); returns 0 on success. */
 int ddt_selftest(void);

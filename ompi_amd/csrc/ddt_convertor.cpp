@@ -85,6 +85,26 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     } catch (const std::exception &ex) {
         return fail(DDT_ERR_OUT_OF_RESOURCE, ex.what());
     }
+    // a whole-message move of a large single-element index list: address-ordered engine
+    if (!same_layout && wins.size() == 1 && wins[0].w0 == 0 && wins[0].w1 == count * uint64_t(t->size)
+        && (wins[0].ptr % 16) == 0) {
+        SortedList *SL = nullptr;
+        try {
+            SL = sorted_plan(t, P, user, stream);
+        } catch (const std::exception &ex) {
+            return fail(DDT_ERR_OUT_OF_RESOURCE, ex.what());
+        }
+        if (SL) {
+            const Leaf &L = P.leaves[0];
+            for (uint64_t i = 0; i < count; ++i) {
+                uint8_t *u = reinterpret_cast<uint8_t *>(user + uint64_t(L.list_shift) + uint64_t(P.dev[0].disp_base)
+                                                         + i * uint64_t(t->extent()));
+                uint8_t *pk = reinterpret_cast<uint8_t *>(wins[0].ptr + i * uint64_t(t->size));
+                HIPCHK(SL->run(u, pk, dir, stream));
+            }
+            return DDT_SUCCESS;
+        }
+    }
     std::shared_ptr<ItemSet> S;
     {
         std::lock_guard<std::mutex> g(P.mu);
@@ -804,6 +824,26 @@ int ddt_copy_content_same_ddt(const ddt_datatype_t *t, size_t count, void *dst, 
     return DDT_SUCCESS;
 }
 
+int ddt_type_engine_info(const ddt_datatype_t *t, int64_t *out4)
+{
+    if (!t || !out4)
+        return DDT_ERR_BAD_PARAM;
+    if (!(t->flags & F_COMMITTED))
+        return fail(DDT_ERR_NOT_COMMITTED, "datatype not committed");
+    std::shared_ptr<Plan> P;
+    try {
+        P = get_plan(const_cast<ddt_datatype *>(t));
+    } catch (const std::exception &ex) {
+        return fail(DDT_ERR_OUT_OF_RESOURCE, ex.what());
+    }
+    std::lock_guard<std::mutex> g(P->mu);
+    out4[0] = P->sorted_state;
+    out4[1] = P->sorted ? int64_t(P->sorted->dev_bytes) : 0;
+    out4[2] = P->sorted ? int64_t(P->sorted->nc) : 0;
+    out4[3] = P->sorted ? int64_t(P->sorted->slots) : 0;
+    return DDT_SUCCESS;
+}
+
 int ddt_type_plan_info(const ddt_datatype_t *t, int64_t *out4)
 {
     if (!t || !out4)
@@ -950,6 +990,8 @@ int ddt_tune(const char *key, long value)
         tuning().interleave = value;
     else if (k == "policy")
         tuning().policy = int(value);
+    else if (k == "sorted")
+        tuning().sorted = value;
     else if (k == "wt")
         tuning().wt = value < 0 ? -1 : int(value > 2 ? 2 : value);
     else if (k == "reset")

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include "ddt_device.h"
+#include "ddt_sorted.h"
 
 namespace ddt {
 
@@ -122,6 +123,10 @@ struct Plan {
     std::mutex mu;
     std::vector<std::shared_ptr<ItemSet>> cache;      // most recent first
     std::vector<std::shared_ptr<ItemSet>> graveyard;  // evicted, freed after a device drain
+    // address-ordered plan of a one-leaf single-element index list (ddt_sorted.hip):
+    // 0 = not tried yet, 1 = built, -1 = not applicable
+    int sorted_state = 0;
+    std::unique_ptr<SortedList> sorted;
     ~Plan();
 };
 

@@ -224,6 +224,90 @@ void ensure_device_lists(Plan &P)
     P.dev_ready = true;
 }
 
+// ------------------------------------------------------------------ address-ordered lists
+// A plan qualifies for the address-ordered engine (ddt_sorted.hip) when it is ONE index
+// list of small blocks (at most 32 bytes on average, every displacement and length a
+// multiple of an element size E of 4, 8 or 16 bytes) with no enclosing loops, at least
+// tuning().sorted blocks (auto: 1 Mi), a span of at most 64 elements per element moved,
+// and few enough elements that a (chunk, bucket) run averages at least half a 64-byte
+// segment.  The engine moves E-byte elements: a block of several elements (blocks merged
+// by the indexed constructors, ompi_datatype_create_indexed.c:59-67) contributes each of
+// them.  Overlapping blocks disqualify the plan (found while building).
+SortedList *sorted_plan(const ddt_datatype *t, Plan &P, uint64_t user, hipStream_t stream)
+{
+    (void) t;
+    const long knob = tuning().sorted;
+    if (knob == 0 || P.sorted_state < 0)
+        return nullptr;
+    if (P.leaves.size() != 1 || P.leaves[0].kind != LEAF_LIST || !P.leaves[0].dims.empty())
+        return nullptr;
+    const Leaf &L = P.leaves[0];
+    const IndexList &X = *L.list;
+    const DevList &D = P.dev[0];
+    const uint64_t nblk = X.nblk();
+    const uint64_t min_blocks = knob > 0 ? uint64_t(knob) : (1ull << 20);
+    const uint64_t g = X.disp_gcd | (X.len.empty() ? X.ulen : X.len_gcd);
+    uint64_t esz = 0, ne = 0;
+    for (uint64_t e = 16; e >= 4 && !esz; e /= 2) {
+        const uint64_t ch = (128ull << 10) / e;
+        if (g % e == 0 && X.total / e <= 2 * ch * ch / (64 / e)) {
+            esz = e;
+            ne = X.total / e;
+        }
+    }
+    if (!esz || nblk < min_blocks || X.total > 32 * nblk || !D.disp32) {
+        P.sorted_state = -1;
+        return nullptr;
+    }
+    const uint64_t span_elems = uint64_t(X.max_end - X.min_disp) / esz;
+    if (span_elems >= (1ull << 32) || span_elems > 64 * ne) {
+        P.sorted_state = -1;
+        return nullptr;
+    }
+    if ((user + uint64_t(L.list_shift) + uint64_t(D.disp_base)) % esz != 0)
+        return nullptr;   // this buffer only: the typed element loads need alignment
+    std::lock_guard<std::mutex> g_(P.mu);
+    if (P.sorted_state == 0) {
+        // element displacements (bytes, relative to the list minimum): the device list
+        // itself when every block is one element, else expanded here
+        const int32_t *ed = static_cast<const int32_t *>(D.disp);
+        void *tmp = nullptr;
+        if (!X.len.empty() || X.ulen != esz) {
+            std::vector<int32_t> h(ne);
+            size_t e = 0;
+            for (size_t i = 0; i < nblk; ++i) {
+                const int64_t b = X.disp[i] - D.disp_base;
+                const uint64_t len = X.len.empty() ? X.ulen : X.len[i];
+                for (uint64_t q = 0; q < len; q += esz)
+                    h[e++] = int32_t(b + int64_t(q));
+            }
+            if (hipMalloc(&tmp, ne * 4 + 16) != hipSuccess
+                || hipMemcpy(tmp, h.data(), ne * 4, hipMemcpyHostToDevice) != hipSuccess) {
+                if (tmp) (void) hipFree(tmp);
+                throw std::runtime_error("sorted list: element displacement upload");
+            }
+            ed = static_cast<const int32_t *>(tmp);
+        }
+        auto S = std::make_unique<SortedList>();
+        bool ok = false;
+        try {
+            ok = S->build(ed, uint32_t(ne), uint32_t(esz), span_elems, stream);
+        } catch (...) {
+            if (tmp) (void) hipFree(tmp);
+            throw;
+        }
+        if (tmp) (void) hipFree(tmp);
+        if (ok) {
+            P.dev_bytes += S->dev_bytes;
+            P.sorted = std::move(S);
+            P.sorted_state = 1;
+        } else {
+            P.sorted_state = -1;
+        }
+    }
+    return P.sorted_state == 1 ? P.sorted.get() : nullptr;
+}
+
 // ------------------------------------------------------------------ items for one call
 namespace {
 

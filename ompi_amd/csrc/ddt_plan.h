@@ -19,12 +19,16 @@ struct Tuning {
     long interleave = 0;  // >0: interleave items in runs of this many tasks
     int policy = 1;       // task sizing: 0 = v0 (~6 K tasks), 1 = per-leaf passes
     int wt = -1;          // write-through (sc1) stores: -1 auto, 0 off, 1 sparse user side, 2 all
+    long sorted = -1;     // address-ordered list engine: -1 auto, 0 off, n > 0 from n blocks up
 };
 Tuning &tuning();
 
 void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t user, uint64_t pk,
                  uint64_t W0, uint64_t W1, bool same_layout, std::vector<Item> &items);
 void assign_tasks(std::vector<Item> &items);
+// The address-ordered engine of plan P for a whole-message pack/unpack, built on first use;
+// null when the plan does not qualify (or `user` is misaligned for it).
+SortedList *sorted_plan(const ddt_datatype *t, Plan &P, uint64_t user, hipStream_t stream);
 uint32_t total_tasks(const std::vector<Item> &items);
 
 // ddt_kernels.hip: dir 0 = pack / typed copy (user side -> packed side), 1 = unpack.

@@ -1,0 +1,35 @@
+// ddt_sorted.h -- address-ordered two-pass plan of a large single-element index list
+// (ddt_sorted.hip).  Internal to libddt_hip.so.
+#pragma once
+
+#include <cstdint>
+
+#include <hip/hip_runtime.h>
+
+namespace ddt {
+
+struct SortedList {
+    uint32_t n = 0;          // blocks (one element each)
+    uint32_t esz = 0;        // element bytes: 4, 8 or 16
+    uint32_t ch = 0;         // elements per chunk (address order) == per bucket (packed order)
+    uint32_t seg = 0;        // elements per 64-byte segment of U
+    uint32_t nc = 0, nb = 0; // chunks, buckets
+    uint64_t slots = 0;      // U slots, runs padded to whole segments
+    uint64_t dev_bytes = 0;  // device bytes held (tables + U)
+    uint32_t *A = nullptr;       // [n] element offset (units of esz) of the j-th block in address order
+    uint16_t *SL = nullptr;      // [n] LDS slot of the j-th block inside its chunk
+    uint16_t *cnt16 = nullptr;   // [nc][nb] blocks of chunk c whose packed position is in bucket k
+    uint16_t *off16 = nullptr;   // [nc][nb] exclusive prefix of cnt16 over k
+    uint32_t *ub = nullptr;      // [nc][nb] first U slot of run (c, k); U is bucket-major
+    uint32_t *bstart = nullptr;  // [nb + 1] first U slot of bucket k
+    uint16_t *upos = nullptr;    // [slots] position inside its bucket, 0xFFFF = padding
+    void *U = nullptr;           // [slots] scratch elements
+    hipEvent_t done = nullptr;   // recorded after every run (U reuse across streams)
+    hipStream_t last_stream = nullptr;
+    bool used = false;
+    ~SortedList();
+    bool build(const int32_t *disp, uint32_t n, uint32_t esz, uint64_t span_elems, hipStream_t stream);
+    hipError_t run(uint8_t *user, uint8_t *packed, int dir, hipStream_t stream);
+};
+
+}  // namespace ddt

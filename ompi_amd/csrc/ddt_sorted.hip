@@ -1,0 +1,466 @@
+// ddt_sorted.hip -- address-ordered two-pass engine for large single-element index lists
+// (MPI_Type_indexed / create_indexed_block / hindexed with one basic element per block,
+// BASELINE config 4: 64 Mi random floats out of a 1 GiB buffer).
+//
+// The direct list kernel (ddt_kernels.hip, run_list_uni) issues one memory request per
+// element: a random 4-byte gather over a span far beyond the Infinity Cache runs at the
+// memory-side request ceiling (~44 G requests/s, profiles/r1_ubench4_requests.log), and a
+// random 4-byte scatter is a read-modify-write of a 32-byte sector (~27 G/s).  Here the
+// user side is visited in ADDRESS order instead, so each 128-byte line is fetched (or
+// written) once, and the permutation back to type-map order runs through LDS:
+//
+//   pack   pass 1 (one workgroup per chunk of CH address-ordered elements):
+//            lds[SL[j]] = user[A[j]]        A = sorted element offsets, SL = LDS slot
+//            U[ubase(c,k) + q] = lds[off(c,k) + q]   runs grouped by destination bucket
+//          pass 2 (one workgroup per bucket of RG packed elements):
+//            lds[upos[s]] = U[s];  packed[k*RG + t] = lds[t]
+//   unpack is the same two passes reversed.
+//
+// U is bucket-major, each (chunk, bucket) run padded to a 64-byte segment so every U
+// store is a whole segment.  CH = RG = 128 KiB / element size, so the LDS image of a
+// chunk or a bucket is 128 KiB (gfx950: 160 KiB per CU).  The plan (A, SL, run tables,
+// upos) is built once on the device from the list's displacements: a bitmap of the
+// touched elements gives each block its address rank by popcount, and duplicate
+// displacements make the list ineligible (the direct kernel then keeps type-map order).
+//
+// This replaces, for such lists, the per-block cbmemcpy loop of
+// opal_pack_accelerator_simple / opal_unpack_accelerator_simple
+// (opal_datatype_pack_accelerator.c:161-295, opal_datatype_unpack_accelerator.c:210-368),
+// whose committed description for config 4 is 32 M DATA entries.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+
+#include "ddt_sorted.h"
+
+namespace ddt {
+
+namespace {
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <int E> struct Elem;
+template <> struct Elem<4> { using T = uint32_t; };
+template <> struct Elem<8> { using T = u32x2; };
+template <> struct Elem<16> { using T = u32x4; };
+
+constexpr int PT = 1024;               // threads per pass workgroup (16 wave64)
+constexpr int BT = 256;                // threads per build workgroup
+constexpr uint32_t LDS_BYTES = 128u << 10;
+constexpr uint16_t PAD = 0xFFFF;       // upos of a padding slot
+
+#define HK(x)                                                                                   \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess)                                                                   \
+            throw std::runtime_error(std::string("sorted list: ") + #x + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// ------------------------------------------------------------------ plan build kernels
+__global__ __launch_bounds__(BT) void k_bitmap(const int32_t *__restrict__ disp, uint32_t n, uint32_t shift,
+                                               uint32_t *__restrict__ bm, uint32_t *__restrict__ dup)
+{
+    for (uint32_t i = blockIdx.x * BT + threadIdx.x; i < n; i += gridDim.x * BT) {
+        const uint32_t a = uint32_t(disp[i]) >> shift;
+        const uint32_t bit = 1u << (a & 31);
+        const uint32_t old = atomicOr(&bm[a >> 5], bit);
+        if (old & bit)
+            atomicOr(dup, 1u);
+    }
+}
+
+__global__ __launch_bounds__(BT) void k_popc(const uint32_t *__restrict__ bm, uint32_t w, uint32_t *__restrict__ pc)
+{
+    for (uint32_t i = blockIdx.x * BT + threadIdx.x; i < w; i += gridDim.x * BT)
+        pc[i] = __popc(bm[i]);
+}
+
+__device__ __forceinline__ uint32_t rank_of(uint32_t a, const uint32_t *bm, const uint32_t *wpre)
+{
+    const uint32_t w = a >> 5, below = (1u << (a & 31)) - 1u;
+    return wpre[w] + __popc(bm[w] & below);
+}
+
+// A[j] = a; count (chunk, bucket) and remember each block's rank inside its run
+__global__ __launch_bounds__(BT) void k_rank(const int32_t *__restrict__ disp, uint32_t n, uint32_t shift,
+                                             const uint32_t *__restrict__ bm, const uint32_t *__restrict__ wpre,
+                                             uint32_t ch, uint32_t nb, uint32_t *__restrict__ A,
+                                             uint32_t *__restrict__ cnt, uint16_t *__restrict__ rr)
+{
+    for (uint32_t i = blockIdx.x * BT + threadIdx.x; i < n; i += gridDim.x * BT) {
+        const uint32_t a = uint32_t(disp[i]) >> shift;
+        const uint32_t j = rank_of(a, bm, wpre);
+        A[j] = a;
+        const uint32_t c = j / ch, k = i / ch;   // CH == RG
+        rr[i] = uint16_t(atomicAdd(&cnt[size_t(c) * nb + k], 1u));
+    }
+}
+
+// per chunk: off(c,k) = exclusive prefix over k of cnt(c,k); padded counts transposed to
+// bucket-major for the U layout scan
+__global__ __launch_bounds__(BT) void k_chunk_tables(const uint32_t *__restrict__ cnt, uint32_t nc, uint32_t nb,
+                                                     uint32_t seg, uint16_t *__restrict__ cnt16,
+                                                     uint16_t *__restrict__ off16, uint32_t *__restrict__ padT)
+{
+    __shared__ uint32_t part[BT];
+    const uint32_t c = blockIdx.x;
+    const uint32_t per = (nb + BT - 1) / BT;
+    const uint32_t k0 = threadIdx.x * per, k1 = min(nb, k0 + per);
+    uint32_t s = 0;
+    for (uint32_t k = k0; k < k1; ++k)
+        s += cnt[size_t(c) * nb + k];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int t = 0; t < BT; ++t) {
+            const uint32_t v = part[t];
+            part[t] = acc;
+            acc += v;
+        }
+    }
+    __syncthreads();
+    uint32_t o = part[threadIdx.x];
+    for (uint32_t k = k0; k < k1; ++k) {
+        const uint32_t v = cnt[size_t(c) * nb + k];
+        cnt16[size_t(c) * nb + k] = uint16_t(v);
+        off16[size_t(c) * nb + k] = uint16_t(o);
+        padT[size_t(k) * nc + c] = (v + seg - 1) / seg * seg;
+        o += v;
+    }
+}
+
+// chunk-major copy of the bucket-major run bases, and the first slot of every bucket
+__global__ __launch_bounds__(BT) void k_run_bases(const uint32_t *__restrict__ ubT, uint32_t nc, uint32_t nb,
+                                                  uint32_t total, uint32_t *__restrict__ ub,
+                                                  uint32_t *__restrict__ bstart)
+{
+    const size_t n = size_t(nc) * nb;
+    for (size_t x = size_t(blockIdx.x) * BT + threadIdx.x; x < n; x += size_t(gridDim.x) * BT) {
+        const uint32_t k = uint32_t(x / nc), c = uint32_t(x % nc);
+        ub[size_t(c) * nb + k] = ubT[x];
+        if (c == 0)
+            bstart[k] = ubT[x];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        bstart[nb] = total;
+}
+
+__global__ __launch_bounds__(BT) void k_assign(const int32_t *__restrict__ disp, uint32_t n, uint32_t shift,
+                                               const uint32_t *__restrict__ bm, const uint32_t *__restrict__ wpre,
+                                               uint32_t ch, uint32_t nb, const uint16_t *__restrict__ rr,
+                                               const uint16_t *__restrict__ off16, const uint32_t *__restrict__ ub,
+                                               uint16_t *__restrict__ SL, uint16_t *__restrict__ upos)
+{
+    for (uint32_t i = blockIdx.x * BT + threadIdx.x; i < n; i += gridDim.x * BT) {
+        const uint32_t a = uint32_t(disp[i]) >> shift;
+        const uint32_t j = rank_of(a, bm, wpre);
+        const uint32_t c = j / ch, k = i / ch;
+        const size_t ck = size_t(c) * nb + k;
+        SL[j] = uint16_t(off16[ck] + rr[i]);
+        upos[ub[ck] + rr[i]] = uint16_t(i - k * ch);
+    }
+}
+
+// ------------------------------------------------------------------ pass kernels
+// pack pass 1: gather the chunk in address order into LDS, emit its runs bucket by bucket
+template <int E>
+__global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, const uint32_t *__restrict__ A,
+                                              const uint16_t *__restrict__ SL, const uint16_t *__restrict__ cnt16,
+                                              const uint16_t *__restrict__ off16, const uint32_t *__restrict__ ub,
+                                              uint8_t *__restrict__ U, uint32_t n, uint32_t nb)
+{
+    using T = typename Elem<E>::T;
+    constexpr uint32_t CH = LDS_BYTES / E, SEG = 64 / E;
+    __shared__ T lds[CH + SEG];
+    const uint32_t c = blockIdx.x, j0 = c * CH;
+    const uint32_t m = min(CH, n - j0);
+    const T *src = reinterpret_cast<const T *>(user);
+    constexpr int K = 4;
+    for (uint32_t t0 = threadIdx.x; t0 < m; t0 += PT * K) {
+        T v[K];
+        uint32_t s[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const uint32_t t = t0 + q * PT;
+            if (t < m) {
+                s[q] = SL[j0 + t];
+                v[q] = src[A[j0 + t]];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            if (t0 + q * PT < m)
+                lds[s[q]] = v[q];
+    }
+    __syncthreads();
+    T *dst = reinterpret_cast<T *>(U);
+    const uint32_t sub = threadIdx.x / SEG, lane = threadIdx.x % SEG;
+    for (uint32_t k = sub; k < nb; k += PT / SEG) {
+        const size_t ck = size_t(c) * nb + k;
+        const uint32_t cn = cnt16[ck];
+        if (cn == 0)
+            continue;
+        const uint32_t o = off16[ck], b = ub[ck], pn = (cn + SEG - 1) / SEG * SEG;
+        for (uint32_t q = lane; q < pn; q += SEG)
+            dst[b + q] = lds[o + q];   // padding slots carry a neighbour's bytes: whole segments
+    }
+}
+
+// pack pass 2: the bucket's runs scatter into LDS by destination, then stream out
+template <int E>
+__global__ __launch_bounds__(PT) void k_pack2(const uint8_t *__restrict__ U, const uint16_t *__restrict__ upos,
+                                              const uint32_t *__restrict__ bstart, uint8_t *__restrict__ packed,
+                                              uint32_t n)
+{
+    using T = typename Elem<E>::T;
+    constexpr uint32_t RG = LDS_BYTES / E;
+    __shared__ T lds[RG];
+    const uint32_t k = blockIdx.x;
+    const uint32_t s0 = bstart[k], s1 = bstart[k + 1];
+    const T *src = reinterpret_cast<const T *>(U);
+    constexpr int K = 4;
+    for (uint32_t x0 = s0 + threadIdx.x; x0 < s1; x0 += PT * K) {
+        T v[K];
+        uint32_t p[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const uint32_t x = x0 + q * PT;
+            p[q] = PAD;
+            if (x < s1) {
+                p[q] = upos[x];
+                v[q] = src[x];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            if (p[q] != PAD)
+                lds[p[q]] = v[q];
+    }
+    __syncthreads();
+    const uint32_t m = min(RG, n - k * RG);
+    T *dst = reinterpret_cast<T *>(packed) + size_t(k) * RG;
+    for (uint32_t t = threadIdx.x; t < m; t += PT)
+        dst[t] = lds[t];
+}
+
+// unpack pass 2': the bucket's packed elements into LDS, then out to U in run order
+template <int E>
+__global__ __launch_bounds__(PT) void k_unpack2(const uint8_t *__restrict__ packed, const uint16_t *__restrict__ upos,
+                                                const uint32_t *__restrict__ bstart, uint8_t *__restrict__ U,
+                                                uint32_t n)
+{
+    using T = typename Elem<E>::T;
+    constexpr uint32_t RG = LDS_BYTES / E;
+    __shared__ T lds[RG];
+    const uint32_t k = blockIdx.x;
+    const uint32_t m = min(RG, n - k * RG);
+    const T *src = reinterpret_cast<const T *>(packed) + size_t(k) * RG;
+    for (uint32_t t = threadIdx.x; t < m; t += PT)
+        lds[t] = src[t];
+    __syncthreads();
+    const uint32_t s0 = bstart[k], s1 = bstart[k + 1];
+    T *dst = reinterpret_cast<T *>(U);
+    for (uint32_t x = s0 + threadIdx.x; x < s1; x += PT) {
+        const uint32_t p = upos[x];
+        T v{};
+        if (p != PAD)
+            v = lds[p];
+        dst[x] = v;   // padding slots written too: whole segments
+    }
+}
+
+// unpack pass 1': the chunk's runs into LDS, then scattered to the user side in address order
+template <int E>
+__global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, const uint32_t *__restrict__ A,
+                                                const uint16_t *__restrict__ SL, const uint16_t *__restrict__ cnt16,
+                                                const uint16_t *__restrict__ off16, const uint32_t *__restrict__ ub,
+                                                const uint8_t *__restrict__ U, uint32_t n, uint32_t nb)
+{
+    using T = typename Elem<E>::T;
+    constexpr uint32_t CH = LDS_BYTES / E, SEG = 64 / E;
+    __shared__ T lds[CH];
+    const uint32_t c = blockIdx.x, j0 = c * CH;
+    const uint32_t m = min(CH, n - j0);
+    const T *src = reinterpret_cast<const T *>(U);
+    const uint32_t sub = threadIdx.x / SEG, lane = threadIdx.x % SEG;
+    for (uint32_t k = sub; k < nb; k += PT / SEG) {
+        const size_t ck = size_t(c) * nb + k;
+        const uint32_t cn = cnt16[ck];
+        if (cn == 0)
+            continue;
+        const uint32_t o = off16[ck], b = ub[ck];
+        for (uint32_t q = lane; q < cn; q += SEG)
+            lds[o + q] = src[b + q];
+    }
+    __syncthreads();
+    T *dst = reinterpret_cast<T *>(user);
+    constexpr int K = 4;
+    for (uint32_t t0 = threadIdx.x; t0 < m; t0 += PT * K) {
+        uint32_t a[K];
+        T v[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const uint32_t t = t0 + q * PT;
+            if (t < m) {
+                a[q] = A[j0 + t];
+                v[q] = lds[SL[j0 + t]];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            if (t0 + q * PT < m)
+                dst[a[q]] = v[q];
+    }
+}
+
+uint32_t grid_for(uint64_t n, uint32_t threads)
+{
+    uint64_t b = (n + threads - 1) / threads;
+    return uint32_t(b < 1 ? 1 : (b > 65536 ? 65536 : b));
+}
+
+template <typename T>
+T *dalloc(size_t n, uint64_t &bytes)
+{
+    void *p = nullptr;
+    HK(hipMalloc(&p, n * sizeof(T) + 16));
+    bytes += n * sizeof(T);
+    return static_cast<T *>(p);
+}
+
+}  // namespace
+
+SortedList::~SortedList()
+{
+    if (done)
+        (void) hipEventSynchronize(done);
+    for (void *p : {(void *) A, (void *) SL, (void *) cnt16, (void *) off16, (void *) ub, (void *) bstart,
+                    (void *) upos, U})
+        if (p)
+            (void) hipFree(p);
+    if (done)
+        (void) hipEventDestroy(done);
+}
+
+// Build the plan on `stream` from the device displacement list (int32, relative to the
+// list's minimum displacement, every value a multiple of esz).  Returns false (and leaves
+// nothing allocated) when the displacements repeat.
+bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t span_elems, hipStream_t stream)
+{
+    n = n_;
+    esz = esz_;
+    ch = LDS_BYTES / esz;
+    seg = 64 / esz;
+    nc = (n + ch - 1) / ch;
+    nb = nc;   // RG == CH
+    uint32_t shift = 0;
+    while ((1u << shift) < esz)
+        ++shift;
+    const uint64_t words = (span_elems + 31) / 32 + 1;
+    const size_t runs = size_t(nc) * nb;
+    uint64_t tmp_bytes = 0;
+    uint32_t *bm = dalloc<uint32_t>(words, tmp_bytes), *wpre = dalloc<uint32_t>(words, tmp_bytes);
+    uint32_t *dup = dalloc<uint32_t>(1, tmp_bytes), *cnt = dalloc<uint32_t>(runs, tmp_bytes);
+    uint32_t *padT = dalloc<uint32_t>(runs + 1, tmp_bytes), *ubT = dalloc<uint32_t>(runs + 1, tmp_bytes);
+    uint16_t *rr = dalloc<uint16_t>(n, tmp_bytes);
+    void *scan_tmp = nullptr;
+    auto release = [&] {
+        for (void *p : {(void *) bm, (void *) wpre, (void *) dup, (void *) cnt, (void *) padT, (void *) ubT,
+                        (void *) rr, scan_tmp})
+            if (p)
+                (void) hipFree(p);
+    };
+    try {
+        HK(hipMemsetAsync(bm, 0, words * 4, stream));
+        HK(hipMemsetAsync(dup, 0, 4, stream));
+        HK(hipMemsetAsync(cnt, 0, runs * 4, stream));
+        hipLaunchKernelGGL(k_bitmap, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, bm, dup);
+        hipLaunchKernelGGL(k_popc, dim3(grid_for(words, BT)), dim3(BT), 0, stream, bm, uint32_t(words), wpre);
+        size_t tb = 0, tb2 = 0;
+        HK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, wpre, wpre, int(words), stream));
+        HK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, padT, ubT, int(runs + 1), stream));
+        HK(hipMalloc(&scan_tmp, std::max(tb, tb2) + 16));
+        HK(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, wpre, wpre, int(words), stream));
+        uint32_t hdup = 0;
+        HK(hipMemcpyAsync(&hdup, dup, 4, hipMemcpyDeviceToHost, stream));
+        HK(hipStreamSynchronize(stream));
+        if (hdup) {
+            release();
+            return false;
+        }
+        uint64_t bytes = 0;
+        A = dalloc<uint32_t>(n, bytes);
+        SL = dalloc<uint16_t>(n, bytes);
+        cnt16 = dalloc<uint16_t>(runs, bytes);
+        off16 = dalloc<uint16_t>(runs, bytes);
+        ub = dalloc<uint32_t>(runs, bytes);
+        bstart = dalloc<uint32_t>(nb + 1, bytes);
+        hipLaunchKernelGGL(k_rank, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, bm, wpre, ch, nb, A,
+                           cnt, rr);
+        HK(hipMemsetAsync(padT + runs, 0, 4, stream));
+        hipLaunchKernelGGL(k_chunk_tables, dim3(nc), dim3(BT), 0, stream, cnt, nc, nb, seg, cnt16, off16, padT);
+        HK(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb2, padT, ubT, int(runs + 1), stream));
+        uint32_t total = 0;
+        HK(hipMemcpyAsync(&total, ubT + runs, 4, hipMemcpyDeviceToHost, stream));
+        HK(hipStreamSynchronize(stream));
+        slots = total;
+        hipLaunchKernelGGL(k_run_bases, dim3(grid_for(runs, BT)), dim3(BT), 0, stream, ubT, nc, nb, total, ub,
+                           bstart);
+        upos = dalloc<uint16_t>(slots, bytes);
+        U = dalloc<uint8_t>(size_t(slots) * esz, bytes);
+        HK(hipMemsetAsync(upos, 0xFF, size_t(slots) * 2, stream));
+        hipLaunchKernelGGL(k_assign, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, bm, wpre, ch, nb,
+                           rr, off16, ub, SL, upos);
+        HK(hipGetLastError());
+        HK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        HK(hipStreamSynchronize(stream));
+        dev_bytes = bytes;
+    } catch (...) {
+        release();
+        throw;
+    }
+    release();
+    return true;
+}
+
+// One whole-list pack (dir 0) or unpack (dir 1) of one instance.  `user` points at the
+// list's first element (minimum displacement), `packed` at the instance's packed bytes.
+hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, hipStream_t stream)
+{
+    // U is one scratch per plan: a launch on another stream waits for the last one
+    if (used && last_stream != stream) {
+        hipError_t e = hipStreamWaitEvent(stream, done, 0);
+        if (e != hipSuccess)
+            return e;
+    }
+    const dim3 gc(nc), gb(nb), blk(PT);
+    uint8_t *u8 = static_cast<uint8_t *>(U);
+#define DDT_SORTED_LAUNCH(E)                                                                              \
+    if (dir == 0) {                                                                                       \
+        hipLaunchKernelGGL((k_pack1<E>), gc, blk, 0, stream, user, A, SL, cnt16, off16, ub, u8, n, nb);   \
+        hipLaunchKernelGGL((k_pack2<E>), gb, blk, 0, stream, u8, upos, bstart, packed, n);                \
+    } else {                                                                                              \
+        hipLaunchKernelGGL((k_unpack2<E>), gb, blk, 0, stream, packed, upos, bstart, u8, n);              \
+        hipLaunchKernelGGL((k_unpack1<E>), gc, blk, 0, stream, user, A, SL, cnt16, off16, ub, u8, n, nb); \
+    }
+    if (esz == 4) {
+        DDT_SORTED_LAUNCH(4)
+    } else if (esz == 8) {
+        DDT_SORTED_LAUNCH(8)
+    } else {
+        DDT_SORTED_LAUNCH(16)
+    }
+#undef DDT_SORTED_LAUNCH
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return e;
+    used = true;
+    last_stream = stream;
+    return hipEventRecord(done, stream);
+}
+
+}  // namespace ddt

@@ -100,6 +100,12 @@ class Datatype:
         check(lib().ddt_type_plan_info(self.handle, out), "ddt_type_plan_info")
         return dict(zip(("leaves", "device_bytes", "list_leaves", "max_dims"), list(out)))
 
+    def engine_info(self) -> dict:
+        """State of the address-ordered index-list engine (ddt_type_engine_info)."""
+        out = (ctypes.c_int64 * 4)()
+        check(lib().ddt_type_engine_info(self.handle, out), "ddt_type_engine_info")
+        return dict(zip(("sorted", "device_bytes", "chunks", "slots"), list(out)))
+
     def __repr__(self):
         return f"Datatype({self.name}, {self.info()})"
 

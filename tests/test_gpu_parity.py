@@ -518,3 +518,95 @@ def test_concurrent_streams_and_descriptor_cache_eviction(device):
     assert not errors, errors
     for t in range(4):
         np.testing.assert_array_equal(_host(outs[t]), ref)
+
+
+# ---------------------------------------------------------------- address-ordered list engine
+@pytest.fixture
+def sorted_from(request):
+    """Lower the address-ordered engine's block threshold for one test (ddt_tune sorted)."""
+    import ompi_amd
+    L = ompi_amd.lib()
+
+    def set_(n):
+        L.ddt_tune(b"sorted", n)
+    yield set_
+    L.ddt_tune(b"sorted", -1)
+
+
+@pytest.mark.parametrize("esz,count,density", [(4, 1, 4), (4, 2, 3), (8, 1, 5), (16, 2, 4), (4, 1, 64)])
+def test_sorted_list_engine(device, sorted_from, esz, count, density):
+    """Single-element index lists through ddt_sorted.hip (forced from 1 block): several
+    chunks and buckets, a ragged last chunk, count > 1; bit-exact vs the oracle both ways."""
+    sorted_from(1)
+    rng = np.random.default_rng(esz * 100 + count * 10 + density)
+    ch = (128 << 10) // esz
+    n = 3 * ch + 1237
+    unit = {4: ("basic", 15), 8: ("basic", 16), 16: ("basic", 16)}[esz]
+    per = esz // (8 if esz == 16 else esz)         # elements of `unit` per block
+    disps = (rng.permutation(density * n)[:n] * per).astype(np.int64)
+    b = R.Built(("indexed_block", per, disps.tolist(), unit))
+    _roundtrip(b, count, device, 5 + esz)
+    st = b.engine().engine_info()
+    assert st["sorted"] == 1 and st["chunks"] == (n + ch - 1) // ch, st
+
+
+def test_sorted_list_engine_falls_back(device, sorted_from):
+    """Overlapping blocks, windows and misaligned buffers keep the per-block kernel (type-map
+    order); a list of merged multi-element blocks still takes the engine.  All bit-exact."""
+    import torch
+    import ompi_amd
+    sorted_from(1)
+    rng = np.random.default_rng(11)
+    n = 40_000
+    d = rng.integers(0, 2 * n, n).astype(np.int64)   # with repeats
+    b = R.Built(("indexed_block", 1, d.tolist(), ("basic", 15)))
+    _roundtrip(b, 1, device, 3)
+    assert b.engine().engine_info()["sorted"] == -1
+    # variable lengths of 1..3 floats (elements of 4 bytes), non-overlapping
+    lens = rng.integers(1, 4, n)
+    starts = rng.permutation(4 * n)[:n] * 4
+    var = R.Built(("indexed", lens.tolist(), starts.tolist(), ("basic", 15)))
+    _roundtrip(var, 2, device, 4)
+    assert var.engine().engine_info()["sorted"] == 1
+    # fragments of a qualifying type use the per-block kernel; the whole message the engine
+    u = R.Built(("indexed_block", 1, rng.permutation(3 * n)[:n].tolist(), ("basic", 15)))
+    _roundtrip(u, 1, device, 6, frags=[4096, 12, 40])
+    assert u.engine().engine_info()["sorted"] == 0
+    _roundtrip(u, 1, device, 6)
+    assert u.engine().engine_info()["sorted"] == 1
+    # a user base that is not element-aligned: per-block kernel for that call
+    info = u.o.info()
+    size = info["size"]
+    span, origin = R.layout(info, 1)
+    host = R.fill(span + 8, 9)
+    user = _dev(host, device)
+    ref = np.frombuffer(u.o.pack(1, host[2:], origin, 0, size, element_granular=False), dtype=np.uint8)
+    packed = torch.zeros(size, dtype=torch.uint8, device=device)
+    assert ompi_amd.pack(user.data_ptr() + 2 + origin, 1, u.engine(), packed, size, 0) == size
+    np.testing.assert_array_equal(_host(packed), ref)
+
+
+def test_sorted_list_engine_auto(device):
+    """Default threshold (1 Mi blocks): a 2 Mi-block random permutation over 8 M floats takes
+    the address-ordered engine by itself; pack and unpack bit-exact vs the oracle."""
+    import torch
+    import ompi_amd
+    rng = np.random.default_rng(21)
+    n = 2 << 20
+    disps = rng.permutation(4 * n)[:n].astype(np.int64)
+    b = R.Built(("indexed_block", 1, disps.tolist(), ("basic", 15)))
+    info = b.o.info()
+    size = info["size"]
+    span, origin = R.layout(info, 1)
+    host = R.fill(span, 8)
+    user = _dev(host, device)
+    ref = np.frombuffer(b.o.pack(1, host, origin, 0, size, element_granular=False), dtype=np.uint8)
+    packed = torch.zeros(size, dtype=torch.uint8, device=device)
+    assert ompi_amd.pack(user.data_ptr() + origin, 1, b.engine(), packed, size, 0) == size
+    np.testing.assert_array_equal(_host(packed), ref)
+    assert b.engine().engine_info()["sorted"] == 1
+    out = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
+    ompi_amd.unpack(packed, size, 0, out.data_ptr() + origin, 1, b.engine())
+    exp = np.full(span, 0xA5, dtype=np.uint8)
+    b.o.unpack(1, exp, origin, 0, ref.tobytes())
+    np.testing.assert_array_equal(_host(out), exp)
