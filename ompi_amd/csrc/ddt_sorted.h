@@ -18,8 +18,8 @@ struct SortedList {
     uint64_t dev_bytes = 0;  // device bytes held (tables + U)
     uint32_t *A = nullptr;       // [n] element offset (units of esz) of the j-th block in address order
     uint16_t *SL = nullptr;      // [n] LDS slot of the j-th block inside its chunk
-    uint16_t *cnt16 = nullptr;   // [nc][nb] blocks of chunk c whose packed position is in bucket k
-    uint16_t *off16 = nullptr;   // [nc][nb] exclusive prefix of cnt16 over k
+    uint16_t *off16 = nullptr;   // [nc][nb] LDS offset of run (c, k): exclusive prefix over k of
+                                 // the blocks of chunk c whose packed position is in bucket k
     uint32_t *ub = nullptr;      // [nc][nb] first U slot of run (c, k); U is bucket-major
     uint32_t *bstart = nullptr;  // [nb + 1] first U slot of bucket k
     uint16_t *upos = nullptr;    // [slots] position inside its bucket, 0xFFFF = padding

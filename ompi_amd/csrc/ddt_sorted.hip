@@ -102,8 +102,8 @@ __global__ __launch_bounds__(BT) void k_rank(const int32_t *__restrict__ disp, u
 // per chunk: off(c,k) = exclusive prefix over k of cnt(c,k); padded counts transposed to
 // bucket-major for the U layout scan
 __global__ __launch_bounds__(BT) void k_chunk_tables(const uint32_t *__restrict__ cnt, uint32_t nc, uint32_t nb,
-                                                     uint32_t seg, uint16_t *__restrict__ cnt16,
-                                                     uint16_t *__restrict__ off16, uint32_t *__restrict__ padT)
+                                                     uint32_t seg, uint16_t *__restrict__ off16,
+                                                     uint32_t *__restrict__ padT)
 {
     __shared__ uint32_t part[BT];
     const uint32_t c = blockIdx.x;
@@ -126,7 +126,6 @@ __global__ __launch_bounds__(BT) void k_chunk_tables(const uint32_t *__restrict_
     uint32_t o = part[threadIdx.x];
     for (uint32_t k = k0; k < k1; ++k) {
         const uint32_t v = cnt[size_t(c) * nb + k];
-        cnt16[size_t(c) * nb + k] = uint16_t(v);
         off16[size_t(c) * nb + k] = uint16_t(o);
         padT[size_t(k) * nc + c] = (v + seg - 1) / seg * seg;
         o += v;
@@ -166,18 +165,39 @@ __global__ __launch_bounds__(BT) void k_assign(const int32_t *__restrict__ disp,
 }
 
 // ------------------------------------------------------------------ pass kernels
+// The (chunk, bucket) run tables of a chunk are staged in LDS first (coalesced; off has a
+// sentinel = the chunk's element count, so cnt(k) = off(k+1) - off(k)): the run loops then
+// wait on no global load for their addresses.  MAXNB = 2*CH/SEG = 4096 for every element
+// size (the sorted_plan size rule), so chunk image + tables = 155 KiB of the 160.
+constexpr uint32_t MAXNB = 4096;
+
+template <int E>
+__device__ __forceinline__ void stage_tables(const uint16_t *__restrict__ off16, const uint32_t *__restrict__ ub,
+                                             uint32_t c, uint32_t nb, uint32_t m, uint16_t *toff, uint32_t *tub)
+{
+    for (uint32_t k = threadIdx.x; k < nb; k += PT) {
+        toff[k] = off16[size_t(c) * nb + k];
+        tub[k] = ub[size_t(c) * nb + k];
+    }
+    if (threadIdx.x == 0)
+        toff[nb] = uint16_t(m);   // m <= CH <= 32 Ki
+}
+
 // pack pass 1: gather the chunk in address order into LDS, emit its runs bucket by bucket
 template <int E>
 __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, const uint32_t *__restrict__ A,
-                                              const uint16_t *__restrict__ SL, const uint16_t *__restrict__ cnt16,
-                                              const uint16_t *__restrict__ off16, const uint32_t *__restrict__ ub,
-                                              uint8_t *__restrict__ U, uint32_t n, uint32_t nb)
+                                              const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
+                                              const uint32_t *__restrict__ ub, uint8_t *__restrict__ U, uint32_t n,
+                                              uint32_t nb)
 {
     using T = typename Elem<E>::T;
     constexpr uint32_t CH = LDS_BYTES / E, SEG = 64 / E;
     __shared__ T lds[CH + SEG];
+    __shared__ uint16_t toff[MAXNB + 1];
+    __shared__ uint32_t tub[MAXNB];
     const uint32_t c = blockIdx.x, j0 = c * CH;
     const uint32_t m = min(CH, n - j0);
+    stage_tables<E>(off16, ub, c, nb, m, toff, tub);
     const T *src = reinterpret_cast<const T *>(user);
     constexpr int K = 4;
     for (uint32_t t0 = threadIdx.x; t0 < m; t0 += PT * K) {
@@ -200,11 +220,8 @@ __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, 
     T *dst = reinterpret_cast<T *>(U);
     const uint32_t sub = threadIdx.x / SEG, lane = threadIdx.x % SEG;
     for (uint32_t k = sub; k < nb; k += PT / SEG) {
-        const size_t ck = size_t(c) * nb + k;
-        const uint32_t cn = cnt16[ck];
-        if (cn == 0)
-            continue;
-        const uint32_t o = off16[ck], b = ub[ck], pn = (cn + SEG - 1) / SEG * SEG;
+        const uint32_t o = toff[k], cn = toff[k + 1] - o;
+        const uint32_t b = tub[k], pn = (cn + SEG - 1) / SEG * SEG;
         for (uint32_t q = lane; q < pn; q += SEG)
             dst[b + q] = lds[o + q];   // padding slots carry a neighbour's bytes: whole segments
     }
@@ -259,42 +276,82 @@ __global__ __launch_bounds__(PT) void k_unpack2(const uint8_t *__restrict__ pack
     const uint32_t k = blockIdx.x;
     const uint32_t m = min(RG, n - k * RG);
     const T *src = reinterpret_cast<const T *>(packed) + size_t(k) * RG;
-    for (uint32_t t = threadIdx.x; t < m; t += PT)
-        lds[t] = src[t];
+    constexpr int K = 4;
+    for (uint32_t t0 = threadIdx.x; t0 < m; t0 += PT * K) {
+        T v[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            if (t0 + q * PT < m)
+                v[q] = src[t0 + q * PT];
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            if (t0 + q * PT < m)
+                lds[t0 + q * PT] = v[q];
+    }
     __syncthreads();
     const uint32_t s0 = bstart[k], s1 = bstart[k + 1];
     T *dst = reinterpret_cast<T *>(U);
-    for (uint32_t x = s0 + threadIdx.x; x < s1; x += PT) {
-        const uint32_t p = upos[x];
-        T v{};
-        if (p != PAD)
-            v = lds[p];
-        dst[x] = v;   // padding slots written too: whole segments
+    for (uint32_t x0 = s0 + threadIdx.x; x0 < s1; x0 += PT * K) {
+        uint32_t p[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            p[q] = x0 + q * PT < s1 ? uint32_t(upos[x0 + q * PT]) : uint32_t(PAD);
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            if (x0 + q * PT < s1) {
+                T v{};
+                if (p[q] != PAD)
+                    v = lds[p[q]];
+                dst[x0 + q * PT] = v;   // padding slots written too: whole segments
+            }
+        }
     }
 }
 
 // unpack pass 1': the chunk's runs into LDS, then scattered to the user side in address order
 template <int E>
 __global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, const uint32_t *__restrict__ A,
-                                                const uint16_t *__restrict__ SL, const uint16_t *__restrict__ cnt16,
-                                                const uint16_t *__restrict__ off16, const uint32_t *__restrict__ ub,
-                                                const uint8_t *__restrict__ U, uint32_t n, uint32_t nb)
+                                                const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
+                                                const uint32_t *__restrict__ ub, const uint8_t *__restrict__ U,
+                                                uint32_t n, uint32_t nb)
 {
     using T = typename Elem<E>::T;
-    constexpr uint32_t CH = LDS_BYTES / E, SEG = 64 / E;
+    constexpr uint32_t CH = LDS_BYTES / E, SEG = 64 / E, NSUB = PT / SEG;
     __shared__ T lds[CH];
+    __shared__ uint16_t toff[MAXNB + 1];
+    __shared__ uint32_t tub[MAXNB];
     const uint32_t c = blockIdx.x, j0 = c * CH;
     const uint32_t m = min(CH, n - j0);
+    stage_tables<E>(off16, ub, c, nb, m, toff, tub);
+    __syncthreads();
     const T *src = reinterpret_cast<const T *>(U);
     const uint32_t sub = threadIdx.x / SEG, lane = threadIdx.x % SEG;
-    for (uint32_t k = sub; k < nb; k += PT / SEG) {
-        const size_t ck = size_t(c) * nb + k;
-        const uint32_t cn = cnt16[ck];
-        if (cn == 0)
-            continue;
-        const uint32_t o = off16[ck], b = ub[ck];
-        for (uint32_t q = lane; q < cn; q += SEG)
-            lds[o + q] = src[b + q];
+    // B runs per round: their first segments are loaded before any is stored (ILP); the
+    // rarer second and later segments follow
+    constexpr int B = 8;
+    for (uint32_t kb = sub; kb < nb; kb += NSUB * B) {
+        T v[B];
+        uint32_t o[B], cn[B], bb[B];
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+            const uint32_t k = kb + uint32_t(i) * NSUB;
+            cn[i] = 0;
+            if (k < nb) {
+                o[i] = toff[k];
+                cn[i] = toff[k + 1] - o[i];
+                bb[i] = tub[k];
+                if (lane < cn[i])
+                    v[i] = src[bb[i] + lane];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < B; ++i)
+            if (lane < cn[i])
+                lds[o[i] + lane] = v[i];
+#pragma unroll
+        for (int i = 0; i < B; ++i)
+            for (uint32_t q = lane + SEG; q < cn[i]; q += SEG)
+                lds[o[i] + q] = src[bb[i] + q];
     }
     __syncthreads();
     T *dst = reinterpret_cast<T *>(user);
@@ -338,7 +395,7 @@ SortedList::~SortedList()
 {
     if (done)
         (void) hipEventSynchronize(done);
-    for (void *p : {(void *) A, (void *) SL, (void *) cnt16, (void *) off16, (void *) ub, (void *) bstart,
+    for (void *p : {(void *) A, (void *) SL, (void *) off16, (void *) ub, (void *) bstart,
                     (void *) upos, U})
         if (p)
             (void) hipFree(p);
@@ -395,14 +452,13 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
         uint64_t bytes = 0;
         A = dalloc<uint32_t>(n, bytes);
         SL = dalloc<uint16_t>(n, bytes);
-        cnt16 = dalloc<uint16_t>(runs, bytes);
         off16 = dalloc<uint16_t>(runs, bytes);
         ub = dalloc<uint32_t>(runs, bytes);
         bstart = dalloc<uint32_t>(nb + 1, bytes);
         hipLaunchKernelGGL(k_rank, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, bm, wpre, ch, nb, A,
                            cnt, rr);
         HK(hipMemsetAsync(padT + runs, 0, 4, stream));
-        hipLaunchKernelGGL(k_chunk_tables, dim3(nc), dim3(BT), 0, stream, cnt, nc, nb, seg, cnt16, off16, padT);
+        hipLaunchKernelGGL(k_chunk_tables, dim3(nc), dim3(BT), 0, stream, cnt, nc, nb, seg, off16, padT);
         HK(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb2, padT, ubT, int(runs + 1), stream));
         uint32_t total = 0;
         HK(hipMemcpyAsync(&total, ubT + runs, 4, hipMemcpyDeviceToHost, stream));
@@ -441,11 +497,11 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, hipStream_t 
     uint8_t *u8 = static_cast<uint8_t *>(U);
 #define DDT_SORTED_LAUNCH(E)                                                                              \
     if (dir == 0) {                                                                                       \
-        hipLaunchKernelGGL((k_pack1<E>), gc, blk, 0, stream, user, A, SL, cnt16, off16, ub, u8, n, nb);   \
+        hipLaunchKernelGGL((k_pack1<E>), gc, blk, 0, stream, user, A, SL, off16, ub, u8, n, nb);   \
         hipLaunchKernelGGL((k_pack2<E>), gb, blk, 0, stream, u8, upos, bstart, packed, n);                \
     } else {                                                                                              \
         hipLaunchKernelGGL((k_unpack2<E>), gb, blk, 0, stream, packed, upos, bstart, u8, n);              \
-        hipLaunchKernelGGL((k_unpack1<E>), gc, blk, 0, stream, user, A, SL, cnt16, off16, ub, u8, n, nb); \
+        hipLaunchKernelGGL((k_unpack1<E>), gc, blk, 0, stream, user, A, SL, off16, ub, u8, n, nb); \
     }
     if (esz == 4) {
         DDT_SORTED_LAUNCH(4)
