@@ -354,6 +354,19 @@ def main():
         if os.path.exists(tfile):
             with open(tfile) as f:
                 result["roofline"]["traffic"] = json.load(f).get("bytes_per_step")
+        # Memory-side request roofline: the sparse faces are bound by requests,
+        # not bytes.  Request counts per step come from the committed rocprofv3 PMC pass
+        # (scripts/requests.py); the rate uses this run's own kernel time.
+        rfile = os.path.join(ROOT, "profiles", f"requests_{args.config}.json")
+        if os.path.exists(rfile):
+            with open(rfile) as f:
+                rq = json.load(f)
+            ops = rq["ops_per_step"]
+            result["request_roofline"] = {
+                "ops_per_step": round(ops), "achieved_G_per_s": round(ops / (tp + tu) / 1e9, 2),
+                "peak_G_per_s": rq["ceiling_requests_per_s"] / 1e9,
+                "frac": round(ops / (tp + tu) / rq["ceiling_requests_per_s"], 4),
+                "source": f"profiles/requests_{args.config}.json"}
 
     if rank == 0 and args.config == "cfg2":
         result["single_face_latency_us"] = single_face_latency(dev, stream, user, origin)

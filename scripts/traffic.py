@@ -20,13 +20,25 @@ import sys
 
 
 def per_kernel(path, counter):
+    """Per direction: the sum over its kernels of each kernel's mean per dispatch (the
+    address-ordered list engine runs two kernels per pack and per unpack)."""
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter or "ddt_move" not in r["Kernel_Name"]:
+        k = r["Kernel_Name"]
+        if r["Counter_Name"] != counter:
             continue
-        direction = "pack" if "<0," in r["Kernel_Name"] else "unpack"
-        acc[direction].append(float(r["Counter_Value"]) * 1024.0)
-    return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
+        if "ddt_move" in k:
+            direction = "pack" if "<0," in k else "unpack"
+        elif "k_pack" in k or "k_unpack" in k:
+            direction = "pack" if "k_pack" in k else "unpack"
+        else:
+            continue
+        acc[(direction, k)].append(float(r["Counter_Value"]) * 1024.0)
+    out, n = collections.defaultdict(float), collections.defaultdict(int)
+    for (d, _), v in acc.items():
+        out[d] += sum(v) / len(v)
+        n[d] += len(v)
+    return dict(out), dict(n)
 
 
 def main():
