@@ -610,3 +610,47 @@ def test_sorted_list_engine_auto(device):
     exp = np.full(span, 0xA5, dtype=np.uint8)
     b.o.unpack(1, exp, origin, 0, ref.tobytes())
     np.testing.assert_array_equal(_host(out), exp)
+
+
+# ---------------------------------------------------------------- edge sizes
+def test_empty_messages(device):
+    """count = 0 and zero-size types: nothing moves, position unchanged, convertors complete
+    at once (opal_convertor_prepare_for_send with local_size 0; opal_convertor.c:258-261)."""
+    import torch
+    import ompi_amd
+    from ompi_amd import datatype as D
+    user = torch.full((64,), 7, dtype=torch.uint8, device=device)
+    packed = torch.full((64,), 9, dtype=torch.uint8, device=device)
+    v = D.create_vector(4, 1, 2, D.MPI.MPI_INT).commit()
+    z = D.create_contiguous(0, D.MPI.MPI_INT).commit()
+    assert ompi_amd.pack(user, 0, v, packed, 64, 5) == 5
+    assert ompi_amd.pack(user, 3, z, packed, 64, 0) == 0
+    assert ompi_amd.unpack(packed, 64, 0, user, 0, v) == 0
+    for t, cnt in ((v, 0), (z, 5)):
+        c = ompi_amd.Convertor().prepare_for_send(t, cnt, user.data_ptr())
+        rc, lens, md = c.pack([(packed, 64)])
+        assert rc == 1 and md == 0 and c.completed
+    assert bool((user == 7).all()) and bool((packed == 9).all())
+
+
+def test_beyond_4g_units(device):
+    """A leaf of more than 2^32 units (the 64-bit index path): hvector(2^31 + 3, 3 B, 4 B) of
+    MPI_BYTE packs 6 GiB.  Checked against torch's own strided view, both directions."""
+    import torch
+    import ompi_amd
+    from ompi_amd import datatype as D
+    n = (1 << 31) + 3
+    t = D.create_hvector(n, 3, 4, D.MPI.MPI_BYTE).commit()
+    assert t.size == 3 * n
+    user = torch.randint(1, 255, (4 * n,), dtype=torch.uint8, device=device)
+    packed = torch.empty(3 * n, dtype=torch.uint8, device=device)
+    assert ompi_amd.pack(user, 1, t, packed, 3 * n, 0) == 3 * n
+    torch.cuda.synchronize()
+    assert torch.equal(packed.view(n, 3), user.view(n, 4)[:, :3])
+    del user
+    out = torch.full((4 * n,), 0xA5, dtype=torch.uint8, device=device)
+    assert ompi_amd.unpack(packed, 3 * n, 0, out, 1, t) == 3 * n
+    torch.cuda.synchronize()
+    o = out.view(n, 4)
+    assert torch.equal(o[:, :3], packed.view(n, 3))
+    assert bool((o[:, 3] == 0xA5).all())
