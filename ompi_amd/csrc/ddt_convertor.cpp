@@ -171,10 +171,12 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     }
     if (S->items.empty())
         return DDT_SUCCESS;
-    if (S->inline_ok)
-        HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, stream));
-    else
-        HIPCHK(launch_move(S->d_items, uint32_t(S->items.size()), S->ntasks, dir, S->has_lists, stream));
+    const uint32_t rev = (tuning().rev == 2 || (tuning().rev == 1 && dir == 1)) ? 1u : 0u;
+    if (S->inline_ok) {
+        HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, rev, stream));
+    } else {
+        HIPCHK(launch_move(S->d_items, uint32_t(S->items.size()), S->ntasks, dir, S->has_lists, rev, stream));
+    }
     return DDT_SUCCESS;
 }
 
@@ -990,6 +992,8 @@ int ddt_tune(const char *key, long value)
         tuning().interleave = value;
     else if (k == "policy")
         tuning().policy = int(value);
+    else if (k == "rev")
+        tuning().rev = int(value);
     else if (k == "sorted")
         tuning().sorted = value;
     else if (k == "wt")

@@ -175,3 +175,19 @@ def test_interleaved_task_order_matches_oracle(chunk):
     finally:
         L.ddt_tune(b"interleave", 0)
         L.ddt_tune(b"task_kb", 0)
+
+
+def test_reference_resized_extent_bounds():
+    """resized_extent.c:148-163 known answers, engine and oracle: resized(int, 0, 6) has
+    lb 0 / extent 6 / true_lb 0 / true_extent 4; contiguous(3, it) keeps extent 18 (not the
+    alignment-rounded 20) with true_extent 16; its packed stream picks the ints at 0, 6, 12."""
+    for rec, want in ((("resized", ("basic", 6), 0, 6), (0, 6, 0, 4)),
+                      (("contig", 3, ("resized", ("basic", 6), 0, 6)), (0, 18, 0, 16))):
+        b = R.Built(rec)
+        for i in (b.o.info(), b.engine().info()):
+            assert (i["lb"], i["ub"] - i["lb"], i["true_lb"], i["true_ub"] - i["true_lb"]) == want
+    b = R.Built(("contig", 3, ("resized", ("basic", 6), 0, 6)))
+    user = np.arange(48, dtype=np.uint8)
+    got = np.frombuffer(b.o.pack(2, user, 0, 0, 24, element_granular=True), dtype=np.uint8)
+    want = np.concatenate([user[p:p + 4] for p in range(0, 36, 6)])
+    np.testing.assert_array_equal(got, want)

@@ -154,3 +154,26 @@ def test_raw_reference_ddt_raw2_description():
     _walk_desc(rows, 0, used, BASE, pieces)
     assert stitched([pieces]) == lists[300]
     assert sum(n for _, n in pieces) == bd["size"]
+
+
+def test_reference_large_data_c():
+    """large_data.c: raw export of multi-GiB types, 10 iovecs per call, never dereferenced.
+    The bytes described must add up to the type size: indexed({192,192}, {576,0}) and
+    indexed({192,192}, {192,384}) of contiguous(20 M, float) (30.72 GB each),
+    vector(INT_MAX/2, 4, 4, float) and contiguous(INT_MAX/2, contiguous(4, float))
+    (16 GiB each; large_data.c:96-172)."""
+    f = D.MPI.MPI_FLOAT
+    ddt = D.create_contiguous(20_000_000, f)
+    big = 2 ** 31 - 1
+    types = [D.create_indexed([192, 192], [3 * 192, 0], ddt),
+             D.create_indexed([192, 192], [192, 2 * 192], ddt),
+             D.create_vector(big // 2, 4, 4, f),
+             D.create_contiguous(big // 2, D.create_contiguous(4, f))]
+    for t in types:
+        t.commit()
+        chunks, total = engine_raw_all(t, 1, BASE, 10)
+        assert total == t.size == sum(n for ch in chunks for _, n in ch)
+    # the sparse index type is its two 15.36 GB blocks; the others one contiguous region
+    assert stitched(engine_raw_all(types[0], 1, BASE, 10)[0]) == [
+        (BASE + 3 * 192 * 80_000_000, 192 * 80_000_000), (BASE, 192 * 80_000_000)]
+    assert stitched(engine_raw_all(types[2], 1, BASE, 10)[0]) == [(BASE, (big // 2) * 16)]

@@ -654,3 +654,86 @@ def test_beyond_4g_units(device):
     o = out.view(n, 4)
     assert torch.equal(o[:, :3], packed.view(n, 3))
     assert bool((o[:, 3] == 0xA5).all())
+
+
+def test_reference_resized_extent_c(device):
+    """resized_extent.c: contiguous(3, resized(int, 0, 6)), count 2.  Bounds lb 0 / extent 18
+    / true_lb 0 / true_extent 16 (not rounded up to 20), the six ints at byte offsets
+    0, 6, ..., 30 pack to 24 bytes in order and unpack back (resized_extent.c:36-138)."""
+    import torch
+    import ompi_amd
+    from ompi_amd import datatype as D
+    r6 = D.create_resized(D.MPI.MPI_INT, 0, 6).commit()
+    c3 = D.create_contiguous(3, r6).commit()
+    i = c3.info()
+    assert (i["lb"], i["ub"] - i["lb"], i["true_lb"], i["true_ub"] - i["true_lb"]) == (0, 18, 0, 16)
+    src = np.full(64, 0xAA, dtype=np.uint8)
+    vals = np.arange(100, 106, dtype=np.int32)
+    for k, p in enumerate(range(0, 36, 6)):
+        src[p:p + 4] = vals[k:k + 1].view(np.uint8)
+    dsrc = _dev(src, device)
+    packed = torch.zeros(64, dtype=torch.uint8, device=device)
+    conv = ompi_amd.Convertor().prepare_for_send(c3, 2, dsrc)
+    rc, lens, md = conv.pack([(packed, 64)])
+    assert rc == 1 and md == 24
+    np.testing.assert_array_equal(_host(packed)[:24].view(np.int32), vals)
+    dst = torch.zeros(64, dtype=torch.uint8, device=device)
+    conv = ompi_amd.Convertor().prepare_for_recv(c3, 2, dst)
+    rc, lens, md = conv.unpack([(packed, 24)])
+    assert rc == 1 and md == 24
+    got = _host(dst)
+    for k, p in enumerate(range(0, 36, 6)):
+        assert got[p:p + 4].view(np.int32)[0] == vals[k]
+    assert not got[36:].any() and not got[4:6].any()
+
+
+def _local_copy_with_convertor(b: R.Built, count: int, chunk: int, device):
+    """ddt_test.c:270-340 local_copy_with_convertor on device buffers: pack at most `chunk`
+    bytes (never splitting an element), unpack exactly what was packed, until both
+    convertors complete; the receive buffer then equals the oracle's unpack of the stream."""
+    import torch
+    import ompi_amd
+    info = b.o.info()
+    size = info["size"] * count
+    span, origin = R.layout(info, count)
+    host = R.fill(span, 77)
+    src = _dev(host, device)
+    dst = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
+    tmp = torch.empty(chunk, dtype=torch.uint8, device=device)
+    e = b.engine()
+    cs = ompi_amd.Convertor().prepare_for_send(e, count, src.data_ptr() + origin)
+    cr = ompi_amd.Convertor().prepare_for_recv(e, count, dst.data_ptr() + origin)
+    done1 = done2 = 0
+    length = 0
+    while not (done1 and done2):
+        md = 0
+        if not done1:
+            done1, _, md = cs.pack([(tmp, chunk)])
+            if md == 0 and not done1:   # an element larger than the chunk
+                raise AssertionError("no progress")
+        if not done2:
+            done2, _, got = cr.unpack([(tmp, md)])
+            assert got == md
+        length += md
+    assert length == size
+    exp = np.full(span, 0xA5, dtype=np.uint8)
+    b.o.unpack(count, exp, origin, 0, b.o.pack(count, host, origin, 0, size, element_granular=False))
+    np.testing.assert_array_equal(_host(dst), exp)
+
+
+@pytest.mark.parametrize("name,recipe,count,chunks", [
+    ("inversed_vector", ("vector", 10, 1, 2, ("basic", 6)), 100, [956]),
+    ("upper_matrix", ("indexed", [100 - i for i in range(100)], [i * 101 for i in range(100)],
+                      ("basic", 16)), 1, [48, 808]),
+    ("contig_4500", ("contig", 4500, ("basic", 16)), 1, [12]),
+    ("contig_450x10", ("contig", 450, ("basic", 16)), 10, [12]),
+    ("contig_45x100", ("contig", 45, ("basic", 16)), 100, [12]),
+    ("contig_10x450", ("contig", 10, ("basic", 16)), 450, [12]),
+    ("vector_450_10_11", ("vector", 450, 10, 11, ("basic", 16)), 1, [12, 82, 6000, 36000]),
+    ("struct_char_double", ("struct", [1, 1], [0, 8], [("basic", 4), ("basic", 16)]), 4500, [12]),
+])
+def test_reference_ddt_test_c(device, name, recipe, count, chunks):
+    """The type x count x chunk matrix of ddt_test.c:370-560 (types of ddt_lib.c:63-470)."""
+    b = R.Built(recipe)
+    for ch in chunks:
+        _local_copy_with_convertor(b, count, ch, device)
