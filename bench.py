@@ -11,6 +11,9 @@ message, device iovec) + one unpack of the same message.
 
   value      = whole-job 2*S*N_gpus / (t_pack + t_unpack)        [GiB/s]
   roofline   = algorithmic bytes (read S + write S per op) / kernel time vs 8 TB/s
+  request_roofline = memory-side requests per step (committed PMC pass, profiles/
+               requests_<config>.json) / this run's kernel time vs the highest request
+               rate measured for any access pattern
   cpu_baseline = the CPU oracle (oracle/ddt_oracle.c, a restatement of the reference
                convertor) on the host cores of the same box, bounded sample.
 

@@ -138,15 +138,9 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                 S->blk.items[i] = S->items[i];
         } else if (!S->items.empty()) {
             size_t bytes = S->items.size() * sizeof(Item);
-            Item *h = nullptr;
-            HIPCHK(hipHostMalloc((void **) &h, bytes, hipHostMallocDefault));
-            std::memcpy(h, S->items.data(), bytes);
             hipError_t e = hipMalloc((void **) &S->d_items, bytes);
             if (e == hipSuccess)
-                e = hipMemcpyAsync(S->d_items, h, bytes, hipMemcpyHostToDevice, stream);
-            if (e == hipSuccess)
-                e = hipStreamSynchronize(stream);   // h is released right after
-            (void) hipHostFree(h);
+                e = upload(S->d_items, S->items.data(), bytes);
             if (e != hipSuccess)
                 return fail(DDT_ERR_HIP, std::string("item upload: ") + hipGetErrorString(e));
         }

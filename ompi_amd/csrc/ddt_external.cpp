@@ -218,8 +218,8 @@ int ext_upload(ExtPlan &X)
     ConvSeg *ds = nullptr;
     ConvRun *dr = nullptr;
     if (hipMalloc((void **) &ds, sb) != hipSuccess || hipMalloc((void **) &dr, rb) != hipSuccess
-        || hipMemcpy(ds, X.segs.data(), sb, hipMemcpyHostToDevice) != hipSuccess
-        || hipMemcpy(dr, X.runs.data(), rb, hipMemcpyHostToDevice) != hipSuccess) {
+        || upload(ds, X.segs.data(), sb) != hipSuccess
+        || upload(dr, X.runs.data(), rb) != hipSuccess) {
         if (ds) (void) hipFree(ds);
         if (dr) (void) hipFree(dr);
         return DDT_ERR_HIP;

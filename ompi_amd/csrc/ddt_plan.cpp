@@ -35,6 +35,34 @@ Tuning &tuning()
     return t;
 }
 
+// Host -> device uploads of plan metadata run on a library-private non-blocking stream,
+// one per device: they never synchronise with (or invalidate a capture on) the caller's
+// stream, so a plan's first use may sit inside a HIP-graph capture.
+hipError_t upload(void *dst, const void *src, size_t n)
+{
+    static std::mutex mu;
+    static std::map<int, hipStream_t> streams;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess)
+        return e;
+    hipStream_t s = nullptr;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = streams.find(dev);
+        if (it == streams.end()) {
+            if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess)
+                return e;
+            streams[dev] = s;
+        } else {
+            s = it->second;
+        }
+    }
+    if ((e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return e;
+    return hipStreamSynchronize(s);
+}
+
 Plan::~Plan()
 {
     // launches that read these descriptors or lists may still be in flight
@@ -191,13 +219,13 @@ void ensure_device_lists(Plan &P)
                 tmp[k] = int32_t(X.disp[k] - D.disp_base);
             if (hipMalloc(&D.disp, n * 4) != hipSuccess)
                 throw std::runtime_error("hipMalloc(list disp)");
-            if (hipMemcpy(D.disp, tmp.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess)
+            if (upload(D.disp, tmp.data(), n * 4) != hipSuccess)
                 throw std::runtime_error("hipMemcpy(list disp)");
             P.dev_bytes += n * 4;
         } else {
             if (hipMalloc(&D.disp, n * 8) != hipSuccess)
                 throw std::runtime_error("hipMalloc(list disp)");
-            if (hipMemcpy(D.disp, X.disp.data(), n * 8, hipMemcpyHostToDevice) != hipSuccess)
+            if (upload(D.disp, X.disp.data(), n * 8) != hipSuccess)
                 throw std::runtime_error("hipMemcpy(list disp)");
             P.dev_bytes += n * 8;
         }
@@ -215,8 +243,8 @@ void ensure_device_lists(Plan &P)
             if (hipMalloc((void **) &D.len, n * 4) != hipSuccess
                 || hipMalloc((void **) &D.goff, ng * 8) != hipSuccess)
                 throw std::runtime_error("hipMalloc(list len)");
-            if (hipMemcpy(D.len, len.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess
-                || hipMemcpy(D.goff, goff.data(), ng * 8, hipMemcpyHostToDevice) != hipSuccess)
+            if (upload(D.len, len.data(), n * 4) != hipSuccess
+                || upload(D.goff, goff.data(), ng * 8) != hipSuccess)
                 throw std::runtime_error("hipMemcpy(list len)");
             P.dev_bytes += n * 4 + ng * 8;
         }
@@ -268,6 +296,11 @@ SortedList *sorted_plan(const ddt_datatype *t, Plan &P, uint64_t user, hipStream
         return nullptr;   // this buffer only: the typed element loads need alignment
     std::lock_guard<std::mutex> g_(P.mu);
     if (P.sorted_state == 0) {
+        // the build allocates and synchronises: never inside a stream capture (a graph
+        // captured before the first eager use keeps the per-block kernel)
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+            return nullptr;
         // element displacements (bytes, relative to the list minimum): the device list
         // itself when every block is one element, else expanded here
         const int32_t *ed = static_cast<const int32_t *>(D.disp);
@@ -282,7 +315,7 @@ SortedList *sorted_plan(const ddt_datatype *t, Plan &P, uint64_t user, hipStream
                     h[e++] = int32_t(b + int64_t(q));
             }
             if (hipMalloc(&tmp, ne * 4 + 16) != hipSuccess
-                || hipMemcpy(tmp, h.data(), ne * 4, hipMemcpyHostToDevice) != hipSuccess) {
+                || upload(tmp, h.data(), ne * 4) != hipSuccess) {
                 if (tmp) (void) hipFree(tmp);
                 throw std::runtime_error("sorted list: element displacement upload");
             }

@@ -23,6 +23,8 @@ struct Tuning {
     int rev = 0;          // reverse task order: 0 off, 1 unpack launches, 2 every launch
 };
 Tuning &tuning();
+// Synchronous host -> device copy on a library-private stream (capture-safe).
+hipError_t upload(void *dst, const void *src, size_t n);
 
 void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t user, uint64_t pk,
                  uint64_t W0, uint64_t W1, bool same_layout, std::vector<Item> &items);

@@ -3,6 +3,7 @@
 #pragma once
 
 #include <cstdint>
+#include <mutex>
 
 #include <hip/hip_runtime.h>
 
@@ -27,6 +28,7 @@ struct SortedList {
     hipEvent_t done = nullptr;   // recorded after every run (U reuse across streams)
     hipStream_t last_stream = nullptr;
     bool used = false;
+    std::mutex mu;               // run() from several host threads: one launch sequence at a time
     ~SortedList();
     bool build(const int32_t *disp, uint32_t n, uint32_t esz, uint64_t span_elems, hipStream_t stream);
     hipError_t run(uint8_t *user, uint8_t *packed, int dir, hipStream_t stream);

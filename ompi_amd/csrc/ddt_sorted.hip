@@ -488,6 +488,7 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
 hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, hipStream_t stream)
 {
     // U is one scratch per plan: a launch on another stream waits for the last one
+    std::lock_guard<std::mutex> g(mu);
     if (used && last_stream != stream) {
         hipError_t e = hipStreamWaitEvent(stream, done, 0);
         if (e != hipSuccess)

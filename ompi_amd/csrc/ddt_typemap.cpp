@@ -1052,9 +1052,62 @@ struct RawEntry {
     int64_t e;    // DATA: disp; END_LOOP: first_elem_disp
 };
 
+// Runs of at least kFoldMin consecutive DATA entries of one basic type, each of at most
+// kFoldCount blocks, are imported as ONE index list instead of one node per entry: the
+// optimizer leaves an indexed type as one- or two-block DATA entries (the 64 Mi blocks of
+// BASELINE config 4 are 32 M entries, opal_datatype_optimize.c:1179-1185), which would
+// otherwise become 32 M plan leaves.  Type-map order and bytes are unchanged.
+constexpr size_t kFoldMin = 64;
+constexpr uint32_t kFoldCount = 16;
+
+struct RawData {
+    uint16_t type;
+    uint32_t count;
+    uint64_t blen;   // bytes
+    int64_t extent, disp;
+};
+
+void flush_data(std::vector<RawData> &run, std::vector<Node> &out)
+{
+    if (run.size() >= kFoldMin) {
+        auto L = std::make_shared<IndexList>();
+        L->esize = kSize[run[0].type];
+        size_t nb = 0;
+        for (const RawData &r : run)
+            nb += r.count;
+        L->disp.reserve(nb);
+        L->len.reserve(nb);
+        for (const RawData &r : run)
+            for (uint32_t k = 0; k < r.count; ++k) {
+                L->disp.push_back(r.disp + int64_t(k) * r.extent);
+                L->len.push_back(r.blen);
+            }
+        Node n;
+        n.kind = Node::LIST;
+        n.esize = L->esize;
+        n.tid = run[0].type;
+        n.list = finish_list(L);
+        out.push_back(std::move(n));
+    } else {
+        for (const RawData &r : run) {
+            Node n;
+            n.kind = Node::DATA;
+            n.esize = kSize[r.type];
+            n.tid = r.type;
+            n.count = r.count;
+            n.blen = r.blen;
+            n.extent = r.extent;
+            n.disp = r.disp;
+            out.push_back(n);
+        }
+    }
+    run.clear();
+}
+
 bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<Node> &out)
 {
     size_t i = begin;
+    std::vector<RawData> run;
     while (i < end) {
         const unsigned char *p = raw + 32 * i;
         uint16_t flags, type;
@@ -1070,17 +1123,16 @@ bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<
             std::memcpy(&disp, p + 24, 8);
             if (type < 4 || type > 27)
                 return false;
-            Node n;
-            n.kind = Node::DATA;
-            n.esize = kSize[type];
-            n.tid = type;
-            n.count = count;
-            n.blen = blocklen * uint64_t(kSize[type]);
-            n.extent = extent;
-            n.disp = disp;
-            out.push_back(n);
+            const RawData d{type, count, blocklen * uint64_t(kSize[type]), extent, disp};
+            const bool foldable = count >= 1 && count <= kFoldCount && d.blen > 0;
+            if (!run.empty() && (!foldable || run[0].type != type))
+                flush_data(run, out);
+            run.push_back(d);
+            if (!foldable)
+                flush_data(run, out);
             ++i;
         } else if (type == 0) {   // LOOP
+            flush_data(run, out);
             uint32_t items, loops;
             int64_t extent;
             std::memcpy(&items, p + 4, 4);
@@ -1105,6 +1157,7 @@ bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<
             return false;   // stray END_LOOP
         }
     }
+    flush_data(run, out);   // a run that ends the description
     return true;
 }
 }  // namespace

@@ -177,3 +177,32 @@ def test_reference_large_data_c():
     assert stitched(engine_raw_all(types[0], 1, BASE, 10)[0]) == [
         (BASE + 3 * 192 * 80_000_000, 192 * 80_000_000), (BASE, 192 * 80_000_000)]
     assert stitched(engine_raw_all(types[2], 1, BASE, 10)[0]) == [(BASE, (big // 2) * 16)]
+
+
+def test_imported_indexed_description_folds_to_one_list():
+    """An indexed type imported from its committed opal description (the bridge's path,
+    INTEGRATION.md §1).  The reference's optimizer leaves an indexed type as two-block DATA
+    entries (opal_datatype_optimize.c:1179-1185: 32 M of them for BASELINE config 4); the
+    import folds a long run into ONE index list (one plan leaf, so the address-ordered
+    engine applies) with the same type map; a short run stays one DATA node per entry."""
+    import numpy as np
+    from tests import plan_emu as E
+    rng = np.random.default_rng(8)
+    for n, leaves, lists in ((4096, 1, 1), (20, 10, 0)):
+        d = rng.permutation(4 * n)[:n].astype(np.int64)
+        b = R.Built(("indexed_block", 1, d.tolist(), ("basic", 15)))
+        info = b.o.info()
+        rows = [("elem", 0x0100, 15, 2, 1, int(d[k + 1] - d[k]) * 4, int(d[k]) * 4) for k in range(0, n, 2)]
+        e = D.from_opal_desc(_opal_desc_bytes(rows), info["size"], info["lb"], info["ub"],
+                             info["true_lb"], info["true_ub"])
+        pi = e.plan_info()
+        assert (pi["leaves"], pi["list_leaves"]) == (leaves, lists), pi
+        np.testing.assert_array_equal(E.engine_blocks(e), E.oracle_blocks(b.o))
+        span, origin = R.layout(info, 1)
+        user = R.fill(span, 3)
+        UA, PA = 1 << 40, 1 << 41
+        its = E.items(e, 1, UA + origin, PA, 0, info["size"])
+        packed = np.zeros(info["size"], dtype=np.uint8)
+        E.emulate(its, user, UA, packed, PA, 0, E.list_tables(e))
+        ref = np.frombuffer(b.o.pack(1, user, origin, 0, info["size"], element_granular=False), dtype=np.uint8)
+        np.testing.assert_array_equal(packed, ref)

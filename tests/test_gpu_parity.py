@@ -737,3 +737,84 @@ def test_reference_ddt_test_c(device, name, recipe, count, chunks):
     b = R.Built(recipe)
     for ch in chunks:
         _local_copy_with_convertor(b, count, ch, device)
+
+
+def test_sorted_list_engine_in_hip_graph(device, sorted_from):
+    """A qualifying list captured into a HIP graph before its first eager use keeps the
+    per-block kernel (the engine's build cannot run inside a capture); after an eager use the
+    engine itself is captured.  Both graphs replay bit-exact."""
+    import torch
+    import ompi_amd
+    sorted_from(1)
+    rng = np.random.default_rng(5)
+    n = 70_000
+    b = R.Built(("indexed_block", 1, rng.permutation(4 * n)[:n].tolist(), ("basic", 15)))
+    info = b.o.info()
+    size = info["size"]
+    span, origin = R.layout(info, 1)
+    host = R.fill(span, 12)
+    user = _dev(host, device)
+    ref = np.frombuffer(b.o.pack(1, host, origin, 0, size, element_granular=False), dtype=np.uint8)
+    e = b.engine()
+    for expect_state in (0, 1):
+        packed = torch.zeros(size, dtype=torch.uint8, device=device)
+        s = torch.cuda.Stream(device)
+        g = torch.cuda.CUDAGraph()
+        c = ompi_amd.Convertor()
+        with torch.cuda.graph(g, stream=s, capture_error_mode="relaxed"):
+            c.set_stream(torch.cuda.current_stream(device), True)
+            c.prepare_for_send(e, 1, user.data_ptr() + origin)
+            c.pack([(packed, size)])
+        assert e.engine_info()["sorted"] == expect_state
+        g.replay()
+        np.testing.assert_array_equal(_host(packed), ref)
+        # an eager whole-message pack builds the engine for the next capture
+        assert ompi_amd.pack(user.data_ptr() + origin, 1, e, packed, size, 0) == size
+        np.testing.assert_array_equal(_host(packed), ref)
+        assert e.engine_info()["sorted"] == 1
+
+
+def test_sorted_list_engine_concurrent_streams(device, sorted_from):
+    """Two host threads on two streams pack one qualifying type at once, 20 times each: the
+    engine's single scratch buffer is handed between streams by its event; both exact."""
+    import threading
+    import torch
+    import ompi_amd
+    sorted_from(1)
+    rng = np.random.default_rng(31)
+    n = 100_000
+    b = R.Built(("indexed_block", 1, rng.permutation(4 * n)[:n].tolist(), ("basic", 15)))
+    info = b.o.info()
+    size = info["size"]
+    span, origin = R.layout(info, 1)
+    host = R.fill(span, 14)
+    user = _dev(host, device)
+    ref = np.frombuffer(b.o.pack(1, host, origin, 0, size, element_granular=False), dtype=np.uint8)
+    e = b.engine()
+    warm = torch.empty(size, dtype=torch.uint8, device=device)
+    assert ompi_amd.pack(user.data_ptr() + origin, 1, e, warm, size, 0) == size   # builds the engine
+    assert e.engine_info()["sorted"] == 1
+    outs = [torch.zeros(size, dtype=torch.uint8, device=device) for _ in range(2)]
+    errors = []
+
+    def worker(t):
+        try:
+            s = torch.cuda.Stream(device)
+            c = ompi_amd.Convertor()
+            c.set_stream(s, True)
+            for _ in range(20):
+                c.prepare_for_send(e, 1, user.data_ptr() + origin)
+                rc, _, md = c.pack([(outs[t], size)])
+                assert rc == 1 and md == size
+            s.synchronize()
+        except Exception as ex:   # surfaced below
+            errors.append(repr(ex))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors
+    for t in range(2):
+        np.testing.assert_array_equal(_host(outs[t]), ref)
