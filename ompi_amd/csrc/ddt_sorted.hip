@@ -420,10 +420,8 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
     const uint64_t words = (span_elems + 31) / 32 + 1;
     const size_t runs = size_t(nc) * nb;
     uint64_t tmp_bytes = 0;
-    uint32_t *bm = dalloc<uint32_t>(words, tmp_bytes), *wpre = dalloc<uint32_t>(words, tmp_bytes);
-    uint32_t *dup = dalloc<uint32_t>(1, tmp_bytes), *cnt = dalloc<uint32_t>(runs, tmp_bytes);
-    uint32_t *padT = dalloc<uint32_t>(runs + 1, tmp_bytes), *ubT = dalloc<uint32_t>(runs + 1, tmp_bytes);
-    uint16_t *rr = dalloc<uint16_t>(n, tmp_bytes);
+    uint32_t *bm = nullptr, *wpre = nullptr, *dup = nullptr, *cnt = nullptr, *padT = nullptr, *ubT = nullptr;
+    uint16_t *rr = nullptr;
     void *scan_tmp = nullptr;
     auto release = [&] {
         for (void *p : {(void *) bm, (void *) wpre, (void *) dup, (void *) cnt, (void *) padT, (void *) ubT,
@@ -432,6 +430,13 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
                 (void) hipFree(p);
     };
     try {
+        bm = dalloc<uint32_t>(words, tmp_bytes);
+        wpre = dalloc<uint32_t>(words, tmp_bytes);
+        dup = dalloc<uint32_t>(1, tmp_bytes);
+        cnt = dalloc<uint32_t>(runs, tmp_bytes);
+        padT = dalloc<uint32_t>(runs + 1, tmp_bytes);
+        ubT = dalloc<uint32_t>(runs + 1, tmp_bytes);
+        rr = dalloc<uint16_t>(n, tmp_bytes);
         HK(hipMemsetAsync(bm, 0, words * 4, stream));
         HK(hipMemsetAsync(dup, 0, 4, stream));
         HK(hipMemsetAsync(cnt, 0, runs * 4, stream));
