@@ -100,7 +100,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                 uint8_t *u = reinterpret_cast<uint8_t *>(user + uint64_t(L.list_shift) + uint64_t(P.dev[0].disp_base)
                                                          + i * uint64_t(t->extent()));
                 uint8_t *pk = reinterpret_cast<uint8_t *>(wins[0].ptr + i * uint64_t(t->size));
-                HIPCHK(SL->run(u, pk, dir, stream));
+                HIPCHK(SL->run(u, pk, dir, uint32_t(tuning().spol), stream));
             }
             return DDT_SUCCESS;
         }
@@ -986,6 +986,8 @@ int ddt_tune(const char *key, long value)
         tuning().interleave = value;
     else if (k == "policy")
         tuning().policy = int(value);
+    else if (k == "spol")
+        tuning().spol = value;
     else if (k == "rev")
         tuning().rev = int(value);
     else if (k == "sorted")

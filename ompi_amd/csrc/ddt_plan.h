@@ -21,6 +21,7 @@ struct Tuning {
     int wt = -1;          // write-through (sc1) stores: -1 auto, 0 off, 1 sparse user side, 2 all
     long sorted = -1;     // address-ordered list engine: -1 auto, 0 off, n > 0 from n blocks up
     int rev = 0;          // reverse task order: 0 off, 1 unpack launches, 2 every launch
+    long spol = 0;        // address-ordered engine access policy bits (ddt_sorted.hip POL_*)
 };
 Tuning &tuning();
 // Synchronous host -> device copy on a library-private stream (capture-safe).

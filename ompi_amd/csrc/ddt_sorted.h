@@ -31,7 +31,8 @@ struct SortedList {
     std::mutex mu;               // run() from several host threads: one launch sequence at a time
     ~SortedList();
     bool build(const int32_t *disp, uint32_t n, uint32_t esz, uint64_t span_elems, hipStream_t stream);
-    hipError_t run(uint8_t *user, uint8_t *packed, int dir, hipStream_t stream);
+    // pol: access policy bits (POL_* in ddt_sorted.hip; ddt_tune "spol")
+    hipError_t run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol, hipStream_t stream);
 };
 
 }  // namespace ddt

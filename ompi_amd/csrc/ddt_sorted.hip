@@ -52,6 +52,36 @@ constexpr int BT = 256;                // threads per build workgroup
 constexpr uint32_t LDS_BYTES = 128u << 10;
 constexpr uint16_t PAD = 0xFFFF;       // upos of a padding slot
 
+// Access policy bits of one run (SortedList::run, ddt_tune("spol")):
+constexpr uint32_t POL_USER_WT = 1;    // unpack 1': user-side stores written through L2 (sc1)
+constexpr uint32_t POL_STREAM_NTS = 2; // stores of U and of the packed side non-temporal
+constexpr uint32_t POL_STREAM_NTL = 4; // loads of A, SL, U, upos and the packed side non-temporal
+constexpr uint32_t POL_USER_NTL = 8;   // pack 1: user-side loads non-temporal
+
+template <typename T> __device__ __forceinline__ T ldp(const T *p, bool nt)
+{
+    return nt ? __builtin_nontemporal_load(p) : *p;
+}
+template <typename T> __device__ __forceinline__ void stp(T *p, T v, bool nt)
+{
+    if (nt)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+__device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v)
+{
+    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_sc1(u32x2 *p, u32x2 v)
+{
+    asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_sc1(u32x4 *p, u32x4 v)
+{
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
 #define HK(x)                                                                                   \
     do {                                                                                        \
         hipError_t e_ = (x);                                                                    \
@@ -188,10 +218,11 @@ template <int E>
 __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, const uint32_t *__restrict__ A,
                                               const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
                                               const uint32_t *__restrict__ ub, uint8_t *__restrict__ U, uint32_t n,
-                                              uint32_t nb)
+                                              uint32_t nb, uint32_t pol)
 {
     using T = typename Elem<E>::T;
     constexpr uint32_t CH = LDS_BYTES / E, SEG = 64 / E;
+    const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS, ntu = pol & POL_USER_NTL;
     __shared__ T lds[CH + SEG];
     __shared__ uint16_t toff[MAXNB + 1];
     __shared__ uint32_t tub[MAXNB];
@@ -207,8 +238,8 @@ __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, 
         for (int q = 0; q < K; ++q) {
             const uint32_t t = t0 + q * PT;
             if (t < m) {
-                s[q] = SL[j0 + t];
-                v[q] = src[A[j0 + t]];
+                s[q] = ldp(&SL[j0 + t], ntl);
+                v[q] = ldp(&src[ldp(&A[j0 + t], ntl)], ntu);
             }
         }
 #pragma unroll
@@ -223,7 +254,7 @@ __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, 
         const uint32_t o = toff[k], cn = toff[k + 1] - o;
         const uint32_t b = tub[k], pn = (cn + SEG - 1) / SEG * SEG;
         for (uint32_t q = lane; q < pn; q += SEG)
-            dst[b + q] = lds[o + q];   // padding slots carry a neighbour's bytes: whole segments
+            stp(&dst[b + q], lds[o + q], nts);   // padding slots carry a neighbour's bytes: whole segments
     }
 }
 
@@ -231,10 +262,11 @@ __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, 
 template <int E>
 __global__ __launch_bounds__(PT) void k_pack2(const uint8_t *__restrict__ U, const uint16_t *__restrict__ upos,
                                               const uint32_t *__restrict__ bstart, uint8_t *__restrict__ packed,
-                                              uint32_t n)
+                                              uint32_t n, uint32_t pol)
 {
     using T = typename Elem<E>::T;
     constexpr uint32_t RG = LDS_BYTES / E;
+    const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS;
     __shared__ T lds[RG];
     const uint32_t k = blockIdx.x;
     const uint32_t s0 = bstart[k], s1 = bstart[k + 1];
@@ -248,8 +280,8 @@ __global__ __launch_bounds__(PT) void k_pack2(const uint8_t *__restrict__ U, con
             const uint32_t x = x0 + q * PT;
             p[q] = PAD;
             if (x < s1) {
-                p[q] = upos[x];
-                v[q] = src[x];
+                p[q] = ldp(&upos[x], ntl);
+                v[q] = ldp(&src[x], ntl);
             }
         }
 #pragma unroll
@@ -261,17 +293,18 @@ __global__ __launch_bounds__(PT) void k_pack2(const uint8_t *__restrict__ U, con
     const uint32_t m = min(RG, n - k * RG);
     T *dst = reinterpret_cast<T *>(packed) + size_t(k) * RG;
     for (uint32_t t = threadIdx.x; t < m; t += PT)
-        dst[t] = lds[t];
+        stp(&dst[t], lds[t], nts);
 }
 
 // unpack pass 2': the bucket's packed elements into LDS, then out to U in run order
 template <int E>
 __global__ __launch_bounds__(PT) void k_unpack2(const uint8_t *__restrict__ packed, const uint16_t *__restrict__ upos,
                                                 const uint32_t *__restrict__ bstart, uint8_t *__restrict__ U,
-                                                uint32_t n)
+                                                uint32_t n, uint32_t pol)
 {
     using T = typename Elem<E>::T;
     constexpr uint32_t RG = LDS_BYTES / E;
+    const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS;
     __shared__ T lds[RG];
     const uint32_t k = blockIdx.x;
     const uint32_t m = min(RG, n - k * RG);
@@ -282,7 +315,7 @@ __global__ __launch_bounds__(PT) void k_unpack2(const uint8_t *__restrict__ pack
 #pragma unroll
         for (int q = 0; q < K; ++q)
             if (t0 + q * PT < m)
-                v[q] = src[t0 + q * PT];
+                v[q] = ldp(&src[t0 + q * PT], ntl);
 #pragma unroll
         for (int q = 0; q < K; ++q)
             if (t0 + q * PT < m)
@@ -295,14 +328,14 @@ __global__ __launch_bounds__(PT) void k_unpack2(const uint8_t *__restrict__ pack
         uint32_t p[K];
 #pragma unroll
         for (int q = 0; q < K; ++q)
-            p[q] = x0 + q * PT < s1 ? uint32_t(upos[x0 + q * PT]) : uint32_t(PAD);
+            p[q] = x0 + q * PT < s1 ? uint32_t(ldp(&upos[x0 + q * PT], ntl)) : uint32_t(PAD);
 #pragma unroll
         for (int q = 0; q < K; ++q) {
             if (x0 + q * PT < s1) {
                 T v{};
                 if (p[q] != PAD)
                     v = lds[p[q]];
-                dst[x0 + q * PT] = v;   // padding slots written too: whole segments
+                stp(&dst[x0 + q * PT], v, nts);   // padding slots written too: whole segments
             }
         }
     }
@@ -313,10 +346,11 @@ template <int E>
 __global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, const uint32_t *__restrict__ A,
                                                 const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
                                                 const uint32_t *__restrict__ ub, const uint8_t *__restrict__ U,
-                                                uint32_t n, uint32_t nb)
+                                                uint32_t n, uint32_t nb, uint32_t pol)
 {
     using T = typename Elem<E>::T;
     constexpr uint32_t CH = LDS_BYTES / E, SEG = 64 / E, NSUB = PT / SEG;
+    const bool ntl = pol & POL_STREAM_NTL, wt = pol & POL_USER_WT;
     __shared__ T lds[CH];
     __shared__ uint16_t toff[MAXNB + 1];
     __shared__ uint32_t tub[MAXNB];
@@ -341,7 +375,7 @@ __global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, cons
                 cn[i] = toff[k + 1] - o[i];
                 bb[i] = tub[k];
                 if (lane < cn[i])
-                    v[i] = src[bb[i] + lane];
+                    v[i] = ldp(&src[bb[i] + lane], ntl);
             }
         }
 #pragma unroll
@@ -363,14 +397,18 @@ __global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, cons
         for (int q = 0; q < K; ++q) {
             const uint32_t t = t0 + q * PT;
             if (t < m) {
-                a[q] = A[j0 + t];
-                v[q] = lds[SL[j0 + t]];
+                a[q] = ldp(&A[j0 + t], ntl);
+                v[q] = lds[ldp(&SL[j0 + t], ntl)];
             }
         }
 #pragma unroll
         for (int q = 0; q < K; ++q)
-            if (t0 + q * PT < m)
-                dst[a[q]] = v[q];
+            if (t0 + q * PT < m) {
+                if (wt)
+                    st_sc1(&dst[a[q]], v[q]);
+                else
+                    dst[a[q]] = v[q];
+            }
     }
 }
 
@@ -490,7 +528,7 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
 
 // One whole-list pack (dir 0) or unpack (dir 1) of one instance.  `user` points at the
 // list's first element (minimum displacement), `packed` at the instance's packed bytes.
-hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, hipStream_t stream)
+hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol, hipStream_t stream)
 {
     // U is one scratch per plan: a launch on another stream waits for the last one
     std::lock_guard<std::mutex> g(mu);
@@ -503,11 +541,11 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, hipStream_t 
     uint8_t *u8 = static_cast<uint8_t *>(U);
 #define DDT_SORTED_LAUNCH(E)                                                                              \
     if (dir == 0) {                                                                                       \
-        hipLaunchKernelGGL((k_pack1<E>), gc, blk, 0, stream, user, A, SL, off16, ub, u8, n, nb);   \
-        hipLaunchKernelGGL((k_pack2<E>), gb, blk, 0, stream, u8, upos, bstart, packed, n);                \
+        hipLaunchKernelGGL((k_pack1<E>), gc, blk, 0, stream, user, A, SL, off16, ub, u8, n, nb, pol);   \
+        hipLaunchKernelGGL((k_pack2<E>), gb, blk, 0, stream, u8, upos, bstart, packed, n, pol);                \
     } else {                                                                                              \
-        hipLaunchKernelGGL((k_unpack2<E>), gb, blk, 0, stream, packed, upos, bstart, u8, n);              \
-        hipLaunchKernelGGL((k_unpack1<E>), gc, blk, 0, stream, user, A, SL, off16, ub, u8, n, nb); \
+        hipLaunchKernelGGL((k_unpack2<E>), gb, blk, 0, stream, packed, upos, bstart, u8, n, pol);              \
+        hipLaunchKernelGGL((k_unpack1<E>), gc, blk, 0, stream, user, A, SL, off16, ub, u8, n, nb, pol); \
     }
     if (esz == 4) {
         DDT_SORTED_LAUNCH(4)
