@@ -9,8 +9,10 @@ for f in ddt_typemap ddt_plan ddt_convertor ddt_external; do
   /opt/rocm/bin/hipcc -std=c++17 -O1 -g -fPIC -I../../include --offload-arch=gfx950 \
     -Xarch_host -fsanitize=address -fno-omit-frame-pointer -c $f.cpp -o build_asan/$f.o
 done
-/opt/rocm/bin/hipcc -std=c++17 -O1 -fPIC -I../../include --offload-arch=gfx950 -x hip \
-  -c ddt_kernels.hip -o build_asan/ddt_kernels.o
+for f in ddt_kernels ddt_sorted; do
+  /opt/rocm/bin/hipcc -std=c++17 -O1 -fPIC -I../../include --offload-arch=gfx950 -x hip \
+    -c $f.hip -o build_asan/$f.o
+done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Xarch_host -fsanitize=address \
   -o build_asan/libddt_hip_asan.so build_asan/*.o
 cd ../..
