@@ -93,7 +93,8 @@ def _roundtrip(b: R.Built, count: int, device, seed: int, frags=None):
     np.testing.assert_array_equal(_host(out), exp)
 
 
-@pytest.mark.parametrize("seed", range(6))
+# DDT_FUZZ_SEEDS widens the sweep for soak runs (default 6 seeds x 60 random types)
+@pytest.mark.parametrize("seed", range(int(__import__("os").environ.get("DDT_FUZZ_SEEDS", "6"))))
 def test_fuzz_full_message(device, seed):
     rng = random.Random(1000 + seed)
     for n in range(60):
