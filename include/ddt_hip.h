@@ -197,6 +197,25 @@ int ddt_convertor_get_packed_size(const ddt_convertor_t *conv, size_t *size);
 /* bConverted and CONVERTOR_COMPLETED (opal_convertor.h:137-148) */
 int ddt_convertor_get_position(const ddt_convertor_t *conv, size_t *position);
 int ddt_convertor_is_completed(const ddt_convertor_t *conv);
+/* opal_convertor_clone (opal_convertor.c:708-756) and clone_with_position
+ * (opal_convertor.h:399-404): `dst` gets `src`'s type, count, buffer, direction and stream.
+ * copy_stack != 0 also copies the position; otherwise the clone starts at position 0 (the
+ * reference leaves bConverted = -1 until a set_position).  `dst`'s own staging buffers stay. */
+int ddt_convertor_clone(const ddt_convertor_t *src, ddt_convertor_t *dst, int copy_stack);
+int ddt_convertor_clone_with_position(const ddt_convertor_t *src, ddt_convertor_t *dst, int copy_stack,
+                                      size_t *position);
+/* opal_convertor_need_buffers (opal_convertor.h:231-240): 0 when the user buffer itself is the
+ * packed stream (no gaps, or one contiguous instance), 1 otherwise; always homogeneous. */
+int ddt_convertor_need_buffers(const ddt_convertor_t *conv);
+/* opal_convertor_get_current_pointer / get_offset_pointer (opal_convertor.h:300-312):
+ * base + position (or offset) + true_lb; meaningful for contiguous types. */
+int ddt_convertor_get_current_pointer(const ddt_convertor_t *conv, void **position);
+int ddt_convertor_get_offset_pointer(const ddt_convertor_t *conv, size_t offset, void **position);
+/* opal_convertor_get_unpacked_size: local size (== packed size, homogeneous). */
+int ddt_convertor_get_unpacked_size(const ddt_convertor_t *conv, size_t *size);
+/* opal_convertor_cleanup (opal_convertor.h:208-219): back to an unprepared, completed
+ * convertor that can be prepared again (freelist reuse); stream and staging are kept. */
+int ddt_convertor_cleanup(ddt_convertor_t *conv);
 /* CONVERTOR_ACCELERATOR_ASYNC + convertor->stream (opal_convertor.h:150, pml_ob1_recvreq.c:627-663):
  * with async != 0 the kernels are enqueued on `hip_stream` and pack/unpack return without
  * synchronizing; the caller records an event on the stream.  async == 0 (default) = synchronous. */

@@ -70,6 +70,13 @@ SIGNATURES = {
     "ddt_convertor_get_packed_size": (c_int, [c_void_p, P(c_size_t)]),
     "ddt_convertor_get_position": (c_int, [c_void_p, P(c_size_t)]),
     "ddt_convertor_is_completed": (c_int, [c_void_p]),
+    "ddt_convertor_clone": (c_int, [c_void_p, c_void_p, c_int]),
+    "ddt_convertor_clone_with_position": (c_int, [c_void_p, c_void_p, c_int, P(c_size_t)]),
+    "ddt_convertor_need_buffers": (c_int, [c_void_p]),
+    "ddt_convertor_get_current_pointer": (c_int, [c_void_p, P(c_void_p)]),
+    "ddt_convertor_get_offset_pointer": (c_int, [c_void_p, c_size_t, P(c_void_p)]),
+    "ddt_convertor_get_unpacked_size": (c_int, [c_void_p, P(c_size_t)]),
+    "ddt_convertor_cleanup": (c_int, [c_void_p]),
     "ddt_convertor_set_stream": (c_int, [c_void_p, c_void_p, c_int]),
     "ddt_pack": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p, c_size_t, P(c_size_t)]),
     "ddt_unpack": (c_int, [c_void_p, c_size_t, P(c_size_t), c_void_p, c_size_t, c_void_p]),

@@ -66,6 +66,42 @@ class Convertor:
               "ddt_convertor_prepare_for_raw")
         return self
 
+    def clone(self, position: int | None = None, copy_stack: bool = False) -> "Convertor":
+        """opal_convertor_clone / clone_with_position: a new convertor on the same message."""
+        c = Convertor()
+        if position is None:
+            check(lib().ddt_convertor_clone(self.h, c.h, int(copy_stack)), "ddt_convertor_clone")
+        else:
+            p = ctypes.c_size_t(position)
+            check(lib().ddt_convertor_clone_with_position(self.h, c.h, int(copy_stack), ctypes.byref(p)),
+                  "ddt_convertor_clone_with_position")
+        return c
+
+    def need_buffers(self) -> bool:
+        """opal_convertor_need_buffers: False when the user buffer is the packed stream."""
+        return bool(lib().ddt_convertor_need_buffers(self.h))
+
+    def current_pointer(self) -> int:
+        p = ctypes.c_void_p()
+        check(lib().ddt_convertor_get_current_pointer(self.h, ctypes.byref(p)), "get_current_pointer")
+        return int(p.value or 0)
+
+    def offset_pointer(self, offset: int) -> int:
+        p = ctypes.c_void_p()
+        check(lib().ddt_convertor_get_offset_pointer(self.h, offset, ctypes.byref(p)), "get_offset_pointer")
+        return int(p.value or 0)
+
+    @property
+    def unpacked_size(self) -> int:
+        s = ctypes.c_size_t()
+        check(lib().ddt_convertor_get_unpacked_size(self.h, ctypes.byref(s)), "get_unpacked_size")
+        return int(s.value)
+
+    def cleanup(self) -> "Convertor":
+        """opal_convertor_cleanup: reusable, unprepared and completed."""
+        check(lib().ddt_convertor_cleanup(self.h), "ddt_convertor_cleanup")
+        return self
+
     def raw(self, max_iov: int):
         """opal_convertor_raw: (1 if the whole message is described else 0,
         [(address, length)] of user memory in type-map order, bytes described)."""

@@ -560,6 +560,86 @@ int ddt_convertor_get_position(const ddt_convertor_t *c, size_t *position)
 
 int ddt_convertor_is_completed(const ddt_convertor_t *c) { return c && c->completed ? 1 : 0; }
 
+int ddt_convertor_clone(const ddt_convertor_t *src, ddt_convertor_t *dst, int copy_stack)
+{
+    // opal_convertor_clone (opal_convertor.c:708-756): the resume state is bConverted only
+    if (!src || !dst || src == dst)
+        return fail(DDT_ERR_BAD_PARAM, "bad convertor");
+    dst->dt = src->dt;
+    dst->plan = src->plan;
+    dst->count = src->count;
+    dst->base = src->base;
+    dst->send = src->send;
+    dst->prepared = src->prepared;
+    dst->local_size = src->local_size;
+    dst->stream = src->stream;
+    dst->async = src->async;
+    dst->bConverted = copy_stack ? src->bConverted : 0;
+    dst->completed = copy_stack ? src->completed : (src->local_size == 0);
+    return DDT_SUCCESS;
+}
+
+int ddt_convertor_clone_with_position(const ddt_convertor_t *src, ddt_convertor_t *dst, int copy_stack,
+                                      size_t *position)
+{
+    int rc = ddt_convertor_clone(src, dst, copy_stack);
+    if (rc != DDT_SUCCESS)
+        return rc;
+    return ddt_convertor_set_position(dst, position);
+}
+
+int ddt_convertor_need_buffers(const ddt_convertor_t *c)
+{
+    // opal_convertor_need_buffers (opal_convertor.h:231-240), homogeneous
+    if (!c || !c->dt)
+        return 1;
+    if (c->dt->flags & F_NO_GAPS)
+        return 0;
+    if (c->count == 1 && (c->dt->flags & F_CONTIGUOUS))
+        return 0;
+    return 1;
+}
+
+int ddt_convertor_get_current_pointer(const ddt_convertor_t *c, void **position)
+{
+    if (!c || !c->dt || !position)
+        return DDT_ERR_BAD_PARAM;
+    *position = reinterpret_cast<void *>(c->base + c->bConverted + uint64_t(c->dt->true_lb));
+    return DDT_SUCCESS;
+}
+
+int ddt_convertor_get_offset_pointer(const ddt_convertor_t *c, size_t offset, void **position)
+{
+    if (!c || !c->dt || !position)
+        return DDT_ERR_BAD_PARAM;
+    *position = reinterpret_cast<void *>(c->base + uint64_t(offset) + uint64_t(c->dt->true_lb));
+    return DDT_SUCCESS;
+}
+
+int ddt_convertor_get_unpacked_size(const ddt_convertor_t *c, size_t *size)
+{
+    if (!c || !size)
+        return DDT_ERR_BAD_PARAM;
+    *size = size_t(c->local_size);
+    return DDT_SUCCESS;
+}
+
+int ddt_convertor_cleanup(ddt_convertor_t *c)
+{
+    // opal_convertor_cleanup (opal_convertor.h:208-219)
+    if (!c)
+        return DDT_ERR_BAD_PARAM;
+    c->dt = nullptr;
+    c->plan.reset();
+    c->count = 0;
+    c->base = 0;
+    c->prepared = false;
+    c->completed = true;
+    c->local_size = 0;
+    c->bConverted = 0;
+    return DDT_SUCCESS;
+}
+
 int ddt_convertor_set_stream(ddt_convertor_t *c, void *s, int async)
 {
     if (!c)

@@ -206,3 +206,35 @@ def test_imported_indexed_description_folds_to_one_list():
         E.emulate(its, user, UA, packed, PA, 0, E.list_tables(e))
         ref = np.frombuffer(b.o.pack(1, user, origin, 0, info["size"], element_granular=False), dtype=np.uint8)
         np.testing.assert_array_equal(packed, ref)
+
+
+def test_convertor_clone_need_buffers_pointers_cleanup():
+    """opal_convertor_clone(_with_position), need_buffers, get_current/offset_pointer,
+    get_unpacked_size and cleanup (opal_convertor.h:208-312, opal_convertor.c:708-756),
+    exercised on raw-prepared convertors (no data moves)."""
+    f = D.MPI.MPI_FLOAT
+    contig = D.create_contiguous(16, f).commit()
+    vec = D.create_vector(8, 1, 2, f).commit()
+    # need_buffers: no gaps or one contiguous instance -> 0; a gapped vector -> 1
+    c = ompi_amd.Convertor().prepare_for_raw(contig, 3, BASE)
+    assert not c.need_buffers()
+    v = ompi_amd.Convertor().prepare_for_raw(vec, 2, BASE)
+    assert v.need_buffers()
+    assert v.unpacked_size == v.packed_size == 2 * 8 * 4
+    # pointers: base + position (+ true_lb)
+    c.set_position(40)
+    assert c.current_pointer() == BASE + 40 and c.offset_pointer(100) == BASE + 100
+    # clone keeps the message, resets or keeps the position; clone_with_position repositions
+    d = c.clone()
+    assert d.packed_size == c.packed_size and d.current_pointer() == BASE
+    e = c.clone(copy_stack=True)
+    assert e.current_pointer() == BASE + 40
+    g = v.clone(position=12)
+    rc, iovs, n = g.raw(64)
+    assert rc == 1 and n == 2 * 8 * 4 - 12
+    assert iovs[0] == (BASE + 3 * 8, 4)   # element 3 of the stream at byte 24 of the vector
+    # cleanup: completed, unprepared, reusable
+    v.cleanup()
+    assert v.completed
+    v.prepare_for_raw(contig, 1, BASE)
+    assert v.packed_size == 64 and not v.completed

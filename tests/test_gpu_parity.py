@@ -819,3 +819,28 @@ def test_sorted_list_engine_concurrent_streams(device, sorted_from):
     assert not errors, errors
     for t in range(2):
         np.testing.assert_array_equal(_host(outs[t]), ref)
+
+
+def test_clone_with_position_fragments(device):
+    """The ob1 pipeline pattern (pml_ob1_sendreq.c:1184-1194): one prepared send convertor,
+    cloned with a position per fragment; every clone packs its own fragment, in any order."""
+    import torch
+    import ompi_amd
+    b = R.Built(("vector", 1000, 3, 7, ("basic", 16)))
+    count = 5
+    info = b.o.info()
+    size = info["size"] * count
+    span, origin = R.layout(info, count)
+    host = R.fill(span, 21)
+    user = _dev(host, device)
+    ref = np.frombuffer(b.o.pack(count, host, origin, 0, size, element_granular=False), dtype=np.uint8)
+    master = ompi_amd.Convertor().prepare_for_send(b.engine(), count, user.data_ptr() + origin)
+    packed = torch.zeros(size, dtype=torch.uint8, device=device)
+    frag = 24 * 1000   # a multiple of the element size: fragments never split an element
+    starts = list(range(0, size, frag))
+    for p in reversed(starts):
+        c = master.clone(position=p)
+        n = min(frag, size - p)
+        rc, _, md = c.pack([(packed.data_ptr() + p, n)])
+        assert md == n and rc == (1 if p + n == size else 0)
+    np.testing.assert_array_equal(_host(packed), ref)
