@@ -246,6 +246,13 @@ int ddt_unpack_window(const ddt_datatype_t *type, size_t count, void *buf, size_
 int ddt_copy_content_same_ddt(const ddt_datatype_t *type, size_t count, void *dst, const void *src,
                               void *hip_stream);
 
+/* ompi_datatype_sndrcv (ompi/datatype/ompi_datatype_sndrcv.c:46-126): local send/recv between
+ * two typed device buffers (collectives' self copies).  A NULL type marks that side as
+ * MPI_PACKED (count = bytes).  Same type: one typed-copy launch; two types: pack into HBM
+ * scratch and unpack, stream-ordered; synchronous on `hip_stream`.  Truncation rules and the
+ * DDT_ERR_TRUNCATE cases are the reference's. */
+int ddt_sndrcv(const void *sbuf, size_t scount, const ddt_datatype_t *stype, void *rbuf, size_t rcount,
+               const ddt_datatype_t *rtype, void *hip_stream);
 /* Plan introspection for tests/benchmarks: number of leaves, device metadata bytes. */
 int ddt_type_plan_info(const ddt_datatype_t *type, int64_t *out4);
 /* Which engine whole-message moves of this type use: out4 = [state, device bytes, chunks,

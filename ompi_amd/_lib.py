@@ -86,6 +86,7 @@ SIGNATURES = {
     "ddt_unpack_window": (c_int, [c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, c_size_t,
                                   c_void_p]),
     "ddt_copy_content_same_ddt": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p, c_void_p]),
+    "ddt_sndrcv": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p]),
     "ddt_type_plan_info": (c_int, [c_void_p, P(c_int64)]),
     "ddt_type_engine_info": (c_int, [c_void_p, P(c_int64)]),
     "ddt_type_plan_leaves": (c_int64, [c_void_p, P(c_int64), c_size_t]),

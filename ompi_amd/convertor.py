@@ -201,6 +201,14 @@ def copy_content_same_ddt(dt: Datatype, count: int, dst, src, stream=None) -> No
                                           stream_handle(stream)), "ddt_copy_content_same_ddt")
 
 
+def sndrcv(sbuf, scount: int, stype, rbuf, rcount: int, rtype, stream=None) -> None:
+    """ompi_datatype_sndrcv: local send/recv between typed device buffers; a type of None
+    marks that side as MPI_PACKED bytes."""
+    check(lib().ddt_sndrcv(addr(sbuf), scount, stype.handle if stype is not None else None,
+                           addr(rbuf), rcount, rtype.handle if rtype is not None else None,
+                           stream_handle(stream)), "ddt_sndrcv")
+
+
 # ------------------------------------------------------------------ external32
 def pack_external_size(incount: int, dt: Datatype, datarep: str = "external32") -> int:
     """MPI_Pack_external_size."""

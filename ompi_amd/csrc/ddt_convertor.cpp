@@ -707,6 +707,64 @@ int ddt_unpack(const void *inbuf, size_t insize, size_t *position, void *outbuf,
     return DDT_SUCCESS;
 }
 
+int ddt_sndrcv(const void *sbuf, size_t scount, const ddt_datatype_t *st, void *rbuf, size_t rcount,
+               const ddt_datatype_t *rt, void *stream)
+{
+    // ompi_datatype_sndrcv (ompi/datatype/ompi_datatype_sndrcv.c:46-126): a local send/recv
+    // between two typed device buffers.  A null type means that side is MPI_PACKED bytes.
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const size_t ssz = st ? size_t(st->size) : 1, rsz = rt ? size_t(rt->size) : 1;
+    if (!st && !rt)
+        return fail(DDT_ERR_BAD_PARAM, "both sides packed");
+    if (rcount == 0 || rsz == 0)
+        return (scount == 0 || ssz == 0) ? DDT_SUCCESS : fail(DDT_ERR_TRUNCATE, "receive is empty");
+    auto one_side = [&](const ddt_datatype_t *t, size_t count, const void *ubuf, void *pbuf, size_t n,
+                        int dir, size_t *moved) -> int {
+        ddt_convertor c;
+        int rc = prepare(&c, t, count, ubuf, dir == 0);
+        if (rc != DDT_SUCCESS)
+            return rc;
+        c.stream = s;
+        struct iovec iov{pbuf, n};
+        uint32_t k = 1;
+        int32_t r = advance(&c, &iov, &k, moved, dir);
+        return r < 0 ? r : DDT_SUCCESS;
+    };
+    size_t moved = 0;
+    int rc;
+    if (st && rt && st == rt) {   // same datatype: typed copy of min(scount, rcount) instances
+        if ((rc = ddt_copy_content_same_ddt(rt, std::min(scount, rcount), rbuf, sbuf, stream)) != DDT_SUCCESS)
+            return rc;
+        return scount > rcount ? fail(DDT_ERR_TRUNCATE, "send larger than receive") : DDT_SUCCESS;
+    }
+    if (!rt) {                    // receive packed: rcount bytes
+        const size_t n = std::min(scount * ssz, rcount);
+        if ((rc = one_side(st, scount, sbuf, rbuf, n, 0, &moved)) != DDT_SUCCESS)
+            return rc;
+        // the reference reports MPI_ERR_TRUNCATE whenever fewer than rcount bytes arrive
+        return moved < rcount ? fail(DDT_ERR_TRUNCATE, "packed receive not filled") : DDT_SUCCESS;
+    }
+    if (!st) {                    // send packed: scount bytes
+        const size_t n = std::min(rcount * rsz, scount);
+        if ((rc = one_side(rt, rcount, rbuf, const_cast<void *>(sbuf), n, 1, &moved)) != DDT_SUCCESS)
+            return rc;
+        return scount > moved ? fail(DDT_ERR_TRUNCATE, "packed send larger than receive") : DDT_SUCCESS;
+    }
+    // two datatypes: pack into HBM scratch, unpack from it (the reference pipelines 64 KiB
+    // host chunks; here it is one launch per side, stream-ordered)
+    const size_t n = std::min(scount * ssz, rcount * rsz);
+    void *tmp = nullptr;
+    HIPCHK(hipMallocAsync(&tmp, n ? n : 1, s));
+    rc = one_side(st, scount, sbuf, tmp, n, 0, &moved);
+    if (rc == DDT_SUCCESS && moved)
+        rc = one_side(rt, rcount, rbuf, tmp, moved, 1, &moved);
+    (void) hipFreeAsync(tmp, s);
+    if (rc != DDT_SUCCESS)
+        return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    return scount * ssz <= rcount * rsz ? DDT_SUCCESS : fail(DDT_ERR_TRUNCATE, "send larger than receive");
+}
+
 // ---------------------------------------------------------------- external32
 namespace {
 

@@ -844,3 +844,48 @@ def test_clone_with_position_fragments(device):
         rc, _, md = c.pack([(packed.data_ptr() + p, n)])
         assert md == n and rc == (1 if p + n == size else 0)
     np.testing.assert_array_equal(_host(packed), ref)
+
+
+def test_sndrcv_matches_oracle(device):
+    """ompi_datatype_sndrcv.c:46-126 on device buffers: two datatypes of one signature
+    (vector -> contiguous, struct -> indexed), the same datatype, MPI_PACKED on either side,
+    and the reference's truncation codes."""
+    import torch
+    import ompi_amd
+    from ompi_amd.convertor import sndrcv
+    cases = [
+        (("vector", 64, 3, 5, ("basic", 16)), 3, ("contig", 192, ("basic", 16)), 3),
+        (("struct", [2, 1], [0, 24], [("basic", 6), ("basic", 16)]), 50,
+         ("indexed", [2, 2], [0, 3], ("basic", 6)), 50),
+        (("hvector", 40, 1, 24, ("basic", 16)), 7, None, 0),
+    ]
+    for srec, scount, rrec, rcount in cases:
+        sb = R.Built(srec)
+        si = sb.o.info()
+        sspan, sorg = R.layout(si, scount)
+        host = R.fill(sspan, 31)
+        src = _dev(host, device)
+        stream_bytes = sb.o.pack(scount, host, sorg, 0, si["size"] * scount, element_granular=False)
+        rb = R.Built(rrec) if rrec else sb
+        rc_ = rcount if rrec else scount
+        ri = rb.o.info()
+        rspan, rorg = R.layout(ri, rc_)
+        dst = torch.full((rspan,), 0xA5, dtype=torch.uint8, device=device)
+        exp = np.full(rspan, 0xA5, dtype=np.uint8)
+        rb.o.unpack(rc_, exp, rorg, 0, stream_bytes)
+        sndrcv(src.data_ptr() + sorg, scount, sb.engine(), dst.data_ptr() + rorg, rc_, rb.engine())
+        np.testing.assert_array_equal(_host(dst), exp)
+        # MPI_PACKED receive and send
+        pk = torch.zeros(len(stream_bytes), dtype=torch.uint8, device=device)
+        sndrcv(src.data_ptr() + sorg, scount, sb.engine(), pk, len(stream_bytes), None)
+        np.testing.assert_array_equal(_host(pk), np.frombuffer(stream_bytes, dtype=np.uint8))
+        dst2 = torch.full((rspan,), 0xA5, dtype=torch.uint8, device=device)
+        sndrcv(pk, len(stream_bytes), None, dst2.data_ptr() + rorg, rc_, rb.engine())
+        np.testing.assert_array_equal(_host(dst2), exp)
+    # truncation: more sent than the receive holds
+    t = R.Built(("contig", 8, ("basic", 6)))
+    a = torch.zeros(64, dtype=torch.uint8, device=device)
+    b = torch.zeros(64, dtype=torch.uint8, device=device)
+    with pytest.raises(ompi_amd.DDTError) as ei:
+        sndrcv(a, 2, t.engine(), b, 1, t.engine())
+    assert ei.value.code == -9
