@@ -18,6 +18,9 @@ struct SortedList {
     uint64_t slots = 0;      // U slots, runs padded to whole segments
     uint64_t dev_bytes = 0;  // device bytes held (tables + U)
     uint32_t *A = nullptr;       // [n] element offset (units of esz) of the j-th block in address order
+                                 // (freed after the build when the compressed form below fits)
+    uint16_t *A16 = nullptr;     // [n] A[j] - Abase[j / 64]: 16-bit offsets inside 64-element groups
+    uint32_t *Abase = nullptr;   // [n / 64] A of each group's first element
     uint16_t *SL = nullptr;      // [n] LDS slot of the j-th block inside its chunk
     uint16_t *off16 = nullptr;   // [nc][nb] LDS offset of run (c, k): exclusive prefix over k of
                                  // the blocks of chunk c whose packed position is in bucket k

@@ -82,6 +82,19 @@ __device__ __forceinline__ void st_sc1(u32x4 *p, u32x4 v)
     asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
 
+// Sorted element offsets as the pass kernels read them: 16-bit offsets within 64-element
+// groups plus one 32-bit base per group when every group spans < 64 Ki elements (the
+// build checks; 2.06 bytes per element instead of 4), else the plain 32-bit array.
+struct AddrList {
+    const uint32_t *A;
+    const uint16_t *A16;
+    const uint32_t *Abase;
+};
+__device__ __forceinline__ uint32_t addr_at(const AddrList &L, uint32_t j, bool nt)
+{
+    return L.A16 ? L.Abase[j >> 6] + uint32_t(ldp(&L.A16[j], nt)) : ldp(&L.A[j], nt);
+}
+
 #define HK(x)                                                                                   \
     do {                                                                                        \
         hipError_t e_ = (x);                                                                    \
@@ -126,6 +139,23 @@ __global__ __launch_bounds__(BT) void k_rank(const int32_t *__restrict__ disp, u
         A[j] = a;
         const uint32_t c = j / ch, k = i / ch;   // CH == RG
         rr[i] = uint16_t(atomicAdd(&cnt[size_t(c) * nb + k], 1u));
+    }
+}
+
+// 16-bit form of A: offsets inside groups of 64 consecutive sorted elements; *maxspan gets
+// the largest group span (the form is used only if it is < 64 Ki)
+__global__ __launch_bounds__(BT) void k_compress(const uint32_t *__restrict__ A, uint32_t n,
+                                                 uint16_t *__restrict__ A16, uint32_t *__restrict__ Abase,
+                                                 uint32_t *__restrict__ maxspan)
+{
+    for (uint32_t j = blockIdx.x * BT + threadIdx.x; j < n; j += gridDim.x * BT) {
+        const uint32_t g0 = j & ~63u, base = A[g0];
+        const uint32_t d = A[j] - base;
+        A16[j] = uint16_t(d);
+        if (j == g0)
+            Abase[j >> 6] = base;
+        if (d > 0xFFFFu)
+            atomicMax(maxspan, d);
     }
 }
 
@@ -215,7 +245,7 @@ __device__ __forceinline__ void stage_tables(const uint16_t *__restrict__ off16,
 
 // pack pass 1: gather the chunk in address order into LDS, emit its runs bucket by bucket
 template <int E>
-__global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, const uint32_t *__restrict__ A,
+__global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, const AddrList al,
                                               const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
                                               const uint32_t *__restrict__ ub, uint8_t *__restrict__ U, uint32_t n,
                                               uint32_t nb, uint32_t pol)
@@ -239,7 +269,7 @@ __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, 
             const uint32_t t = t0 + q * PT;
             if (t < m) {
                 s[q] = ldp(&SL[j0 + t], ntl);
-                v[q] = ldp(&src[ldp(&A[j0 + t], ntl)], ntu);
+                v[q] = ldp(&src[addr_at(al, j0 + t, ntl)], ntu);
             }
         }
 #pragma unroll
@@ -343,7 +373,7 @@ __global__ __launch_bounds__(PT) void k_unpack2(const uint8_t *__restrict__ pack
 
 // unpack pass 1': the chunk's runs into LDS, then scattered to the user side in address order
 template <int E>
-__global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, const uint32_t *__restrict__ A,
+__global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, const AddrList al,
                                                 const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
                                                 const uint32_t *__restrict__ ub, const uint8_t *__restrict__ U,
                                                 uint32_t n, uint32_t nb, uint32_t pol)
@@ -397,7 +427,7 @@ __global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, cons
         for (int q = 0; q < K; ++q) {
             const uint32_t t = t0 + q * PT;
             if (t < m) {
-                a[q] = ldp(&A[j0 + t], ntl);
+                a[q] = addr_at(al, j0 + t, ntl);
                 v[q] = lds[ldp(&SL[j0 + t], ntl)];
             }
         }
@@ -433,8 +463,8 @@ SortedList::~SortedList()
 {
     if (done)
         (void) hipEventSynchronize(done);
-    for (void *p : {(void *) A, (void *) SL, (void *) off16, (void *) ub, (void *) bstart,
-                    (void *) upos, U})
+    for (void *p : {(void *) A, (void *) A16, (void *) Abase, (void *) SL, (void *) off16, (void *) ub,
+                    (void *) bstart, (void *) upos, U})
         if (p)
             (void) hipFree(p);
     if (done)
@@ -500,6 +530,26 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
         bstart = dalloc<uint32_t>(nb + 1, bytes);
         hipLaunchKernelGGL(k_rank, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, bm, wpre, ch, nb, A,
                            cnt, rr);
+        {   // the 16-bit form of A, kept when every 64-element group spans < 64 Ki elements
+            uint64_t cb = 0;
+            A16 = dalloc<uint16_t>(n, cb);
+            Abase = dalloc<uint32_t>((n + 63) / 64, cb);
+            HK(hipMemsetAsync(dup, 0, 4, stream));
+            hipLaunchKernelGGL(k_compress, dim3(grid_for(n, BT)), dim3(BT), 0, stream, A, n, A16, Abase, dup);
+            uint32_t span = 0;
+            HK(hipMemcpyAsync(&span, dup, 4, hipMemcpyDeviceToHost, stream));
+            HK(hipStreamSynchronize(stream));
+            if (span == 0) {   // every d <= 0xFFFF
+                HK(hipFree(A));
+                A = nullptr;
+                bytes += cb - uint64_t(n) * 4;
+            } else {
+                HK(hipFree(A16));
+                HK(hipFree(Abase));
+                A16 = nullptr;
+                Abase = nullptr;
+            }
+        }
         HK(hipMemsetAsync(padT + runs, 0, 4, stream));
         hipLaunchKernelGGL(k_chunk_tables, dim3(nc), dim3(BT), 0, stream, cnt, nc, nb, seg, off16, padT);
         HK(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb2, padT, ubT, int(runs + 1), stream));
@@ -538,14 +588,15 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol
             return e;
     }
     const dim3 gc(nc), gb(nb), blk(PT);
+    const AddrList al{A, A16, Abase};
     uint8_t *u8 = static_cast<uint8_t *>(U);
 #define DDT_SORTED_LAUNCH(E)                                                                              \
     if (dir == 0) {                                                                                       \
-        hipLaunchKernelGGL((k_pack1<E>), gc, blk, 0, stream, user, A, SL, off16, ub, u8, n, nb, pol);   \
+        hipLaunchKernelGGL((k_pack1<E>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);   \
         hipLaunchKernelGGL((k_pack2<E>), gb, blk, 0, stream, u8, upos, bstart, packed, n, pol);                \
     } else {                                                                                              \
         hipLaunchKernelGGL((k_unpack2<E>), gb, blk, 0, stream, packed, upos, bstart, u8, n, pol);              \
-        hipLaunchKernelGGL((k_unpack1<E>), gc, blk, 0, stream, user, A, SL, off16, ub, u8, n, nb, pol); \
+        hipLaunchKernelGGL((k_unpack1<E>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol); \
     }
     if (esz == 4) {
         DDT_SORTED_LAUNCH(4)

@@ -889,3 +889,15 @@ def test_sndrcv_matches_oracle(device):
     with pytest.raises(ompi_amd.DDTError) as ei:
         sndrcv(a, 2, t.engine(), b, 1, t.engine())
     assert ei.value.code == -9
+
+
+def test_sorted_list_engine_wide_groups(device, sorted_from):
+    """A 165 k-element hole inside one 64-element group of the address order: the engine keeps
+    its 32-bit offset form (the 16-bit group form needs spans < 64 Ki); bit-exact both ways."""
+    sorted_from(1)
+    rng = np.random.default_rng(41)
+    d = np.concatenate([np.arange(0, 35000), np.arange(200000, 235000)])
+    d = rng.permutation(d).astype(np.int64)
+    b = R.Built(("indexed_block", 1, d.tolist(), ("basic", 15)))
+    _roundtrip(b, 1, device, 19)
+    assert b.engine().engine_info()["sorted"] == 1
