@@ -50,6 +50,8 @@ template <> struct Elem<16> { using T = u32x4; };
 constexpr int PT = 1024;               // threads per pass workgroup (16 wave64)
 constexpr int BT = 256;                // threads per build workgroup
 constexpr uint32_t LDS_BYTES = 128u << 10;
+constexpr uint32_t SEG_BYTES = 64;     // U runs are padded to whole segments of this many bytes
+                                       // (32 B segments: less padding, but cfg4 1461 -> 1512 us)
 constexpr uint16_t PAD = 0xFFFF;       // upos of a padding slot
 
 // Access policy bits of one run (SortedList::run, ddt_tune("spol")):
@@ -251,7 +253,7 @@ __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, 
                                               uint32_t nb, uint32_t pol)
 {
     using T = typename Elem<E>::T;
-    constexpr uint32_t CH = LDS_BYTES / E, SEG = 64 / E;
+    constexpr uint32_t CH = LDS_BYTES / E, SEG = SEG_BYTES / E;
     const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS, ntu = pol & POL_USER_NTL;
     __shared__ T lds[CH + SEG];
     __shared__ uint16_t toff[MAXNB + 1];
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, cons
                                                 uint32_t n, uint32_t nb, uint32_t pol)
 {
     using T = typename Elem<E>::T;
-    constexpr uint32_t CH = LDS_BYTES / E, SEG = 64 / E, NSUB = PT / SEG;
+    constexpr uint32_t CH = LDS_BYTES / E, SEG = SEG_BYTES / E, NSUB = PT / SEG;
     const bool ntl = pol & POL_STREAM_NTL, wt = pol & POL_USER_WT;
     __shared__ T lds[CH];
     __shared__ uint16_t toff[MAXNB + 1];
@@ -479,7 +481,7 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
     n = n_;
     esz = esz_;
     ch = LDS_BYTES / esz;
-    seg = 64 / esz;
+    seg = SEG_BYTES / esz;
     nc = (n + ch - 1) / ch;
     nb = nc;   // RG == CH
     uint32_t shift = 0;
