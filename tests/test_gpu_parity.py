@@ -901,3 +901,33 @@ def test_sorted_list_engine_wide_groups(device, sorted_from):
     b = R.Built(("indexed_block", 1, d.tolist(), ("basic", 15)))
     _roundtrip(b, 1, device, 19)
     assert b.engine().engine_info()["sorted"] == 1
+
+
+@pytest.mark.parametrize("name", sorted(_corpus.CORPUS))
+def test_corpus_sndrcv_to_self(device, name):
+    """to_self.c:1538-1700 over the corpus (to_self.c:1814): a local send/recv of every corpus
+    type, received as MPI_PACKED (== the reference's by-hand stream, golden SHA-256), received
+    into the same type (typed copy) and sent back from MPI_PACKED."""
+    import torch
+    from ompi_amd.convertor import sndrcv
+    rec, _ = _corpus.CORPUS[name]()
+    b = R.Built(rec)
+    g = _GOLD[name]
+    count = g["count"]
+    info = b.o.info()
+    size = count * info["size"]
+    span, origin = R.layout(info, count)
+    host = R.fill(span, 0x5A)
+    user = _dev(host, device)
+    e = b.engine()
+    packed = torch.zeros(size, dtype=torch.uint8, device=device)
+    sndrcv(user.data_ptr() + origin, count, e, packed, size, None)
+    assert _hashlib.sha256(_host(packed).tobytes()).hexdigest() == g["sha256"]
+    if _overlapping(b.o, count):
+        return
+    exp = np.full(span, 0xA5, dtype=np.uint8)
+    b.o.unpack(count, exp, origin, 0, _host(packed).tobytes())
+    for src, stype in ((user.data_ptr() + origin, e), (packed.data_ptr(), None)):
+        out = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
+        sndrcv(src, count if stype else size, stype, out.data_ptr() + origin, count, e)
+        np.testing.assert_array_equal(_host(out), exp)
