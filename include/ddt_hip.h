@@ -280,8 +280,9 @@ int64_t ddt_type_plan_list(const ddt_datatype_t *type, size_t leaf, int64_t *dis
  * reorder items in runs of this many tasks (0 off); "wt" = write-through stores (-1 auto,
  * 0 off, 1 every sparse leaf, 2 all); "sorted" = address-ordered list engine (-1 auto from
  * 1 Mi blocks, 0 off, n > 0 from n blocks; read when a type's plan first runs);
- * "rev" = reverse task order (0 off, 1 unpack, 2 all); "spol" = the address-ordered engine's
- * access-policy bits (ddt_sorted.hip POL_*); "reset" = restore the defaults.
+ * "spol" = the address-ordered engine's
+ * access-policy bits (ddt_sorted.hip POL_*); "ptr" = launch reused descriptor sets by pointer
+ * (1, default) or always from the kernel-argument segment (0); "reset" = restore the defaults.
  * Environment: DDT_NT, DDT_TASK_KB, DDT_WT. */
 int ddt_tune(const char *key, long value);
 /* Library self-check of host-side index arithmetic (fast division); returns 0 on success. */

@@ -151,7 +151,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             if (P.cache.size() > kCacheEntries) {
                 // an evicted descriptor set may still be read by a launch in flight:
                 // park it, and free parked sets only after the device has drained
-                if (!P.cache.back()->inline_ok)
+                if (P.cache.back()->d_items)
                     P.graveyard.push_back(P.cache.back());
                 P.cache.pop_back();
                 drain = P.graveyard.size() > kCacheEntries;
@@ -165,12 +165,30 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     }
     if (S->items.empty())
         return DDT_SUCCESS;
-    const uint32_t rev = (tuning().rev == 2 || (tuning().rev == 1 && dir == 1)) ? 1u : 0u;
-    if (S->inline_ok) {
-        HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, rev, stream));
-    } else {
-        HIPCHK(launch_move(S->d_items, uint32_t(S->items.size()), S->ntasks, dir, S->has_lists, rev, stream));
+    // A descriptor set travels in the kernel-argument segment on its first launch (no upload
+    // for one-off windows).  From its second launch on it is launched by pointer from HBM:
+    // with device-resident kernel arguments every 64-byte line of arguments is a host write
+    // across PCIe, and a 528-byte block costs 2.6 us of host time per launch against 0.7 us
+    // for a pointer (scripts/hostbench.cpp, profiles/r1_hostbench.log).
+    Item *d_items = nullptr;
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        if (S->inline_ok && ++S->uses >= 2 && !S->d_items && tuning().ptr) {
+            size_t bytes = S->items.size() * sizeof(Item);
+            Item *d = nullptr;
+            if (hipMalloc((void **) &d, bytes) == hipSuccess) {
+                if (upload(d, S->items.data(), bytes) == hipSuccess)
+                    S->d_items = d;
+                else
+                    (void) hipFree(d);
+            }
+        }
+        d_items = (S->inline_ok && !tuning().ptr) ? nullptr : S->d_items;
     }
+    if (!d_items)
+        HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, stream));
+    else
+        HIPCHK(launch_move(d_items, uint32_t(S->items.size()), S->ntasks, dir, S->has_lists, stream));
     return DDT_SUCCESS;
 }
 
@@ -1124,10 +1142,10 @@ int ddt_tune(const char *key, long value)
         tuning().interleave = value;
     else if (k == "policy")
         tuning().policy = int(value);
+    else if (k == "ptr")
+        tuning().ptr = value ? 1 : 0;
     else if (k == "spol")
         tuning().spol = value;
-    else if (k == "rev")
-        tuning().rev = int(value);
     else if (k == "sorted")
         tuning().sorted = value;
     else if (k == "wt")

@@ -109,6 +109,8 @@ struct ItemSet {
     uint32_t ntasks = 0;
     bool has_lists = false;
     bool inline_ok = false;       // <= INLINE_ITEMS: launched from the kernarg segment
+    uint32_t uses = 0;            // launches so far; a reused inline set is uploaded once and
+                                  // launched by pointer (see run_windows)
     ItemBlock blk{};
     ~ItemSet();
 };

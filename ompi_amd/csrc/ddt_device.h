@@ -96,8 +96,7 @@ constexpr uint32_t INLINE_ITEMS = 7;
 template <uint32_t NI>
 struct ItemBlockN {
     uint32_t n;
-    uint32_t rev;           // 1: workgroups take tasks in reverse order (see launch_move)
-    uint32_t pad[2];
+    uint32_t pad[3];
     Item items[NI];
 };
 using ItemBlock = ItemBlockN<INLINE_ITEMS>;

@@ -391,9 +391,9 @@ __device__ __forceinline__ void dispatch_list_uni(const Item *it, uint32_t ub, u
 // LISTS = false: affine + fragment items only (vector/hvector/subarray/struct nests), a
 // lean register budget; LISTS = true adds the index-list paths.
 template <int DIR, bool LISTS>
-__device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32_t nitems, uint32_t rev)
+__device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32_t nitems)
 {
-    const uint32_t b = rev ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
+    const uint32_t b = blockIdx.x;
     uint32_t lo = 0, hi = nitems - 1;
     while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
@@ -455,10 +455,9 @@ __device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32
 }
 
 template <int DIR, bool LISTS>
-__global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restrict__ items, uint32_t nitems,
-                                                           uint32_t rev)
+__global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restrict__ items, uint32_t nitems)
 {
-    move_body<DIR, LISTS>(items, nitems, rev);
+    move_body<DIR, LISTS>(items, nitems);
 }
 
 // Small launches carry their descriptors in the kernel-argument segment: no device
@@ -470,15 +469,14 @@ __global__ __launch_bounds__(THREADS) void ddt_move_inline_kernel(ItemBlockN<NI>
     // would copy it to scratch)
     const ItemBlockN<NI> *kb = reinterpret_cast<const ItemBlockN<NI> *>(
         (const void *) __builtin_amdgcn_kernarg_segment_ptr());
-    move_body<DIR, LISTS>(kb->items, kb->n, kb->rev);
+    move_body<DIR, LISTS>(kb->items, kb->n);
 }
 
 template <int DIR, bool LISTS, uint32_t NI>
-static void launch_inline_n(const ItemBlock &blk, uint32_t ntasks, uint32_t rev, hipStream_t stream)
+static void launch_inline_n(const ItemBlock &blk, uint32_t ntasks, hipStream_t stream)
 {
     ItemBlockN<NI> b;
     b.n = blk.n;
-    b.rev = rev;
     for (uint32_t i = 0; i < blk.n; ++i)
         b.items[i] = blk.items[i];
     hipLaunchKernelGGL((ddt_move_inline_kernel<DIR, LISTS, NI>), dim3(ntasks), dim3(THREADS), 0,
@@ -486,50 +484,48 @@ static void launch_inline_n(const ItemBlock &blk, uint32_t ntasks, uint32_t rev,
 }
 
 template <int DIR, bool LISTS>
-static void launch_inline(const ItemBlock &blk, uint32_t ntasks, uint32_t rev, hipStream_t stream)
+static void launch_inline(const ItemBlock &blk, uint32_t ntasks, hipStream_t stream)
 {
-    if (blk.n == 1) launch_inline_n<DIR, LISTS, 1>(blk, ntasks, rev, stream);
-    else if (blk.n == 2) launch_inline_n<DIR, LISTS, 2>(blk, ntasks, rev, stream);
-    else if (blk.n <= 4) launch_inline_n<DIR, LISTS, 4>(blk, ntasks, rev, stream);
-    else launch_inline_n<DIR, LISTS, INLINE_ITEMS>(blk, ntasks, rev, stream);
+    if (blk.n == 1) launch_inline_n<DIR, LISTS, 1>(blk, ntasks, stream);
+    else if (blk.n == 2) launch_inline_n<DIR, LISTS, 2>(blk, ntasks, stream);
+    else if (blk.n <= 4) launch_inline_n<DIR, LISTS, 4>(blk, ntasks, stream);
+    else launch_inline_n<DIR, LISTS, INLINE_ITEMS>(blk, ntasks, stream);
 }
 
 template <int DIR>
-static void launch_dir(const Item *d_items, uint32_t nitems, uint32_t ntasks, bool lists, uint32_t rev,
-                       hipStream_t stream)
+static void launch_dir(const Item *d_items, uint32_t nitems, uint32_t ntasks, bool lists, hipStream_t stream)
 {
     if (lists)
         hipLaunchKernelGGL((ddt_move_kernel<DIR, true>), dim3(ntasks), dim3(THREADS), 0, stream,
-                           d_items, nitems, rev);
+                           d_items, nitems);
     else
         hipLaunchKernelGGL((ddt_move_kernel<DIR, false>), dim3(ntasks), dim3(THREADS), 0, stream,
-                           d_items, nitems, rev);
+                           d_items, nitems);
 }
 
-hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, uint32_t rev,
-                              hipStream_t stream)
+hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, hipStream_t stream)
 {
     if (ntasks == 0 || blk.n == 0)
         return hipSuccess;
     if (dir == 0) {
-        if (lists) launch_inline<0, true>(blk, ntasks, rev, stream);
-        else launch_inline<0, false>(blk, ntasks, rev, stream);
+        if (lists) launch_inline<0, true>(blk, ntasks, stream);
+        else launch_inline<0, false>(blk, ntasks, stream);
     } else {
-        if (lists) launch_inline<1, true>(blk, ntasks, rev, stream);
-        else launch_inline<1, false>(blk, ntasks, rev, stream);
+        if (lists) launch_inline<1, true>(blk, ntasks, stream);
+        else launch_inline<1, false>(blk, ntasks, stream);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
-                       uint32_t rev, hipStream_t stream)
+                       hipStream_t stream)
 {
     if (ntasks == 0 || nitems == 0)
         return hipSuccess;
     if (dir == 0)
-        launch_dir<0>(d_items, nitems, ntasks, lists, rev, stream);
+        launch_dir<0>(d_items, nitems, ntasks, lists, stream);
     else
-        launch_dir<1>(d_items, nitems, ntasks, lists, rev, stream);
+        launch_dir<1>(d_items, nitems, ntasks, lists, stream);
     return hipGetLastError();
 }
 

@@ -20,8 +20,8 @@ struct Tuning {
     int policy = 1;       // task sizing: 0 = v0 (~6 K tasks), 1 = per-leaf passes
     int wt = -1;          // write-through (sc1) stores: -1 auto, 0 off, 1 sparse user side, 2 all
     long sorted = -1;     // address-ordered list engine: -1 auto, 0 off, n > 0 from n blocks up
-    int rev = 0;          // reverse task order: 0 off, 1 unpack launches, 2 every launch
     long spol = 0;        // address-ordered engine access policy bits (ddt_sorted.hip POL_*)
+    int ptr = 1;          // 1: a reused inline descriptor set is launched by pointer; 0: always inline
 };
 Tuning &tuning();
 // Synchronous host -> device copy on a library-private stream (capture-safe).
@@ -36,11 +36,9 @@ SortedList *sorted_plan(const ddt_datatype *t, Plan &P, uint64_t user, hipStream
 uint32_t total_tasks(const std::vector<Item> &items);
 
 // ddt_kernels.hip: dir 0 = pack / typed copy (user side -> packed side), 1 = unpack.
-// rev = 1: workgroup b runs task ntasks-1-b (reverse dispatch order).
-hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, uint32_t rev,
-                              hipStream_t stream);
+hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, hipStream_t stream);
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
-                       uint32_t rev, hipStream_t stream);
+                       hipStream_t stream);
 
 // external32 conversion between a native packed stream and its big-endian form.
 hipError_t launch_ext(const ConvSeg *segs, uint32_t nseg, const ConvRun *runs, uint64_t E,

@@ -1,4 +1,5 @@
-# reverse task order A/B (ddt_tune rev) in the pack+unpack pair loop
+# reverse task order A/B (ddt_tune rev) in the pack+unpack pair loop.
+# Historical: the knob was removed after this A/B showed no gain (profiles/r1_rev_ab.log).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out

@@ -17,6 +17,8 @@
 #define HCHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s\n", hipGetErrorString(e)); exit(1); } } while (0)
 
 __global__ void nullptr_kernel() {}
+struct Arg528 { unsigned char b[528]; };
+__global__ void arg_kernel(Arg528 a) { if (a.b[0] == 255 && threadIdx.x == 999) a.b[1] = 0; }
 
 static double now_us()
 {
@@ -60,6 +62,48 @@ int main()
     }
     std::sort(t.begin(), t.end());
     printf("async enqueue median %.2f us/call\n", t[t.size() / 2]);
+    for (long ptr : {0L, 1L}) {   // reused descriptor set: kernel-argument block vs pointer
+        CHK(ddt_tune("ptr", ptr));
+        CHK(ddt_convertor_prepare_for_send(c, x, 1, user));
+        HCHK(hipStreamSynchronize(s));
+        std::vector<double> r;
+        for (int rep = 0; rep < 5; ++rep) {
+            double t0 = now_us();
+            for (int i = 0; i < iters; ++i) {
+                size_t pos = 0;
+                CHK(ddt_convertor_set_position(c, &pos));
+                struct iovec iov{packed, fs};
+                uint32_t cnt = 1;
+                size_t md = 0;
+                CHK(ddt_convertor_pack(c, &iov, &cnt, &md));
+            }
+            r.push_back((now_us() - t0) / iters);
+            HCHK(hipStreamSynchronize(s));
+        }
+        std::sort(r.begin(), r.end());
+        printf("repeated pack, descriptors %s: median %.2f us/call (host)\n",
+               ptr ? "by pointer" : "as kernel arguments", r[r.size() / 2]);
+    }
+    {   // the same pack with the convertor prepared once (set_position(0) per call)
+        CHK(ddt_convertor_prepare_for_send(c, x, 1, user));
+        HCHK(hipStreamSynchronize(s));
+        double t0 = now_us();
+        for (int i = 0; i < iters; ++i) {
+            size_t pos = 0;
+            CHK(ddt_convertor_set_position(c, &pos));
+            struct iovec iov{packed, fs};
+            uint32_t cnt = 1;
+            size_t md = 0;
+            CHK(ddt_convertor_pack(c, &iov, &cnt, &md));
+        }
+        double t1 = now_us();
+        HCHK(hipStreamSynchronize(s));
+        printf("async pack without prepare: %.2f us/call (host)\n", (t1 - t0) / iters);
+        t0 = now_us();
+        for (int i = 0; i < iters; ++i)
+            CHK(ddt_convertor_prepare_for_send(c, x, 1, user));
+        printf("prepare_for_send alone: %.3f us/call\n", (now_us() - t0) / iters);
+    }
     std::vector<double> w;
     for (int i = 0; i < 500; ++i) {
         size_t pos = 0;
@@ -84,6 +128,13 @@ int main()
         HCHK(hipStreamSynchronize(s));
         printf("empty kernel launch: %.3f us/call (host enqueue), %.3f us incl. drain\n", (t1 - t0) / m,
                (now_us() - t0) / m);
+        Arg528 arg{};
+        t0 = now_us();
+        for (int i = 0; i < m; ++i)
+            hipLaunchKernelGGL(arg_kernel, dim3(32), dim3(256), 0, s, arg);
+        t1 = now_us();
+        HCHK(hipStreamSynchronize(s));
+        printf("launch with a 528-byte argument: %.3f us/call (host enqueue)\n", (t1 - t0) / m);
     }
     ddt_convertor_destroy(c);
     ddt_type_destroy(&x);
