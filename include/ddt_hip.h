@@ -36,6 +36,7 @@ extern "C" {
 #define DDT_ERR_HIP (-8)            /* a HIP runtime call failed */
 #define DDT_ERR_TRUNCATE (-9)       /* MPI_ERR_TRUNCATE analogue for ddt_pack/ddt_unpack */
 #define DDT_ERR_NOT_SUPPORTED (-10)
+#define DDT_ERR_VALUE_OUT_OF_BOUNDS (-11) /* MPI_Get_elements: the bytes end inside an element */
 
 /* ---- predefined type ids: identical to OPAL_DATATYPE_* (opal_datatype_internal.h:71-99) ---- */
 #define DDT_INT1 4
@@ -253,6 +254,12 @@ int ddt_copy_content_same_ddt(const ddt_datatype_t *type, size_t count, void *ds
  * DDT_ERR_TRUNCATE cases are the reference's. */
 int ddt_sndrcv(const void *sbuf, size_t scount, const ddt_datatype_t *stype, void *rbuf, size_t rcount,
                const ddt_datatype_t *rtype, void *hip_stream);
+/* ompi_datatype_get_elements (ompi/datatype/ompi_datatype_get_elements.c:30-76, MPI_Get_elements):
+ * basic elements in the first `ucount` packed bytes of a message of this type; whole instances
+ * count every element of the type map, a leftover is counted by opal_datatype_get_element_count's
+ * walk (opal_datatype_get_count.c:32-92).  DDT_ERR_VALUE_OUT_OF_BOUNDS when the bytes end inside
+ * an element (MPI_UNDEFINED). */
+int ddt_get_elements(const ddt_datatype_t *type, size_t ucount, size_t *count);
 /* Plan introspection for tests/benchmarks: number of leaves, device metadata bytes. */
 int ddt_type_plan_info(const ddt_datatype_t *type, int64_t *out4);
 /* Which engine whole-message moves of this type use: out4 = [state, device bytes, chunks,

@@ -1025,6 +1025,90 @@ int ddt_type_get_true_extent(const ddt_datatype_t *t, ptrdiff_t *true_lb, ptrdif
 
 uint32_t ddt_type_flags(const ddt_datatype_t *t) { return t ? t->flags : 0; }
 
+namespace {
+// Basic elements of one instance of a node list (the uncommitted description: every element
+// keeps its own type size, like opal_datatype_compute_ptypes over desc).
+uint64_t elements_of(const std::vector<Node> &nodes)
+{
+    uint64_t e = 0;
+    for (const Node &n : nodes) {
+        if (n.kind == Node::DATA)
+            e += n.count * (n.blen / uint64_t(n.esize));
+        else if (n.kind == Node::LOOP)
+            e += n.count * elements_of(n.body);
+        else if (n.list)
+            e += n.list->total / uint64_t(n.esize);
+    }
+    return e;
+}
+
+// opal_datatype_get_element_count (opal_datatype_get_count.c:32-92): elements within the first
+// `left` packed bytes of one instance, walking the type map in order; -1 when the budget ends
+// inside an element.  *done is set once the budget is used up.
+int64_t count_within(const std::vector<Node> &nodes, uint64_t &left, bool &done)
+{
+    int64_t acc = 0;
+    for (const Node &n : nodes) {
+        if (n.kind == Node::LOOP) {
+            if (n.body_size == 0)
+                continue;
+            const uint64_t total = n.count * n.body_size;
+            const uint64_t be = elements_of(n.body);
+            if (total < left) {   // whole loop
+                acc += int64_t(n.count * be);
+                left -= total;
+                continue;
+            }
+            const uint64_t full = left == 0 ? 0 : (left - 1) / n.body_size;   // iterations before the last
+            acc += int64_t(full * be);
+            left -= full * n.body_size;
+            const int64_t r = count_within(n.body, left, done);
+            return r < 0 ? -1 : acc + r;
+        }
+        const uint64_t bytes = n.packed_bytes();
+        const uint64_t es = uint64_t(n.esize);
+        if (bytes >= left) {   // the budget ends in this entry (opal_datatype_get_count.c:81-86)
+            done = true;
+            const uint64_t k = left / es;
+            const bool whole = left == k * es;
+            left = 0;
+            return whole ? acc + int64_t(k) : -1;
+        }
+        acc += int64_t(bytes / es);
+        left -= bytes;
+    }
+    return acc;
+}
+}  // namespace
+
+int ddt_get_elements(const ddt_datatype_t *t, size_t ucount, size_t *count)
+{
+    // ompi_datatype_get_elements (ompi/datatype/ompi_datatype_get_elements.c:30-76)
+    if (!t || !count)
+        return DDT_ERR_BAD_PARAM;
+    *count = 0;
+    const uint64_t size = uint64_t(t->size);
+    if (size == 0)
+        return DDT_SUCCESS;
+    uint64_t full = ucount / size, left = ucount - full * size;
+    if (is_predefined(t)) {
+        if (left)
+            return DDT_ERR_VALUE_OUT_OF_BOUNDS;
+        *count = size_t(full);
+        return DDT_SUCCESS;
+    }
+    uint64_t n = full ? full * elements_of(t->desc) : 0;
+    if (left) {
+        bool done = false;
+        const int64_t r = count_within(t->desc, left, done);
+        if (r < 0)
+            return DDT_ERR_VALUE_OUT_OF_BOUNDS;
+        n += uint64_t(r);
+    }
+    *count = size_t(n);
+    return DDT_SUCCESS;
+}
+
 int ddt_type_info(const ddt_datatype_t *t, int64_t *o)
 {
     if (!t || !o)

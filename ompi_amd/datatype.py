@@ -100,6 +100,16 @@ class Datatype:
         check(lib().ddt_type_plan_info(self.handle, out), "ddt_type_plan_info")
         return dict(zip(("leaves", "device_bytes", "list_leaves", "max_dims"), list(out)))
 
+    def get_elements(self, ucount: int):
+        """MPI_Get_elements (ompi_datatype_get_elements): basic elements in `ucount` packed
+        bytes, or None (MPI_UNDEFINED) when the bytes end inside an element."""
+        n = ctypes.c_size_t()
+        rc = lib().ddt_get_elements(self.handle, ucount, ctypes.byref(n))
+        if rc == -11:
+            return None
+        check(rc, "ddt_get_elements")
+        return int(n.value)
+
     def engine_info(self) -> dict:
         """State of the address-ordered index-list engine (ddt_type_engine_info)."""
         out = (ctypes.c_int64 * 4)()

@@ -191,3 +191,46 @@ def test_reference_resized_extent_bounds():
     got = np.frombuffer(b.o.pack(2, user, 0, 0, 24, element_granular=True), dtype=np.uint8)
     want = np.concatenate([user[p:p + 4] for p in range(0, 36, 6)])
     np.testing.assert_array_equal(got, want)
+
+
+def _oracle_get_elements(o, ucount):
+    """ompi_datatype_get_elements restated on the oracle's type map (runs of whole basic
+    elements of one size, in type-map order): whole instances count every element; the
+    leftover walks the runs and is MPI_UNDEFINED (None) if it ends inside an element."""
+    info = o.info()
+    size = info["size"]
+    if size == 0:
+        return 0
+    runs = o.runs()
+    per = sum(n // e for _, n, e in runs)
+    full, left = divmod(ucount, size)
+    acc = full * per
+    if left:
+        for _, n, e in runs:
+            if n >= left:
+                return acc + left // e if left % e == 0 else None
+            acc += n // e
+            left -= n
+    return acc
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_get_elements_matches_oracle(seed):
+    """MPI_Get_elements (ompi_datatype_get_elements.c:30-76 with opal_datatype_get_count.c:32-92)
+    on fuzzed types and byte counts, against the oracle's type map."""
+    rng = random.Random(700 + seed)
+    for _ in range(150):
+        b = R.Built(R.random_recipe(rng))
+        size = b.o.info()["size"]
+        e = b.engine()
+        for uc in {0, size, 3 * size, rng.randrange(0, 4 * size + 9), rng.randrange(0, size + 1) + size}:
+            assert e.get_elements(uc) == _oracle_get_elements(b.o, uc), (b.recipe, uc)
+
+
+def test_get_elements_known_answers():
+    from ompi_amd import datatype as D
+    st = D.create_struct([1, 3], [0, 8], [D.MPI.MPI_DOUBLE, D.MPI.MPI_INT]).commit()   # size 20
+    assert st.get_elements(60) == 12 and st.get_elements(68) == 13 and st.get_elements(70) is None
+    v = D.create_vector(3, 2, 4, D.MPI.MPI_DOUBLE).commit()                              # size 48
+    assert v.get_elements(24) == 3 and v.get_elements(48 * 5) == 30 and v.get_elements(20) is None
+    assert D.MPI.MPI_INT.get_elements(12) == 3 and D.MPI.MPI_INT.get_elements(6) is None
