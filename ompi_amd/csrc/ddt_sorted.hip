@@ -1,6 +1,6 @@
-// ddt_sorted.hip -- address-ordered two-pass engine for large single-element index lists
-// (MPI_Type_indexed / create_indexed_block / hindexed with one basic element per block,
-// BASELINE config 4: 64 Mi random floats out of a 1 GiB buffer).
+// ddt_sorted.hip -- address-ordered two-pass engine for large small-block index lists
+// (MPI_Type_indexed / create_indexed_block / hindexed whose blocks are a few elements of
+// 4, 8 or 16 bytes; BASELINE config 4: 64 Mi random floats out of a 1 GiB buffer).
 //
 // The direct list kernel (ddt_kernels.hip, run_list_uni) issues one memory request per
 // element: a random 4-byte gather over a span far beyond the Infinity Cache runs at the
@@ -20,8 +20,8 @@
 // store is a whole segment.  CH = RG = 128 KiB / element size, so the LDS image of a
 // chunk or a bucket is 128 KiB (gfx950: 160 KiB per CU).  The plan (A, SL, run tables,
 // upos) is built once on the device from the list's displacements: a bitmap of the
-// touched elements gives each block its address rank by popcount, and duplicate
-// displacements make the list ineligible (the direct kernel then keeps type-map order).
+// touched elements gives each element its address rank by popcount, and a repeated element
+// makes the list ineligible (the direct kernel then keeps type-map order).
 //
 // This replaces, for such lists, the per-block cbmemcpy loop of
 // opal_pack_accelerator_simple / opal_unpack_accelerator_simple
@@ -30,7 +30,6 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
-#include <cstdio>
 #include <stdexcept>
 #include <string>
 
