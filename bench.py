@@ -223,6 +223,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--faces", action="store_true", help="also time each face type alone")
     ap.add_argument("--no-graph", action="store_true", help="skip the HIP-graph replay measurement")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the single-face latency probe (profiling runs: one workload per trace)")
     args = ap.parse_args()
 
     import torch
@@ -371,7 +373,7 @@ def main():
                 "frac": round(ops / (tp + tu) / rq["ceiling_requests_per_s"], 4),
                 "source": f"profiles/requests_{args.config}.json"}
 
-    if rank == 0 and args.config == "cfg2":
+    if rank == 0 and args.config == "cfg2" and not args.no_latency:
         result["single_face_latency_us"] = single_face_latency(dev, stream, user, origin)
 
     if args.faces and rank == 0:

@@ -21,6 +21,14 @@ import csv
 import json
 import sys
 
+
+def family(kernel_name):
+    """ddt_move_kernel / ddt_move_inline_kernel (either launch form) = one family per step."""
+    for f in ("k_pack1", "k_pack2", "k_unpack1", "k_unpack2"):
+        if f in kernel_name:
+            return f
+    return "move"
+
 CEILING = 61.7e9   # requests/s of a 16 B/lane streaming copy (copy16, ubench4)
 
 
@@ -35,9 +43,10 @@ def main():
             d = "pack" if "k_pack" in k else "unpack"
         else:
             continue
-        acc[(d, k, r["Counter_Name"])].append(float(r["Counter_Value"]))
-    # per kernel: mean over its dispatches; per direction: sum over its kernels (the
-    # address-ordered list engine runs two kernels per direction)
+        acc[(d, family(k), r["Counter_Name"])].append(float(r["Counter_Value"]))
+    # per kernel family: mean over its dispatches; per direction: sum over its families (the
+    # address-ordered list engine runs two kernels per direction).  The move kernel's
+    # kernel-argument and by-pointer launches are one family: one of them runs per step.
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     for (d, _, ctr), v in acc.items():
         per[d][ctr] += sum(v) / len(v)

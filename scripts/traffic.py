@@ -19,6 +19,14 @@ import json
 import sys
 
 
+def family(kernel_name):
+    """ddt_move_kernel / ddt_move_inline_kernel (either launch form) = one family per step."""
+    for f in ("k_pack1", "k_pack2", "k_unpack1", "k_unpack2"):
+        if f in kernel_name:
+            return f
+    return "move"
+
+
 def per_kernel(path, counter):
     """Per direction: the sum over its kernels of each kernel's mean per dispatch (the
     address-ordered list engine runs two kernels per pack and per unpack)."""
@@ -33,7 +41,7 @@ def per_kernel(path, counter):
             direction = "pack" if "k_pack" in k else "unpack"
         else:
             continue
-        acc[(direction, k)].append(float(r["Counter_Value"]) * 1024.0)
+        acc[(direction, family(k))].append(float(r["Counter_Value"]) * 1024.0)
     out, n = collections.defaultdict(float), collections.defaultdict(int)
     for (d, _), v in acc.items():
         out[d] += sum(v) / len(v)
