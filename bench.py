@@ -236,11 +236,12 @@ def main():
     # backend "nccl" is RCCL on ROCm; DDT_BENCH_BACKEND=gloo rehearses the multi-rank path
     # with several ranks sharing one GPU (code-path check only, not a scaling number)
     backend = os.environ.get("DDT_BENCH_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
-    if world > 1:
-        dist.init_process_group(backend=backend)
     local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        # bind the RCCL communicator to this rank's GPU up front (no device guess in barrier())
+        dist.init_process_group(backend=backend, **({"device_id": dev} if backend == "nccl" else {}))
 
     import ompi_amd
     from ompi_amd import recipe as ER
