@@ -289,8 +289,11 @@ int64_t ddt_type_plan_list(const ddt_datatype_t *type, size_t leaf, int64_t *dis
  * 1 Mi blocks, 0 off, n > 0 from n blocks; read when a type's plan first runs);
  * "spol" = the address-ordered engine's
  * access-policy bits (ddt_sorted.hip POL_*); "ptr" = launch reused descriptor sets by pointer
- * (1, default) or always from the kernel-argument segment (0); "reset" = restore the defaults.
- * Environment: DDT_NT, DDT_TASK_KB, DDT_WT. */
+ * (1, default) or always from the kernel-argument segment (0); "xcd" = mapping of workgroups to
+ * tasks (-1, default: each XCD runs a contiguous slab of a streaming or line-dense leaf, sparse
+ * gathers stay round-robin; 0: all round-robin; 1: all slabs);
+ * "reset" = restore the defaults.
+ * Environment: DDT_NT, DDT_TASK_KB, DDT_WT, DDT_XCD. */
 int ddt_tune(const char *key, long value);
 /* Library self-check of host-side index arithmetic (fast division); returns 0 on success. */
 int ddt_selftest(void);

@@ -86,7 +86,8 @@ struct Item {
     uint64_t nbytes;        // FRAG: bytes
     uint32_t wt;            // store policy: 1 = user-side stores (unpack) write through L2 (sc1);
                             // 2 = every store of the launch sc1
-    uint32_t pad2;          // keeps sizeof(Item) == 512
+    uint32_t slab;          // 1: this item's tasks are mapped XCD-contiguous (move_body);
+                            // keeps sizeof(Item) == 512
 };
 
 // Descriptors passed by value in the kernel-argument segment (<= 4 KiB).

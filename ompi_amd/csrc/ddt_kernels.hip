@@ -401,7 +401,14 @@ __device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32
         else hi = mid - 1;
     }
     const Item *it = items + lo;
-    const uint64_t t = b - it->task_begin;
+    uint32_t t = b - it->task_begin;
+    if (it->slab) {
+        // Workgroups are dispatched round-robin over the 8 XCDs, so the item's local task t
+        // runs on XCD (task_begin + t) % 8.  Give each XCD one contiguous slab of the item's
+        // tasks instead of every 8th one (a bijection on [0, ntasks)).
+        const uint32_t T = it->ntasks, x = t & 7u, i = t >> 3, per = T >> 3, rem = T & 7u;
+        t = x * per + (x < rem ? x : rem) + i;
+    }
     const uint64_t ub = it->u0 + t * it->units_per_task;
     uint64_t ue = ub + it->units_per_task;
     if (ue > it->u1) ue = it->u1;

@@ -30,6 +30,8 @@ Tuning &tuning()
             v.task_kb = std::atol(e);
         if (const char *e = std::getenv("DDT_WT"))
             v.wt = std::atoi(e);
+        if (const char *e = std::getenv("DDT_XCD"))
+            v.xcd = std::atoi(e) < 0 ? -1 : (std::atoi(e) ? 1 : 0);
         return v;
     }();
     return t;
@@ -736,6 +738,25 @@ void assign_tasks(std::vector<Item> &items)
         it.ntasks = uint32_t(nt);
         b += uint32_t(nt);
     }
+}
+
+bool use_slab(const Item &it)
+{
+    if (it.kind != ITEM_AFFINE && it.kind != ITEM_LIST_UNI)
+        return false;
+    if (tuning().xcd >= 0)
+        return tuning().xcd == 1;
+    // Measured per access class (scripts/gpu_xcd_ab.sh, profiles/r1_xcd_ab.log): streams and
+    // line-dense records (cfg5: 20 B of every 32 B) run faster when each XCD owns one
+    // contiguous slab; sparse gathers (one element per line: x faces) and index lists run
+    // faster spread round-robin over all XCDs.
+    if (it.kind != ITEM_AFFINE)
+        return false;
+    const uint64_t blk = it.upb * it.U;
+    if (blk >= 64 || it.ndim == 0)
+        return true;
+    const uint64_t stride = uint64_t(it.ustr[it.ndim - 1] < 0 ? -it.ustr[it.ndim - 1] : it.ustr[it.ndim - 1]);
+    return stride < 2 * blk;
 }
 
 uint32_t total_tasks(const std::vector<Item> &items)

@@ -22,6 +22,7 @@ struct Tuning {
     long sorted = -1;     // address-ordered list engine: -1 auto, 0 off, n > 0 from n blocks up
     long spol = 0;        // address-ordered engine access policy bits (ddt_sorted.hip POL_*)
     int ptr = 1;          // 1: a reused inline descriptor set is launched by pointer; 0: always inline
+    int xcd = -1;         // XCD-contiguous task slabs: -1 auto (line-dense affine items), 0 off, 1 all
 };
 Tuning &tuning();
 // Synchronous host -> device copy on a library-private stream (capture-safe).
@@ -33,6 +34,8 @@ void assign_tasks(std::vector<Item> &items);
 // The address-ordered engine of plan P for a whole-message pack/unpack, built on first use;
 // null when the plan does not qualify (or `user` is misaligned for it).
 SortedList *sorted_plan(const ddt_datatype *t, Plan &P, uint64_t user, hipStream_t stream);
+// XCD-contiguous task mapping for this item (Item::slab; tuning().xcd)
+bool use_slab(const Item &it);
 uint32_t total_tasks(const std::vector<Item> &items);
 
 // ddt_kernels.hip: dir 0 = pack / typed copy (user side -> packed side), 1 = unpack.

@@ -37,7 +37,7 @@ class Item(ctypes.Structure):
         ("ldisp32", ctypes.c_uint32), ("leaf", ctypes.c_uint32),
         ("same", ctypes.c_uint32), ("nt", ctypes.c_uint32),
         ("w0", ctypes.c_int64), ("w1", ctypes.c_int64), ("nbytes", ctypes.c_uint64),
-        ("wt", ctypes.c_uint32), ("pad2", ctypes.c_uint32),
+        ("wt", ctypes.c_uint32), ("slab", ctypes.c_uint32),
     ]
 
 
