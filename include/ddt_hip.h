@@ -291,7 +291,8 @@ int64_t ddt_type_plan_list(const ddt_datatype_t *type, size_t leaf, int64_t *dis
  * access-policy bits (ddt_sorted.hip POL_*); "ptr" = launch reused descriptor sets by pointer
  * (1, default) or always from the kernel-argument segment (0); "xcd" = mapping of workgroups to
  * tasks (-1, default: each XCD runs a contiguous slab of a streaming or line-dense leaf, sparse
- * gathers stay round-robin; 0: all round-robin; 1: all slabs);
+ * gathers stay round-robin; 0: all round-robin; 1: all slabs); "xchunk" = tasks per XCD run for
+ * slab items (0, default: one slab per XCD);
  * "reset" = restore the defaults.
  * Environment: DDT_NT, DDT_TASK_KB, DDT_WT, DDT_XCD. */
 int ddt_tune(const char *key, long value);

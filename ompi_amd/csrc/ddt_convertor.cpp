@@ -129,7 +129,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         assign_tasks(S->items);
         S->ntasks = total_tasks(S->items);
         for (Item &it : S->items)
-            it.slab = use_slab(it) ? 1 : 0;
+            it.slab = use_slab(it) ? (tuning().xchunk > 0 ? uint32_t(tuning().xchunk) : SLAB_FULL) : 0;
         for (const Item &it : S->items)
             S->has_lists = S->has_lists || it.kind == ITEM_LIST_UNI || it.kind == ITEM_LIST_VAR;
         if (S->items.size() <= INLINE_ITEMS) {
@@ -1146,6 +1146,8 @@ int ddt_tune(const char *key, long value)
         tuning().policy = int(value);
     else if (k == "ptr")
         tuning().ptr = value ? 1 : 0;
+    else if (k == "xchunk")
+        tuning().xchunk = value < 0 ? 0 : value;
     else if (k == "xcd")
         tuning().xcd = value < 0 ? -1 : (value ? 1 : 0);
     else if (k == "spol")

@@ -14,6 +14,7 @@ namespace ddt {
 
 constexpr int MAXD = 8;             // affine dims per item, instance dim included
 constexpr int THREADS = 256;        // workgroup size (4 wave64)
+constexpr uint32_t SLAB_FULL = 0xffffffffu;
 // units each thread loads before storing, per pass of the affine loop
 constexpr int unroll_of(uint32_t U) { return U >= 16 ? 4 : 8; }
 
@@ -86,7 +87,8 @@ struct Item {
     uint64_t nbytes;        // FRAG: bytes
     uint32_t wt;            // store policy: 1 = user-side stores (unpack) write through L2 (sc1);
                             // 2 = every store of the launch sc1
-    uint32_t slab;          // 1: this item's tasks are mapped XCD-contiguous (move_body);
+    uint32_t slab;          // XCD task mapping (move_body): 0 round-robin, SLAB_FULL one
+                            // contiguous slab per XCD, else runs of `slab` tasks per XCD;
                             // keeps sizeof(Item) == 512
 };
 

@@ -406,8 +406,18 @@ __device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32
         // Workgroups are dispatched round-robin over the 8 XCDs, so the item's local task t
         // runs on XCD (task_begin + t) % 8.  Give each XCD one contiguous slab of the item's
         // tasks instead of every 8th one (a bijection on [0, ntasks)).
-        const uint32_t T = it->ntasks, x = t & 7u, i = t >> 3, per = T >> 3, rem = T & 7u;
-        t = x * per + (x < rem ? x : rem) + i;
+        const uint32_t T = it->ntasks;
+        if (it->slab == SLAB_FULL) {
+            const uint32_t x = t & 7u, i = t >> 3, per = T >> 3, rem = T & 7u;
+            t = x * per + (x < rem ? x : rem) + i;
+        } else {
+            // runs of C tasks per XCD inside groups of 8C (the tail stays round-robin)
+            const uint32_t C = it->slab, G = C * 8u;
+            if (t < T - T % G) {
+                const uint32_t r = t % G;
+                t = t - r + (r & 7u) * C + (r >> 3);
+            }
+        }
     }
     const uint64_t ub = it->u0 + t * it->units_per_task;
     uint64_t ue = ub + it->units_per_task;

@@ -23,6 +23,7 @@ struct Tuning {
     long spol = 0;        // address-ordered engine access policy bits (ddt_sorted.hip POL_*)
     int ptr = 1;          // 1: a reused inline descriptor set is launched by pointer; 0: always inline
     int xcd = -1;         // XCD-contiguous task slabs: -1 auto (line-dense affine items), 0 off, 1 all
+    long xchunk = 0;      // tasks per XCD run for slab items: 0 = one slab per XCD
 };
 Tuning &tuning();
 // Synchronous host -> device copy on a library-private stream (capture-safe).
