@@ -37,7 +37,13 @@ def main():
     faces["xx"] = ("resized", ("struct", [1, 1], [0, (n - 1) * 8], [xf, xf]), 0, field)
     faces["yz"] = ("resized", ("struct", [1, 1, 1, 1], [0, (n - 1) * n * 8, 0, (n - 1) * n * n * 8],
                                [yf, yf, faces["z"][1], faces["z"][1]]), 0, field)
-    if args.config in faces:
+    n3, f3 = 512, 512 ** 3 * 4
+    for i, (sub, st) in enumerate((([1, n3, n3], [n3 - 1, 0, 0]), ([n3, 1, n3], [0, n3 - 1, 0]),
+                                   ([n3, n3, 1], [0, 0, n3 - 1]))):
+        faces[f"c3d{i}"] = ("resized", ("subarray", [n3] * 3, sub, st, 0, ("basic", 15)), 0, f3)
+    if args.config.startswith("c3d"):
+        recipe, count = faces[args.config], 8
+    elif args.config in faces:
         recipe, count = faces[args.config], 16
     else:
         recipe, count, _ = bench.make_workload(args.config)
