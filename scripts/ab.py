@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--mode", default="pair", choices=["pair", "pack", "unpack"],
                     help="pair = pack then unpack per step; pack/unpack = that direction only")
+    ap.add_argument("--unpack-rev", action="store_true",
+                    help="timing only: unpack with a type that writes the same bytes in reverse order "
+                         "(fields, faces and rows reversed; xx and cfg2), to test Infinity Cache reuse")
     ap.add_argument("--prewarm", type=float, default=0.0, help="seconds of HBM copies first")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -47,6 +50,21 @@ def main():
         recipe, count = faces[args.config], 16
     else:
         recipe, count, _ = bench.make_workload(args.config)
+    rev_recipe = None
+    if args.unpack_rev:
+        d8 = ("basic", 16)
+        xr = ("hvector", n * n, 1, -n * 8, d8)                       # x face, rows last to first
+        yr = ("hvector", n, n, -n * n * 8, d8)                       # y face, planes last to first
+        zr = ("contig", n * n, d8)
+        last_row = (n * n - 1) * n * 8
+        if args.config == "xx":
+            one = ("struct", [1, 1], [(n - 1) * 8 + last_row, last_row], [xr, xr])
+        else:
+            lp = (n - 1) * n * n * 8
+            one = ("struct", [1] * 6,
+                   [(n - 1) * n * n * 8, 0, (n - 1) * n * 8 + lp, lp, (n - 1) * 8 + last_row, last_row],
+                   [zr, zr, yr, yr, xr, xr])
+        rev_recipe = ("struct", [1], [15 * field], [("hvector", 16, 1, -field, one)])
     variants = [dict(kv.split("=") for kv in v.split(";")) for v in args.variants.split(",")]
     probe = ER.build_committed(recipe)
     info = probe.info()
@@ -72,6 +90,9 @@ def main():
             for k, val in v.items():
                 L.ddt_tune(k.encode(), int(val))
             dt = ER.build_committed(recipe)
+            udt, ucount = (ER.build_committed(rev_recipe), 1) if rev_recipe else (dt, count)
+            if rev_recipe:
+                assert udt.info()["size"] == S
             cp, cu = ompi_amd.Convertor(), ompi_amd.Convertor()
             st = torch.cuda.current_stream(dev)
             cp.set_stream(st, True)
@@ -85,7 +106,7 @@ def main():
                     cp.pack([(packed, S)])
                 b.record()
                 if args.mode != "pack":
-                    cu.prepare_for_recv(dt, count, uptr)
+                    cu.prepare_for_recv(udt, ucount, uptr)
                     cu.unpack([(packed, S)])
                 c.record()
                 if i >= 3:
