@@ -931,3 +931,26 @@ def test_corpus_sndrcv_to_self(device, name):
         out = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
         sndrcv(src, count if stype else size, stype, out.data_ptr() + origin, count, e)
         np.testing.assert_array_equal(_host(out), exp)
+
+
+@pytest.mark.parametrize("xcd,xchunk", [(0, 0), (1, 0), (1, 3), (1, 16), (-1, 0)])
+def test_xcd_task_mappings(device, xcd, xchunk):
+    """Every workgroup -> task mapping (ddt_tune "xcd" / "xchunk": round-robin, one slab per
+    XCD, runs of 3 and 16 tasks with a round-robin tail, the default rule) moves the same
+    bytes.  Launches of hundreds of tasks per item, so slabs, runs and tails all occur."""
+    import ompi_amd
+    L = ompi_amd.lib()
+    recipes = [
+        ("hvector", 60000, 1, 32, ("struct", [1, 3], [0, 8], [("basic", 16), ("basic", 6)])),  # cfg5-like
+        ("vector", 4099, 1, 256, ("basic", 16)),                                                 # x-face-like
+        ("struct", [1, 1, 1], [0, 1 << 20, 2 << 20],
+         [("vector", 3001, 1, 64, ("basic", 15)), ("contig", 50000, ("basic", 16)),
+          ("vector", 300, 37, 80, ("basic", 6))]),
+    ]
+    try:
+        L.ddt_tune(b"xcd", xcd)
+        L.ddt_tune(b"xchunk", xchunk)
+        for i, rec in enumerate(recipes):
+            _roundtrip(R.Built(rec), 3, device, 77 + i)
+    finally:
+        L.ddt_tune(b"reset", 0)
