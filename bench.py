@@ -235,6 +235,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # backend "nccl" is RCCL on ROCm; DDT_BENCH_BACKEND=gloo rehearses the multi-rank path
     # with several ranks sharing one GPU (code-path check only, not a scaling number)
+    if args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N > 1 with "
+              "python -m torch.distributed.run --nproc-per-node N (reporting n_gpus = WORLD_SIZE)",
+              file=sys.stderr)
     backend = os.environ.get("DDT_BENCH_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
     local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
