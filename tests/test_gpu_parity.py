@@ -106,7 +106,8 @@ def test_fuzz_full_message(device, seed):
 def test_fuzz_fragments(device, frags):
     """opt_desc_equiv.c:63 fragment matrix {12, 16, 40, 4096} + a ragged trace."""
     rng = random.Random(hash(tuple(frags)) & 0xffff)
-    for n in range(25):
+    # DDT_FUZZ_FRAG_TYPES widens the sweep for soak runs (default 25 random types per trace)
+    for n in range(int(__import__("os").environ.get("DDT_FUZZ_FRAG_TYPES", "25"))):
         b = R.Built(R.random_recipe(rng))
         _roundtrip(b, rng.choice([1, 3, 7]), device, n, frags=frags)
 
