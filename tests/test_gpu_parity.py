@@ -140,6 +140,46 @@ def test_out_of_order_unpack(device):
     np.testing.assert_array_equal(_host(out), exp)
 
 
+@pytest.mark.parametrize("seed", range(int(__import__("os").environ.get("DDT_FUZZ_OOO_SEEDS", "3"))))
+def test_fuzz_out_of_order_windows(device, seed):
+    """unpack_ooo.c / pml_ucx_datatype.c:72-123 on random types: the packed stream is cut at
+    random byte offsets (mid-element included), each window is packed with pack_window and
+    unpacked through set_position, in shuffled order; every byte == oracle."""
+    import torch
+    import ompi_amd
+    from ompi_amd import convertor as C
+    rng = random.Random(5000 + seed)
+    for n in range(40):
+        b = R.Built(R.random_recipe(rng))
+        count = rng.choice([1, 2, 5])
+        info = b.o.info()
+        size = info["size"] * count
+        if size == 0 or _overlapping(b.o, count):
+            continue
+        span, origin = R.layout(info, count)
+        host = R.fill(span, seed * 100 + n)
+        user = _dev(host, device)
+        e = b.engine()
+        ref = np.frombuffer(b.o.pack(count, host, origin, 0, size, element_granular=False), dtype=np.uint8)
+        cuts = sorted(set([0, size] + [rng.randint(1, size - 1) for _ in range(min(12, size - 1))]))
+        segs = list(zip(cuts[:-1], cuts[1:]))
+        rng.shuffle(segs)
+        packed = torch.zeros(size, dtype=torch.uint8, device=device)
+        for a, z in segs:
+            got = C.pack_window(e, count, user.data_ptr() + origin, a, packed.data_ptr() + a, z - a)
+            assert got == z - a
+        np.testing.assert_array_equal(_host(packed), ref)
+        out = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
+        conv = ompi_amd.Convertor().prepare_for_recv(e, count, out.data_ptr() + origin)
+        rng.shuffle(segs)
+        for a, z in segs:
+            assert conv.set_position(a) == a
+            conv.unpack([(packed.data_ptr() + a, z - a)])
+        exp = np.full(span, 0xA5, dtype=np.uint8)
+        b.o.unpack(count, exp, origin, 0, ref.tobytes())
+        np.testing.assert_array_equal(_host(out), exp)
+
+
 def test_multi_iovec_and_host_iovec(device):
     """Several iovecs per call; host (pageable) packed buffers go through HBM staging."""
     import torch
