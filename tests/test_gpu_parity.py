@@ -102,6 +102,45 @@ def test_fuzz_full_message(device, seed):
         _roundtrip(b, rng.choice([1, 2, 3, 7]), device, seed * 100 + n)
 
 
+@pytest.mark.parametrize("seed", range(int(__import__("os").environ.get("DDT_FUZZ_BIG_SEEDS", "2"))))
+def test_fuzz_large_counts(device, seed):
+    """Random types repeated to 0.5-4 MiB of packed data (thousands of instances), so the
+    launch is cut into many tasks and workgroups: whole-message pack == oracle; unpack into
+    0xA5 == oracle whenever the count instances touch disjoint bytes (checked by unpacking an
+    all-0xFF stream into zeros with the oracle and counting the bytes set)."""
+    import torch
+    import ompi_amd
+    rng = random.Random(9000 + seed)
+    done = 0
+    while done < 8:
+        b = R.Built(R.random_recipe(rng))
+        info = b.o.info()
+        if info["size"] == 0:
+            continue
+        target = rng.choice([1 << 19, 1 << 20, 1 << 22])
+        count = max(1, min(target // info["size"], 1 << 20))
+        span, origin = R.layout(info, count)
+        if span > (64 << 20):
+            continue
+        size = info["size"] * count
+        host = R.fill(span, seed * 31 + done)
+        user = _dev(host, device)
+        e = b.engine()
+        ref = np.frombuffer(b.o.pack_all(count, host, origin), dtype=np.uint8)
+        packed = torch.zeros(size, dtype=torch.uint8, device=device)
+        assert ompi_amd.pack(user.data_ptr() + origin, count, e, packed, size, 0) == size
+        np.testing.assert_array_equal(_host(packed), ref)
+        touched = np.zeros(span, dtype=np.uint8)
+        b.o.unpack(count, touched, origin, 0, b"\xff" * size)
+        if int(np.count_nonzero(touched)) == size:
+            out = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
+            ompi_amd.unpack(packed, size, 0, out.data_ptr() + origin, count, e)
+            exp = np.full(span, 0xA5, dtype=np.uint8)
+            b.o.unpack(count, exp, origin, 0, ref.tobytes())
+            np.testing.assert_array_equal(_host(out), exp)
+        done += 1
+
+
 @pytest.mark.parametrize("frags", [[12], [16], [40], [4096], [7, 33, 1000]])
 def test_fuzz_fragments(device, frags):
     """opt_desc_equiv.c:63 fragment matrix {12, 16, 40, 4096} + a ragged trace."""
