@@ -48,12 +48,12 @@ def _worker(rank, world, port, q):
         from tests import recipes as R
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        # 32^3 float subarray face stack (BASELINE config 3 shape, scaled), 6 fields
+        # 32^3 float subarray face stack (BASELINE config 3 shape, scaled), 7 fields
         rec = ("resized", ("subarray", [32, 32, 32], [32, 32, 1], [0, 0, 31], 0, ("basic", 15)),
                0, 32 ** 3 * 4)
         b = R.Built(rec)
         info = b.o.info()
-        count = 6
+        count = 7   # uneven split over 2 and 3 ranks
         span, origin = R.layout(info, count)
         host = R.fill(span, 42)
         first, n, uoff, poff = shard.shard_of(count, info["size"], info["ub"] - info["lb"], rank, world)
@@ -68,12 +68,13 @@ def _worker(rank, world, port, q):
         q.put(repr(ex))
 
 
-def test_gather_of_shards_equals_whole_message_gloo():
+@pytest.mark.parametrize("world", [2, 3])   # 3 ranks: uneven count split
+def test_gather_of_shards_equals_whole_message_gloo(world):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
