@@ -1,4 +1,4 @@
-"""Multi-rank sharding on CPU: world_size 2 with the gloo backend.
+"""Multi-rank sharding on CPU: world_size 2 and 3 with the gloo backend.
 
 Each rank packs its instance range of one message (here with the CPU oracle, the
 checker -- the GPU engine is exercised by the same shard arithmetic in bench.py), the
