@@ -404,7 +404,8 @@ def test_external32_matches_oracle(device, host_ext):
     import ompi_amd
     rng = random.Random(8100 + int(host_ext))
     tested = 0
-    for n in range(70):
+    # DDT_FUZZ_EXT_TYPES widens the sweep for soak runs (default 70 random types)
+    for n in range(int(__import__("os").environ.get("DDT_FUZZ_EXT_TYPES", "70"))):
         b = R.Built(R.random_recipe(rng, basics=R.EXT_BASICS))
         info = b.o.info()
         count = rng.choice([1, 2, 4])
