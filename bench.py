@@ -223,6 +223,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--faces", action="store_true", help="also time each face type alone")
     ap.add_argument("--no-graph", action="store_true", help="skip the HIP-graph replay measurement")
+    ap.add_argument("--event-every", type=int, default=10,
+                    help="bracket every Nth timed step with HIP events (kernel durations)")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-face latency probe (profiling runs: one workload per trace)")
     args = ap.parse_args()
@@ -294,19 +296,27 @@ def main():
         pack()
         unpack()
 
+    every = max(1, args.event_every)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+           torch.cuda.Event(enable_timing=True)) if i % every == 0 else None
+          for i in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for e0, e1, e2 in ev:
+    for es in ev:
+        if es is None:
+            pack()
+            unpack()
+            continue
+        e0, e1, e2 = es
         e0.record(stream)
         pack()
         e1.record(stream)
         unpack()
         e2.record(stream)
     torch.cuda.synchronize()
+    ev = [es for es in ev if es is not None]
     wall = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([wall], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
