@@ -298,8 +298,8 @@ def main():
 
     every = max(1, args.event_every)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) if i % every == 0 else None
-          for i in range(args.steps)]
+           torch.cuda.Event(enable_timing=True)) if (args.steps - 1 - i) % every == 0 else None
+          for i in range(args.steps)]   # counted from the last step: step 0 (host enqueue lag) is skipped
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
