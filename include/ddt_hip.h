@@ -267,6 +267,10 @@ int ddt_type_plan_info(const ddt_datatype_t *type, int64_t *out4);
  * use, 0 = not tried yet (built at the first whole-message pack/unpack), -1 = not applicable
  * (the per-block list kernel runs). */
 int ddt_type_engine_info(const ddt_datatype_t *type, int64_t *out4);
+/* Descriptor-set cache of a type's plan: out4 = [cached sets, evicted sets waiting for their
+ * retirement events, sets held for captured graphs, HIP device of the plan (-1 before first
+ * use)].  Sets are keyed by the request's shape and pointer alignment, not by buffer address. */
+int ddt_type_cache_info(const ddt_datatype_t *type, int64_t *out4);
 /* ---- introspection for the CPU test-suite (no data movement; never used by pack/unpack) ----
  * ddt_type_plan_leaves: serialises the plan's leaf streams as int64 records
  *   [kind, blen, src_off, dst_off, ndim, list_leaf_index, (cnt, sstr, dstr) x ndim] and returns

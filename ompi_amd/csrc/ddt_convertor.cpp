@@ -62,23 +62,113 @@ struct Window {
 };
 
 constexpr size_t kCacheEntries = 32;
+constexpr size_t kRetiredMax = 64;
 constexpr uint64_t kStageChunk = 16ull << 20;   // host staging pipeline chunk
 
+bool capturing(hipStream_t s)
+{
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess) {
+        (void) hipGetLastError();
+        return true;   // unknown: treat as captured (the safe side: keep the memory)
+    }
+    return cs != hipStreamCaptureStatusNone;
+}
+
+// Free retired descriptor sets whose eviction events every launching stream has passed.
+// With `block` (never inside a capture), wait for the oldest until at most kRetiredMax
+// remain: a host wait on those streams' events, not a device-wide synchronisation.
+void reap(Plan &P, bool block)   // P.mu held
+{
+    for (size_t i = 0; i < P.graveyard.size();) {
+        bool done = true;
+        for (hipEvent_t e : P.graveyard[i].events) {
+            if (hipEventQuery(e) != hipSuccess) {
+                (void) hipGetLastError();   // hipErrorNotReady must not look like a launch error
+                done = false;
+                break;
+            }
+        }
+        if (!done) {
+            ++i;
+            continue;
+        }
+        for (hipEvent_t e : P.graveyard[i].events)
+            (void) hipEventDestroy(e);
+        P.graveyard.erase(P.graveyard.begin() + long(i));
+    }
+    while (block && P.graveyard.size() > kRetiredMax) {
+        for (hipEvent_t e : P.graveyard.front().events) {
+            (void) hipEventSynchronize(e);
+            (void) hipEventDestroy(e);
+        }
+        P.graveyard.erase(P.graveyard.begin());
+    }
+}
+
+// An evicted set's device descriptors may still be read by launches in flight: record an
+// event behind them on every stream that launched the set, free it once they pass.  A set
+// a captured graph holds (or whose stream cannot take an event) lives as long as the plan.
+void retire(Plan &P, const std::shared_ptr<ItemSet> &S)   // P.mu held
+{
+    if (!S->d_items)
+        return;
+    if (S->pinned) {
+        P.pinned.push_back(S);
+        return;
+    }
+    Retired r{S, {}};
+    for (hipStream_t st : S->streams) {
+        hipEvent_t e = nullptr;
+        if (capturing(st) || hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess
+            || hipEventRecord(e, st) != hipSuccess) {
+            (void) hipGetLastError();
+            if (e)
+                (void) hipEventDestroy(e);
+            for (hipEvent_t x : r.events)
+                (void) hipEventDestroy(x);
+            P.pinned.push_back(S);
+            return;
+        }
+        r.events.push_back(e);
+    }
+    P.graveyard.push_back(std::move(r));
+}
+
 // Find or build the descriptor set of one launch and run it on `stream`.
+//
+// Descriptor sets are independent of the absolute buffers: items address the user side
+// relative to ubase = user rounded down to 16 bytes and the packed side relative to pbase
+// (the first window's pointer rounded down), and the cache key holds only the low four
+// bits of the pointers (all a unit-size choice depends on) plus the windows' shape.  A
+// double-buffered halo, a fragment stream or the staging slots of a host pipeline hit the
+// same set whatever buffers they use.
 int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                 const std::vector<Window> &wins, bool same_layout, int dir, hipStream_t stream)
 {
     if (wins.empty())
         return DDT_SUCCESS;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        if (P.device < 0)
+            P.device = dev;
+    }
+    if (P.device != dev)
+        return fail(DDT_ERR_NOT_SUPPORTED, "datatype plan lives on device " + std::to_string(P.device)
+                                               + "; current device is " + std::to_string(dev)
+                                               + " (one device per committed datatype)");
+    const uint64_t ubase = user & ~uint64_t(15), pbase = wins[0].ptr & ~uint64_t(15);
     std::vector<uint64_t> key;
     key.reserve(4 + 3 * wins.size());
     key.push_back(count);
-    key.push_back(user);
+    key.push_back(user - ubase);
     key.push_back(same_layout ? 1 : 0);
     for (const Window &w : wins) {
         key.push_back(w.w0);
         key.push_back(w.w1);
-        key.push_back(w.ptr);
+        key.push_back(w.ptr - pbase);
     }
     try {
         ensure_device_lists(P);
@@ -122,7 +212,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         S->key = key;
         try {
             for (const Window &w : wins)
-                build_items(t, P, count, user, w.ptr, w.w0, w.w1, same_layout, S->items);
+                build_items(t, P, count, user - ubase, w.ptr - pbase, w.w0, w.w1, same_layout, S->items);
         } catch (const std::exception &ex) {
             return fail(DDT_ERR_NOT_SUPPORTED, ex.what());
         }
@@ -146,24 +236,14 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             if (e != hipSuccess)
                 return fail(DDT_ERR_HIP, std::string("item upload: ") + hipGetErrorString(e));
         }
-        bool drain = false;
-        {
-            std::lock_guard<std::mutex> g(P.mu);
-            P.cache.insert(P.cache.begin(), S);
-            if (P.cache.size() > kCacheEntries) {
-                // an evicted descriptor set may still be read by a launch in flight:
-                // park it, and free parked sets only after the device has drained
-                if (P.cache.back()->d_items)
-                    P.graveyard.push_back(P.cache.back());
-                P.cache.pop_back();
-                drain = P.graveyard.size() > kCacheEntries;
-            }
+        const bool block = !capturing(stream);
+        std::lock_guard<std::mutex> g(P.mu);
+        P.cache.insert(P.cache.begin(), S);
+        if (P.cache.size() > kCacheEntries) {
+            retire(P, P.cache.back());
+            P.cache.pop_back();
         }
-        if (drain) {
-            HIPCHK(hipDeviceSynchronize());
-            std::lock_guard<std::mutex> g(P.mu);
-            P.graveyard.clear();
-        }
+        reap(P, block);
     }
     if (S->items.empty())
         return DDT_SUCCESS;
@@ -186,11 +266,18 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             }
         }
         d_items = (S->inline_ok && !tuning().ptr) ? nullptr : S->d_items;
+        if (d_items) {
+            if (capturing(stream))
+                S->pinned = true;   // the graph keeps this pointer: never free before the plan
+            if (std::find(S->streams.begin(), S->streams.end(), stream) == S->streams.end())
+                S->streams.push_back(stream);
+        }
     }
     if (!d_items)
-        HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, stream));
+        HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, ubase, pbase, stream));
     else
-        HIPCHK(launch_move(d_items, uint32_t(S->items.size()), S->ntasks, dir, S->has_lists, stream));
+        HIPCHK(launch_move(d_items, uint32_t(S->items.size()), S->ntasks, dir, S->has_lists, ubase, pbase,
+                           stream));
     return DDT_SUCCESS;
 }
 
@@ -208,10 +295,16 @@ struct ddt_convertor {
     uint64_t bConverted = 0;
     hipStream_t stream = nullptr;
     bool async = false;
-    // host-iovec staging pipeline (two HBM slots, one copy stream)
+    // host-iovec staging pipeline (two HBM slots, one copy stream).  The slot state lives
+    // with the convertor, not with one call: a slot is written only after the last reader
+    // of its previous contents -- the D2H copy of a pack (ev_c) or the kernel of an unpack
+    // (ev_k), possibly queued by an earlier asynchronous call on another stream -- has
+    // passed (pml_ob1_recvreq.c:627-663 issues such back-to-back async unpacks).
     void *stage[2] = {nullptr, nullptr};
     hipStream_t copy_stream = nullptr;
     hipEvent_t ev_k[2] = {nullptr, nullptr}, ev_c[2] = {nullptr, nullptr};
+    bool rec_k[2] = {false, false}, rec_c[2] = {false, false};
+    uint32_t next_slot = 0;
     ~ddt_convertor()
     {
         if (stream)
@@ -221,6 +314,7 @@ struct ddt_convertor {
             (void) hipStreamDestroy(copy_stream);
         }
         for (int i = 0; i < 2; ++i) {
+            if (ev_k[i] && rec_k[i]) (void) hipEventSynchronize(ev_k[i]);
             if (stage[i]) (void) hipFree(stage[i]);
             if (ev_k[i]) (void) hipEventDestroy(ev_k[i]);
             if (ev_c[i]) (void) hipEventDestroy(ev_c[i]);
@@ -238,9 +332,26 @@ struct ddt_convertor {
         }
         return DDT_SUCCESS;
     }
+    // make `writer` wait until slot s may be overwritten
+    int slot_free_on(int s, hipStream_t writer)
+    {
+        if (rec_k[s])
+            HIPCHK(hipStreamWaitEvent(writer, ev_k[s], 0));
+        if (rec_c[s])
+            HIPCHK(hipStreamWaitEvent(writer, ev_c[s], 0));
+        return DDT_SUCCESS;
+    }
 };
 
 namespace {
+
+// Chunk schedule of a staged window: a short first chunk (the copy engine starts while
+// the first kernel is still short), then full slots.
+uint64_t stage_chunk(uint64_t done, uint64_t left)
+{
+    const uint64_t want = done == 0 ? (kStageChunk >> 3) : kStageChunk;
+    return std::min<uint64_t>(want, left);
+}
 
 // Move the packed windows of a convertor call: device iovecs in one launch, host iovecs
 // through the HBM staging pipeline (kernel on the user stream, copies on copy_stream).
@@ -253,39 +364,44 @@ int execute(ddt_convertor *c, const std::vector<Window> &dev_wins,
     if (!host_wins.empty()) {
         if ((rc = c->ensure_staging()) != DDT_SUCCESS)
             return rc;
-        int k = 0;
-        bool used[2] = {false, false};
+        bool last[2] = {false, false};
         for (const auto &hw : host_wins) {
-            for (uint64_t off = hw.first.w0; off < hw.first.w1; off += kStageChunk, ++k) {
-                const int s = k & 1;
-                const uint64_t n = std::min<uint64_t>(kStageChunk, hw.first.w1 - off);
+            for (uint64_t off = hw.first.w0; off < hw.first.w1;) {
+                const int s = int(c->next_slot++ & 1u);
+                const uint64_t n = stage_chunk(off - hw.first.w0, hw.first.w1 - off);
                 char *hp = static_cast<char *>(hw.second) + (off - hw.first.w0);
                 std::vector<Window> w{{off, off + n, uint64_t(uintptr_t(c->stage[s]))}};
                 if (dir == 0) {   // pack: kernel -> D2H
-                    if (used[s])
-                        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_c[s], 0));
+                    if ((rc = c->slot_free_on(s, c->stream)))
+                        return rc;
                     if ((rc = run_windows(c->dt, *c->plan, c->count, c->base, w, false, 0, c->stream)))
                         return rc;
                     HIPCHK(hipEventRecord(c->ev_k[s], c->stream));
+                    c->rec_k[s] = true;
                     HIPCHK(hipStreamWaitEvent(c->copy_stream, c->ev_k[s], 0));
                     HIPCHK(hipMemcpyAsync(hp, c->stage[s], n, hipMemcpyDeviceToHost, c->copy_stream));
                     HIPCHK(hipEventRecord(c->ev_c[s], c->copy_stream));
+                    c->rec_c[s] = true;
                 } else {          // unpack: H2D -> kernel
-                    if (used[s])
-                        HIPCHK(hipStreamWaitEvent(c->copy_stream, c->ev_k[s], 0));
+                    if ((rc = c->slot_free_on(s, c->copy_stream)))
+                        return rc;
                     HIPCHK(hipMemcpyAsync(c->stage[s], hp, n, hipMemcpyHostToDevice, c->copy_stream));
                     HIPCHK(hipEventRecord(c->ev_c[s], c->copy_stream));
+                    c->rec_c[s] = true;
                     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_c[s], 0));
                     if ((rc = run_windows(c->dt, *c->plan, c->count, c->base, w, false, 1, c->stream)))
                         return rc;
                     HIPCHK(hipEventRecord(c->ev_k[s], c->stream));
+                    c->rec_k[s] = true;
                 }
-                used[s] = true;
+                last[s] = true;
+                off += n;
             }
         }
-        // the user stream observes completion of the last copies
+        // the user stream observes completion of this call's copies (an event the caller
+        // records on it after the call covers the whole message)
         for (int s = 0; s < 2; ++s)
-            if (used[s])
+            if (last[s] && dir == 0)
                 HIPCHK(hipStreamWaitEvent(c->stream, c->ev_c[s], 0));
     }
     if (!c->async)
@@ -788,9 +904,12 @@ int ddt_sndrcv(const void *sbuf, size_t scount, const ddt_datatype_t *st, void *
 // ---------------------------------------------------------------- external32
 namespace {
 
+// Scratch of one external32 call from the stream-ordered pool of the null stream: no
+// hipMalloc / hipFree (and their device synchronisation) per call.
 struct DevBuf {
     void *p = nullptr;
-    ~DevBuf() { if (p) (void) hipFree(p); }
+    hipError_t alloc(size_t n) { return hipMallocAsync(&p, n ? n : 1, nullptr); }
+    ~DevBuf() { if (p) (void) hipFreeAsync(p, nullptr); }
 };
 
 int ext_plan_for(const ddt_datatype_t *t, std::shared_ptr<ExtPlan> &X)
@@ -842,7 +961,7 @@ int ddt_pack_external(const char *datarep, const void *inbuf, size_t incount,
     if ((rc = ext_upload(*X)) != DDT_SUCCESS)
         return fail(rc, "external32 table upload");
     DevBuf tn, te;
-    HIPCHK(hipMalloc(&tn.p, native));
+    HIPCHK(tn.alloc(native));
     ddt_convertor c;
     if ((rc = prepare(&c, t, incount, inbuf, true)) != DDT_SUCCESS)
         return rc;
@@ -854,7 +973,7 @@ int ddt_pack_external(const char *datarep, const void *inbuf, size_t incount,
     char *dst = static_cast<char *>(outbuf) + *position;
     const bool dev_out = classify(dst) == MEM_DEVICE;
     if (!dev_out)
-        HIPCHK(hipMalloc(&te.p, need));
+        HIPCHK(te.alloc(need));
     HIPCHK(launch_ext(X->d_segs, uint32_t(X->segs.size()), X->d_runs, X->E, incount,
                       uint64_t(t->size), X->Se, tn.p, dev_out ? dst : te.p, 0, nullptr));
     if (!dev_out)
@@ -889,10 +1008,10 @@ int ddt_unpack_external(const char *datarep, const void *inbuf, ptrdiff_t insize
     DevBuf tn, te;
     const bool dev_in = classify(src) == MEM_DEVICE;
     if (!dev_in) {
-        HIPCHK(hipMalloc(&te.p, need));
+        HIPCHK(te.alloc(need));
         HIPCHK(hipMemcpy(te.p, src, need, hipMemcpyHostToDevice));
     }
-    HIPCHK(hipMalloc(&tn.p, native));
+    HIPCHK(tn.alloc(native));
     HIPCHK(launch_ext(X->d_segs, uint32_t(X->segs.size()), X->d_runs, X->E, outcount,
                       uint64_t(t->size), X->Se, tn.p, dev_in ? const_cast<char *>(src) : te.p, 1,
                       nullptr));
@@ -995,6 +1114,27 @@ int ddt_type_engine_info(const ddt_datatype_t *t, int64_t *out4)
     out4[1] = P->sorted ? int64_t(P->sorted->dev_bytes) : 0;
     out4[2] = P->sorted ? int64_t(P->sorted->nc) : 0;
     out4[3] = P->sorted ? int64_t(P->sorted->slots) : 0;
+    return DDT_SUCCESS;
+}
+
+int ddt_type_cache_info(const ddt_datatype_t *t, int64_t *out4)
+{
+    if (!t || !out4)
+        return DDT_ERR_BAD_PARAM;
+    if (!(t->flags & F_COMMITTED))
+        return fail(DDT_ERR_NOT_COMMITTED, "datatype not committed");
+    std::shared_ptr<Plan> P;
+    try {
+        P = get_plan(const_cast<ddt_datatype *>(t));
+    } catch (const std::exception &ex) {
+        return fail(DDT_ERR_OUT_OF_RESOURCE, ex.what());
+    }
+    std::lock_guard<std::mutex> g(P->mu);
+    reap(*P, false);
+    out4[0] = int64_t(P->cache.size());
+    out4[1] = int64_t(P->graveyard.size());
+    out4[2] = int64_t(P->pinned.size());
+    out4[3] = P->device;
     return DDT_SUCCESS;
 }
 

@@ -102,6 +102,9 @@ struct DevList {                  // device copy of an IndexList
 // Launch descriptors of one (count, buffers, windows) request, resident in HBM.
 // Repeated requests (the halo-exchange pattern: same type, same buffers every
 // iteration) reuse them with no host work and no upload.
+// Items hold addresses relative to the launch's two bases (16-byte aligned), so the key is
+// the request's shape and alignment only: a double-buffered halo, a staged pipeline's HBM
+// slots or a PML fragment stream reuse one set across buffers.
 struct ItemSet {
     std::vector<uint64_t> key;
     std::vector<Item> items;
@@ -111,8 +114,18 @@ struct ItemSet {
     bool inline_ok = false;       // <= INLINE_ITEMS: launched from the kernarg segment
     uint32_t uses = 0;            // launches so far; a reused inline set is uploaded once and
                                   // launched by pointer (see run_windows)
+    bool pinned = false;          // launched by pointer inside a stream capture: a graph holds
+                                  // d_items, so it lives as long as the plan
+    std::vector<hipStream_t> streams;  // streams that launched d_items (retirement events)
     ItemBlock blk{};
     ~ItemSet();
+};
+
+// An evicted descriptor set waits here until every stream that launched it has passed the
+// event recorded at eviction (no device-wide synchronisation).
+struct Retired {
+    std::shared_ptr<ItemSet> set;
+    std::vector<hipEvent_t> events;
 };
 
 struct ExtPlan;
@@ -123,8 +136,10 @@ struct Plan {
     uint64_t dev_bytes = 0;       // device metadata bytes
     bool dev_ready = false;       // index lists uploaded
     std::mutex mu;
+    int device = -1;              // HIP device holding this plan's device state (first use)
     std::vector<std::shared_ptr<ItemSet>> cache;      // most recent first
-    std::vector<std::shared_ptr<ItemSet>> graveyard;  // evicted, freed after a device drain
+    std::vector<Retired> graveyard;                   // evicted, freed once their events pass
+    std::vector<std::shared_ptr<ItemSet>> pinned;     // evicted but held by captured graphs
     // address-ordered plan of a one-leaf single-element index list (ddt_sorted.hip):
     // 0 = not tried yet, 1 = built, -1 = not applicable
     int sorted_state = 0;

@@ -66,8 +66,8 @@ struct Item {
     uint32_t ntasks;
     uint64_t upb;           // units per block (affine / list-uniform)
     FastDiv fd_upb;
-    uint64_t user;          // user-side base address (uintptr)
-    uint64_t packed;        // packed-side base address (uintptr)
+    uint64_t user;          // user-side address, relative to the launch's user base
+    uint64_t packed;        // packed-side address, relative to the launch's packed base
     uint64_t cnt[MAXD];
     FastDiv fd[MAXD];
     int64_t ustr[MAXD];     // user-side stride per dim (bytes)
@@ -99,7 +99,9 @@ constexpr uint32_t INLINE_ITEMS = 7;
 template <uint32_t NI>
 struct ItemBlockN {
     uint32_t n;
-    uint32_t pad[3];
+    uint32_t pad;
+    uint64_t ubase, pbase;  // the launch's base pointers (Item::user / Item::packed are relative)
+    uint64_t pad2;
     Item items[NI];
 };
 using ItemBlock = ItemBlockN<INLINE_ITEMS>;

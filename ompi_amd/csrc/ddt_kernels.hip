@@ -91,11 +91,17 @@ __device__ __forceinline__ void nest_offsets64(const Item *it, uint64_t blk, int
 
 template <int U> constexpr int unroll() { return unroll_of(U); }
 
+// Item::user / Item::packed are offsets from the launch's two base pointers (Bases), so one
+// descriptor set serves every buffer pair with the same 16-byte alignment (ddt_convertor.cpp).
+struct Bases {
+    uint64_t u, p;
+};
+
 template <int U, int DIR>
-__device__ __noinline__ void run_affine64(const Item *it, uint64_t ub, uint64_t ue)
+__device__ __noinline__ void run_affine64(const Item *it, Bases bs, uint64_t ub, uint64_t ue)
 {
     using T = typename Vec<U>::T;
-    const uint64_t user = it->user, packed = it->packed, upb = it->upb;
+    const uint64_t user = bs.u + it->user, packed = bs.p + it->packed, upb = it->upb;
     for (uint64_t u = ub + threadIdx.x; u < ue; u += THREADS) {
         uint64_t blk = u / upb, within = u - blk * upb;
         int64_t uo = int64_t(within) * U, po = uo;
@@ -141,11 +147,11 @@ template <typename T, bool WT> __device__ __forceinline__ void st(T *p, T v)
 }
 
 template <int U, int DIR, int ND, bool NT, bool WT>
-__device__ __forceinline__ void run_affine(const Item *it, uint32_t ub, uint32_t ue)
+__device__ __forceinline__ void run_affine(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
 {
     using T = typename Vec<U>::T;
     constexpr int K = unroll<U>();
-    const uint64_t user = it->user, packed = it->packed;
+    const uint64_t user = bs.u + it->user, packed = bs.p + it->packed;
     Nest<ND> n;
     load_nest(it, n);
     const FastDiv fdu = it->fd_upb;
@@ -175,10 +181,10 @@ __device__ __forceinline__ void run_affine(const Item *it, uint32_t ub, uint32_t
 }
 
 template <int U, int DIR>
-__device__ __noinline__ void run_list_uni64(const Item *it, uint64_t ub, uint64_t ue)
+__device__ __noinline__ void run_list_uni64(const Item *it, Bases bs, uint64_t ub, uint64_t ue)
 {
     using T = typename Vec<U>::T;
-    const uint64_t user = it->user, packed = it->packed, ulen = it->ulen;
+    const uint64_t user = bs.u + it->user, packed = bs.p + it->packed, ulen = it->ulen;
     const bool d32 = it->ldisp32 != 0;
     const int32_t *disp32 = reinterpret_cast<const int32_t *>(it->ldisp);
     const int64_t *disp64 = reinterpret_cast<const int64_t *>(it->ldisp);
@@ -201,11 +207,11 @@ __device__ __noinline__ void run_list_uni64(const Item *it, uint64_t ub, uint64_
 // (coalesced) before the K dependent gathers, so each round pays two memory latencies
 // instead of 2K.
 template <int U, int DIR, bool WT>
-__device__ __forceinline__ void run_list_uni(const Item *it, uint32_t ub, uint32_t ue)
+__device__ __forceinline__ void run_list_uni(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
 {
     using T = typename Vec<U>::T;
     constexpr int K = unroll<U>();
-    const uint64_t user = it->user, packed = it->packed;
+    const uint64_t user = bs.u + it->user, packed = bs.p + it->packed;
     const uint64_t ulen = it->ulen;
     const bool d32 = it->ldisp32 != 0;
     const bool same = it->same != 0;
@@ -277,10 +283,10 @@ __device__ __forceinline__ void copy_bytes_aligned(uint8_t *dst, const uint8_t *
 // come from the per-group base (plan time) plus a wave-level exclusive prefix scan of
 // the 64 block lengths, so no per-block packed offset is stored in HBM.
 template <int DIR>
-__device__ __forceinline__ void run_list_var(const Item *it, uint64_t ub, uint64_t ue)
+__device__ __forceinline__ void run_list_var(const Item *it, Bases bs, uint64_t ub, uint64_t ue)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t user = it->user, packed = it->packed;
+    const uint64_t user = bs.u + it->user, packed = bs.p + it->packed;
     const uint32_t *len = reinterpret_cast<const uint32_t *>(it->llen);
     const uint64_t *goff = reinterpret_cast<const uint64_t *>(it->lgoff);
     const bool d32 = it->ldisp32 != 0;
@@ -319,10 +325,10 @@ __device__ __forceinline__ void run_list_var(const Item *it, uint64_t ub, uint64
 // Deep nests (> 4 dims) are rare: their dims are re-read from the (cached) item on every
 // unit instead of being held in registers, which keeps the kernel's SGPR budget small.
 template <int U, int DIR, bool NT, bool WT>
-__device__ __forceinline__ void run_affine_deep(const Item *it, uint32_t ub, uint32_t ue)
+__device__ __forceinline__ void run_affine_deep(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
 {
     using T = typename Vec<U>::T;
-    const uint64_t user = it->user, packed = it->packed;
+    const uint64_t user = bs.u + it->user, packed = bs.p + it->packed;
     const FastDiv fdu = it->fd_upb;
     const uint32_t upb = uint32_t(it->upb);
     const int nd = int(it->ndim);
@@ -346,26 +352,26 @@ __device__ __forceinline__ void run_affine_deep(const Item *it, uint32_t ub, uin
 }
 
 template <int U, int DIR, bool NT, bool WT>
-__device__ __forceinline__ void dispatch_affine_u(const Item *it, uint32_t ub, uint32_t ue)
+__device__ __forceinline__ void dispatch_affine_u(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
 {
     switch (it->ndim) {
-    case 1: run_affine<U, DIR, 1, NT, WT>(it, ub, ue); break;
-    case 2: run_affine<U, DIR, 2, NT, WT>(it, ub, ue); break;
-    case 3: run_affine<U, DIR, 3, NT, WT>(it, ub, ue); break;
-    case 4: run_affine<U, DIR, 4, NT, WT>(it, ub, ue); break;
-    default: run_affine_deep<U, DIR, NT, WT>(it, ub, ue); break;
+    case 1: run_affine<U, DIR, 1, NT, WT>(it, bs, ub, ue); break;
+    case 2: run_affine<U, DIR, 2, NT, WT>(it, bs, ub, ue); break;
+    case 3: run_affine<U, DIR, 3, NT, WT>(it, bs, ub, ue); break;
+    case 4: run_affine<U, DIR, 4, NT, WT>(it, bs, ub, ue); break;
+    default: run_affine_deep<U, DIR, NT, WT>(it, bs, ub, ue); break;
     }
 }
 
 template <int DIR, bool NT, bool WT>
-__device__ __forceinline__ void dispatch_affine(const Item *it, uint32_t ub, uint32_t ue)
+__device__ __forceinline__ void dispatch_affine(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
 {
     switch (it->U) {
-    case 16: dispatch_affine_u<16, DIR, NT, WT>(it, ub, ue); break;
-    case 8: dispatch_affine_u<8, DIR, NT, WT>(it, ub, ue); break;
-    case 4: dispatch_affine_u<4, DIR, NT, WT>(it, ub, ue); break;
-    case 2: dispatch_affine_u<2, DIR, NT, WT>(it, ub, ue); break;
-    default: dispatch_affine_u<1, DIR, NT, WT>(it, ub, ue); break;
+    case 16: dispatch_affine_u<16, DIR, NT, WT>(it, bs, ub, ue); break;
+    case 8: dispatch_affine_u<8, DIR, NT, WT>(it, bs, ub, ue); break;
+    case 4: dispatch_affine_u<4, DIR, NT, WT>(it, bs, ub, ue); break;
+    case 2: dispatch_affine_u<2, DIR, NT, WT>(it, bs, ub, ue); break;
+    default: dispatch_affine_u<1, DIR, NT, WT>(it, bs, ub, ue); break;
     }
 }
 
@@ -377,21 +383,21 @@ __device__ __forceinline__ bool wt_stores(const Item *it)
 }
 
 template <int DIR, bool WT>
-__device__ __forceinline__ void dispatch_list_uni(const Item *it, uint32_t ub, uint32_t ue)
+__device__ __forceinline__ void dispatch_list_uni(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
 {
     switch (it->U) {
-    case 16: run_list_uni<16, DIR, WT>(it, ub, ue); break;
-    case 8: run_list_uni<8, DIR, WT>(it, ub, ue); break;
-    case 4: run_list_uni<4, DIR, WT>(it, ub, ue); break;
-    case 2: run_list_uni<2, DIR, WT>(it, ub, ue); break;
-    default: run_list_uni<1, DIR, WT>(it, ub, ue); break;
+    case 16: run_list_uni<16, DIR, WT>(it, bs, ub, ue); break;
+    case 8: run_list_uni<8, DIR, WT>(it, bs, ub, ue); break;
+    case 4: run_list_uni<4, DIR, WT>(it, bs, ub, ue); break;
+    case 2: run_list_uni<2, DIR, WT>(it, bs, ub, ue); break;
+    default: run_list_uni<1, DIR, WT>(it, bs, ub, ue); break;
     }
 }
 
 // LISTS = false: affine + fragment items only (vector/hvector/subarray/struct nests), a
 // lean register budget; LISTS = true adds the index-list paths.
 template <int DIR, bool LISTS>
-__device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32_t nitems)
+__device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32_t nitems, Bases bs)
 {
     const uint32_t b = blockIdx.x;
     uint32_t lo = 0, hi = nitems - 1;
@@ -426,19 +432,19 @@ __device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32
     case ITEM_AFFINE:
         if (it->idx64) {
             switch (it->U) {
-            case 16: run_affine64<16, DIR>(it, ub, ue); break;
-            case 8: run_affine64<8, DIR>(it, ub, ue); break;
-            case 4: run_affine64<4, DIR>(it, ub, ue); break;
-            case 2: run_affine64<2, DIR>(it, ub, ue); break;
-            default: run_affine64<1, DIR>(it, ub, ue); break;
+            case 16: run_affine64<16, DIR>(it, bs, ub, ue); break;
+            case 8: run_affine64<8, DIR>(it, bs, ub, ue); break;
+            case 4: run_affine64<4, DIR>(it, bs, ub, ue); break;
+            case 2: run_affine64<2, DIR>(it, bs, ub, ue); break;
+            default: run_affine64<1, DIR>(it, bs, ub, ue); break;
             }
         } else {
             if (wt_stores<DIR>(it)) {
-                if (DIR == 0 && it->nt) dispatch_affine<DIR, true, true>(it, uint32_t(ub), uint32_t(ue));
-                else dispatch_affine<DIR, false, true>(it, uint32_t(ub), uint32_t(ue));
+                if (DIR == 0 && it->nt) dispatch_affine<DIR, true, true>(it, bs, uint32_t(ub), uint32_t(ue));
+                else dispatch_affine<DIR, false, true>(it, bs, uint32_t(ub), uint32_t(ue));
             } else {
-                if (DIR == 0 && it->nt) dispatch_affine<DIR, true, false>(it, uint32_t(ub), uint32_t(ue));
-                else dispatch_affine<DIR, false, false>(it, uint32_t(ub), uint32_t(ue));
+                if (DIR == 0 && it->nt) dispatch_affine<DIR, true, false>(it, bs, uint32_t(ub), uint32_t(ue));
+                else dispatch_affine<DIR, false, false>(it, bs, uint32_t(ub), uint32_t(ue));
             }
         }
         break;
@@ -446,24 +452,24 @@ __device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32
         if (!LISTS) break;
         if (it->idx64) {
             switch (it->U) {
-            case 16: run_list_uni64<16, DIR>(it, ub, ue); break;
-            case 8: run_list_uni64<8, DIR>(it, ub, ue); break;
-            case 4: run_list_uni64<4, DIR>(it, ub, ue); break;
-            case 2: run_list_uni64<2, DIR>(it, ub, ue); break;
-            default: run_list_uni64<1, DIR>(it, ub, ue); break;
+            case 16: run_list_uni64<16, DIR>(it, bs, ub, ue); break;
+            case 8: run_list_uni64<8, DIR>(it, bs, ub, ue); break;
+            case 4: run_list_uni64<4, DIR>(it, bs, ub, ue); break;
+            case 2: run_list_uni64<2, DIR>(it, bs, ub, ue); break;
+            default: run_list_uni64<1, DIR>(it, bs, ub, ue); break;
             }
         } else {
-            if (wt_stores<DIR>(it)) dispatch_list_uni<DIR, true>(it, uint32_t(ub), uint32_t(ue));
-            else dispatch_list_uni<DIR, false>(it, uint32_t(ub), uint32_t(ue));
+            if (wt_stores<DIR>(it)) dispatch_list_uni<DIR, true>(it, bs, uint32_t(ub), uint32_t(ue));
+            else dispatch_list_uni<DIR, false>(it, bs, uint32_t(ub), uint32_t(ue));
         }
         break;
     case ITEM_LIST_VAR:
-        if (LISTS) run_list_var<DIR>(it, ub, ue);
+        if (LISTS) run_list_var<DIR>(it, bs, ub, ue);
         break;
     default:   // ITEM_FRAG
         if (threadIdx.x == 0) {
-            const uint8_t *src = reinterpret_cast<const uint8_t *>(DIR == 0 ? it->user : it->packed);
-            uint8_t *dst = reinterpret_cast<uint8_t *>(DIR == 0 ? it->packed : it->user);
+            const uint8_t *src = reinterpret_cast<const uint8_t *>(DIR == 0 ? bs.u + it->user : bs.p + it->packed);
+            uint8_t *dst = reinterpret_cast<uint8_t *>(DIR == 0 ? bs.p + it->packed : bs.u + it->user);
             for (uint64_t k = 0; k < it->nbytes; ++k)
                 dst[k] = src[k];
         }
@@ -472,9 +478,10 @@ __device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32
 }
 
 template <int DIR, bool LISTS>
-__global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restrict__ items, uint32_t nitems)
+__global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restrict__ items, uint32_t nitems,
+                                                           uint64_t ubase, uint64_t pbase)
 {
-    move_body<DIR, LISTS>(items, nitems);
+    move_body<DIR, LISTS>(items, nitems, Bases{ubase, pbase});
 }
 
 // Small launches carry their descriptors in the kernel-argument segment: no device
@@ -486,14 +493,17 @@ __global__ __launch_bounds__(THREADS) void ddt_move_inline_kernel(ItemBlockN<NI>
     // would copy it to scratch)
     const ItemBlockN<NI> *kb = reinterpret_cast<const ItemBlockN<NI> *>(
         (const void *) __builtin_amdgcn_kernarg_segment_ptr());
-    move_body<DIR, LISTS>(kb->items, kb->n);
+    move_body<DIR, LISTS>(kb->items, kb->n, Bases{kb->ubase, kb->pbase});
 }
 
 template <int DIR, bool LISTS, uint32_t NI>
-static void launch_inline_n(const ItemBlock &blk, uint32_t ntasks, hipStream_t stream)
+static void launch_inline_n(const ItemBlock &blk, uint32_t ntasks, uint64_t ubase, uint64_t pbase,
+                            hipStream_t stream)
 {
     ItemBlockN<NI> b;
     b.n = blk.n;
+    b.ubase = ubase;
+    b.pbase = pbase;
     for (uint32_t i = 0; i < blk.n; ++i)
         b.items[i] = blk.items[i];
     hipLaunchKernelGGL((ddt_move_inline_kernel<DIR, LISTS, NI>), dim3(ntasks), dim3(THREADS), 0,
@@ -501,48 +511,51 @@ static void launch_inline_n(const ItemBlock &blk, uint32_t ntasks, hipStream_t s
 }
 
 template <int DIR, bool LISTS>
-static void launch_inline(const ItemBlock &blk, uint32_t ntasks, hipStream_t stream)
+static void launch_inline(const ItemBlock &blk, uint32_t ntasks, uint64_t ubase, uint64_t pbase,
+                          hipStream_t stream)
 {
-    if (blk.n == 1) launch_inline_n<DIR, LISTS, 1>(blk, ntasks, stream);
-    else if (blk.n == 2) launch_inline_n<DIR, LISTS, 2>(blk, ntasks, stream);
-    else if (blk.n <= 4) launch_inline_n<DIR, LISTS, 4>(blk, ntasks, stream);
-    else launch_inline_n<DIR, LISTS, INLINE_ITEMS>(blk, ntasks, stream);
+    if (blk.n == 1) launch_inline_n<DIR, LISTS, 1>(blk, ntasks, ubase, pbase, stream);
+    else if (blk.n == 2) launch_inline_n<DIR, LISTS, 2>(blk, ntasks, ubase, pbase, stream);
+    else if (blk.n <= 4) launch_inline_n<DIR, LISTS, 4>(blk, ntasks, ubase, pbase, stream);
+    else launch_inline_n<DIR, LISTS, INLINE_ITEMS>(blk, ntasks, ubase, pbase, stream);
 }
 
 template <int DIR>
-static void launch_dir(const Item *d_items, uint32_t nitems, uint32_t ntasks, bool lists, hipStream_t stream)
+static void launch_dir(const Item *d_items, uint32_t nitems, uint32_t ntasks, bool lists, uint64_t ubase,
+                       uint64_t pbase, hipStream_t stream)
 {
     if (lists)
         hipLaunchKernelGGL((ddt_move_kernel<DIR, true>), dim3(ntasks), dim3(THREADS), 0, stream,
-                           d_items, nitems);
+                           d_items, nitems, ubase, pbase);
     else
         hipLaunchKernelGGL((ddt_move_kernel<DIR, false>), dim3(ntasks), dim3(THREADS), 0, stream,
-                           d_items, nitems);
+                           d_items, nitems, ubase, pbase);
 }
 
-hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, hipStream_t stream)
+hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, uint64_t ubase,
+                              uint64_t pbase, hipStream_t stream)
 {
     if (ntasks == 0 || blk.n == 0)
         return hipSuccess;
     if (dir == 0) {
-        if (lists) launch_inline<0, true>(blk, ntasks, stream);
-        else launch_inline<0, false>(blk, ntasks, stream);
+        if (lists) launch_inline<0, true>(blk, ntasks, ubase, pbase, stream);
+        else launch_inline<0, false>(blk, ntasks, ubase, pbase, stream);
     } else {
-        if (lists) launch_inline<1, true>(blk, ntasks, stream);
-        else launch_inline<1, false>(blk, ntasks, stream);
+        if (lists) launch_inline<1, true>(blk, ntasks, ubase, pbase, stream);
+        else launch_inline<1, false>(blk, ntasks, ubase, pbase, stream);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
-                       hipStream_t stream)
+                       uint64_t ubase, uint64_t pbase, hipStream_t stream)
 {
     if (ntasks == 0 || nitems == 0)
         return hipSuccess;
     if (dir == 0)
-        launch_dir<0>(d_items, nitems, ntasks, lists, stream);
+        launch_dir<0>(d_items, nitems, ntasks, lists, ubase, pbase, stream);
     else
-        launch_dir<1>(d_items, nitems, ntasks, lists, stream);
+        launch_dir<1>(d_items, nitems, ntasks, lists, ubase, pbase, stream);
     return hipGetLastError();
 }
 

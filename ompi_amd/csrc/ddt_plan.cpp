@@ -67,11 +67,16 @@ hipError_t upload(void *dst, const void *src, size_t n)
 
 Plan::~Plan()
 {
-    // launches that read these descriptors or lists may still be in flight
-    if (!cache.empty() || !graveyard.empty() || dev_ready)
+    // launches that read these descriptors or lists may still be in flight (the datatype is
+    // being destroyed: the reference frees its description at once, opal_datatype_destruct)
+    if (!cache.empty() || !graveyard.empty() || !pinned.empty() || dev_ready)
         (void) hipDeviceSynchronize();
     cache.clear();
+    for (Retired &r : graveyard)
+        for (hipEvent_t e : r.events)
+            (void) hipEventDestroy(e);
     graveyard.clear();
+    pinned.clear();
     for (DevList &d : dev) {
         if (d.disp) (void) hipFree(d.disp);
         if (d.len) (void) hipFree(d.len);

@@ -40,9 +40,10 @@ bool use_slab(const Item &it);
 uint32_t total_tasks(const std::vector<Item> &items);
 
 // ddt_kernels.hip: dir 0 = pack / typed copy (user side -> packed side), 1 = unpack.
-hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, hipStream_t stream);
+hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, uint64_t ubase,
+                              uint64_t pbase, hipStream_t stream);
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
-                       hipStream_t stream);
+                       uint64_t ubase, uint64_t pbase, hipStream_t stream);
 
 // external32 conversion between a native packed stream and its big-endian form.
 hipError_t launch_ext(const ConvSeg *segs, uint32_t nseg, const ConvRun *runs, uint64_t E,

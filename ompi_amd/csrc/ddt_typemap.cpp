@@ -1222,18 +1222,33 @@ bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<
             std::memcpy(&items, p + 4, 4);
             std::memcpy(&loops, p + 8, 4);
             std::memcpy(&extent, p + 24, 8);
-            size_t endi = i + items;
-            if (endi >= end + 1 || items < 1)
+            // the matching END_LOOP sits `items` entries on and carries the same item count
+            // (CREATE_LOOP_START / CREATE_LOOP_END, opal_datatype_internal.h:171-189); it must
+            // lie inside this level, and its size must be the body's packed bytes
+            const size_t endi = i + items;
+            if (items < 1 || endi >= end)
                 return false;
             const unsigned char *q = raw + 32 * endi;
+            uint16_t eflags, etype;
+            uint32_t eitems;
             uint64_t size;
+            std::memcpy(&eflags, q, 2);
+            std::memcpy(&etype, q + 2, 2);
+            std::memcpy(&eitems, q + 4, 4);
             std::memcpy(&size, q + 16, 8);
+            if ((eflags & F_DATA) || etype != 1 || eitems != items)
+                return false;
             Node l;
             l.kind = Node::LOOP;
             l.count = loops;
             l.extent = extent;
             l.body_size = size;
             if (!parse_opal(raw, i + 1, endi, l.body))
+                return false;
+            uint64_t body = 0;
+            for (const Node &n : l.body)
+                body += n.packed_bytes();
+            if (body != size)
                 return false;
             out.push_back(std::move(l));
             i = endi + 1;

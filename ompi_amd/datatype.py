@@ -116,6 +116,12 @@ class Datatype:
         check(lib().ddt_type_engine_info(self.handle, out), "ddt_type_engine_info")
         return dict(zip(("sorted", "device_bytes", "chunks", "slots"), list(out)))
 
+    def cache_info(self) -> dict:
+        """Descriptor-set cache of the plan (ddt_type_cache_info)."""
+        out = (ctypes.c_int64 * 4)()
+        check(lib().ddt_type_cache_info(self.handle, out), "ddt_type_cache_info")
+        return dict(zip(("cached", "retiring", "pinned", "device"), list(out)))
+
     def __repr__(self):
         return f"Datatype({self.name}, {self.info()})"
 

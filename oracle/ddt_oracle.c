@@ -590,6 +590,12 @@ void ort_info(const ort_type *t, int64_t *out)
     out[7] = t->nruns;
 }
 
+/* OPAL id of the elements of run i (the DATA entry type of a flat description) */
+int64_t ort_run_tid(const ort_type *t, int64_t i)
+{
+    return t->runs[i].tid;
+}
+
 /* run i of the flattened map: disp, len, esize */
 void ort_run_at(const ort_type *t, int64_t i, int64_t *out)
 {

@@ -44,6 +44,7 @@ def lib():
             "ort_darray": (vp, [i, i, i, vp, vp, vp, vp, i, vp]),
             "ort_resized": (vp, [vp, i64, i64]),
             "ort_info": (None, [vp, vp]), "ort_run_at": (None, [vp, i64, vp]),
+            "ort_run_tid": (i64, [vp, i64]),
             "ort_pack": (i64, [vp, i64, vp, i64, vp, i64]),
             "ort_pack_bytes": (i64, [vp, i64, vp, i64, vp, i64]),
             "ort_unpack": (i64, [vp, i64, vp, i64, vp, i64]),
@@ -94,6 +95,10 @@ class OType:
             lib().ort_run_at(self.h, r, out)
             res.append((out[0], out[1], out[2]))
         return res
+
+    def typed_runs(self):
+        """[(disp, len, esize, opal id)] of the flattened type map, in type-map order."""
+        return [r + (int(lib().ort_run_tid(self.h, i)),) for i, r in enumerate(self.runs())]
 
     @property
     def size(self):

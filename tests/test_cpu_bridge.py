@@ -1,0 +1,128 @@
+"""The opal fAdvance bridge on CPU: layout of Open MPI's objects, attach semantics of the
+post-prepare hook, and the per-datatype import cache (no data moves without a GPU)."""
+from __future__ import annotations
+
+import ctypes
+
+import pytest
+
+from tests import opal_shapes as S
+from tests import recipes as R
+
+FLOAT8, FLOAT4, INT4, UINT4 = 16, 15, 6, 11
+
+
+def _xface(n=16):
+    """Appendix A shape of a 3D-vector x face: FLOAT8 count n*n blen 1 extent 8n."""
+    ents = [S.data(FLOAT8, n * n, 1, 8 * n, 0)]
+    size = 8 * n * n
+    ub = (n * n - 1) * 8 * n + 8
+    return S.OpalType(ents, size, 0, ub, 0, ub)
+
+
+def test_layout_matches_compiled_bridge():
+    compiled, mine = S.check_layout()
+    assert compiled == mine
+    # the layout notes of the reference headers (opal_datatype.h:204-211, opal_convertor.h:136,149)
+    assert compiled[0] == 200 and compiled[3] == 64 and S.OpalConvertor.sizes.offset == 128
+
+
+def test_attach_installs_movers_on_accelerator_convertors():
+    L = S.bridge_lib()
+    t = _xface()
+    c = S.Convertor()
+    assert c.prepare(t, 3, 0x7000_0000_0000, send=True) == S.OPAL_SUCCESS
+    assert c.c.fAdvance == ctypes.cast(L.opal_pack_hip, ctypes.c_void_p).value
+    assert c.c.fPosition == ctypes.cast(L.opal_position_hip, ctypes.c_void_p).value
+    assert c.c.local_size == 3 * t.dt.size and not (c.c.flags & S.CONVERTOR_NO_OP)
+    r = S.Convertor()
+    assert r.prepare(t, 1, 0x7000_0000_0000, send=False) == S.OPAL_SUCCESS
+    assert r.c.fAdvance == ctypes.cast(L.opal_unpack_hip, ctypes.c_void_p).value
+    # a host buffer (check_addr == 0) keeps the reference movers: the bridge declines
+    h = S.Convertor()
+    assert h.prepare(t, 1, 0x1000, send=True, device=False) == S.OPAL_ERR_NOT_SUPPORTED
+    assert not h.c.fAdvance
+    t.destruct()
+
+
+def test_position_function_resumes_at_byte_offset():
+    t = _xface()
+    c = S.Convertor()
+    c.prepare(t, 2, 0x7000_0000_0000, send=False)
+    assert c.set_position(777) == 777
+    assert c.c.bConverted == 777 and not (c.c.flags & S.CONVERTOR_COMPLETED)
+    assert c.set_position(10 ** 9) == 2 * t.dt.size   # clamped, completed (opal_convertor.h:372-377)
+    assert c.c.flags & S.CONVERTOR_COMPLETED
+    t.destruct()
+
+
+def test_import_cache_hits_invalidation_and_stale_addresses():
+    S.bridge_lib().opal_hip_bridge_finalize()
+    base = S.stats()
+    t = _xface()
+    for _ in range(4):
+        S.Convertor().prepare(t, 1, 0x7000_0000_0000, send=True)
+    st = S.stats()
+    assert st["imports"] - base["imports"] == 1 and st["hits"] - base["hits"] >= 3
+    assert st["entries"] == 1
+    # opal_datatype_destruct drops the entry; the next prepare imports again
+    t.destruct()
+    assert S.stats()["entries"] == 0
+    S.Convertor().prepare(t, 1, 0x7000_0000_0000, send=True)
+    assert S.stats()["imports"] - base["imports"] == 2
+    # a different description at the same opal_datatype_t address (destruct never called):
+    # the fingerprint notices and re-imports instead of serving the old plan
+    raw2 = t.raw.copy()
+    t.raw = raw2
+    t.dt.opt_desc.desc = raw2.ctypes.data
+    S.Convertor().prepare(t, 1, 0x7000_0000_0000, send=True)
+    st = S.stats()
+    assert st["stale"] - base["stale"] == 1 and st["entries"] == 1
+    S.bridge_lib().opal_hip_bridge_finalize()
+    assert S.stats()["entries"] == 0
+
+
+def test_no_op_and_empty_convertors_skip_the_bridge():
+    """OPAL_CONVERTOR_PREPARE returns before dispatch for NO_GAPS types (opal_convertor.c:
+    562-567) and empty messages (:539-544): opal_convertor_pack copies those itself."""
+    contig = S.OpalType([S.data(FLOAT8, 1, 64, 512, 0)], 512, 0, 512, 0, 512,
+                        flags=S.F_CONTIGUOUS | S.F_NO_GAPS)
+    c = S.Convertor()
+    c.prepare(contig, 4, 0x7000_0000_0000, send=True)
+    assert c.c.flags & S.CONVERTOR_NO_OP and not c.c.fAdvance
+    e = S.Convertor()
+    e.prepare(_xface(), 0, 0x7000_0000_0000, send=True)
+    assert e.c.flags & S.CONVERTOR_COMPLETED and e.c.local_size == 0
+
+
+@pytest.mark.parametrize("case", ["end_missing", "end_items", "end_size", "past_used"])
+def test_malformed_descriptions_are_refused(case):
+    """The import validates LOOP/END_LOOP pairing (CREATE_LOOP_START/END,
+    opal_datatype_internal.h:171-189) before anything reads past the description."""
+    body = S.data(FLOAT4, 4, 1, 8, 0)
+    if case == "end_missing":
+        ents = [S.loop(3, 2, 64), body, S.data(FLOAT4, 1, 1, 4, 40)]
+    elif case == "end_items":
+        ents = [S.loop(3, 2, 64), body, S.end_loop(3, 16, 0)]
+    elif case == "end_size":
+        ents = [S.loop(3, 2, 64), body, S.end_loop(2, 20, 0)]
+    else:
+        ents = [S.loop(3, 4, 64), body, S.end_loop(2, 16, 0)]
+    t = S.OpalType(ents, 48, 0, 64 * 2 + 28, 0, 64 * 2 + 28)
+    c = S.Convertor()
+    assert c.prepare(t, 1, 0x7000_0000_0000, send=True) == -5   # OPAL_ERR_BAD_PARAM
+    ok = S.OpalType([S.loop(3, 2, 64), body, S.end_loop(2, 16, 0)], 48, 0, 64 * 2 + 28, 0, 64 * 2 + 28)
+    assert S.Convertor().prepare(ok, 1, 0x7000_0000_0000, send=True) == S.OPAL_SUCCESS
+    ok.destruct()
+
+
+def test_flat_descriptions_of_corpus_types_import():
+    from tests import corpus
+    for name in sorted(corpus.CORPUS):
+        rec, _ = corpus.CORPUS[name]()
+        b = R.Built(rec)
+        t = S.flat_from_oracle(b.o)
+        c = S.Convertor()
+        rc = c.prepare(t, 2, 0x7000_0000_0000, send=True)
+        assert rc == S.OPAL_SUCCESS, name
+        t.destruct()
