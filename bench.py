@@ -213,6 +213,51 @@ def single_face_latency(dev, stream, user, origin, reps=200):
     return out
 
 
+# ------------------------------------------------------------------ per-face throughput
+def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z")):
+    """The north star's per-face figure: ONE face type of the 256^3
+    double grid over `fields` fields in one launch (count = fields), pack then unpack, each
+    timed with HIP events (median over `steps`).  With 512 fields a face's working set
+    (user lines + packed stream, 2 x 256 MiB) is twice the 256 MiB Infinity Cache, so the
+    loop streams from HBM; at the bench's 16 fields a face is 8 MiB and launch-bound."""
+    import torch
+    import ompi_amd
+    from ompi_amd import recipe as ER
+    recs = face_recipes()
+    field = 256 ** 3 * 8
+    user = torch.empty(fields * field, dtype=torch.uint8, device=dev)
+    user.fill_(0x5A)
+    stream = torch.cuda.current_stream(dev)
+    out = {"fields": fields}
+    for k in faces:
+        ft = ER.build_committed(recs[k])
+        fS = ft.info()["size"] * fields
+        fp = torch.empty(fS, dtype=torch.uint8, device=dev)
+        c1 = ompi_amd.Convertor()
+        c1.set_stream(stream, True)
+        evs = []
+        for i in range(warmup + steps):
+            a, b_, c_ = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            a.record(stream)
+            c1.prepare_for_send(ft, fields, user.data_ptr())
+            c1.pack([(fp, fS)])
+            b_.record(stream)
+            c1.prepare_for_recv(ft, fields, user.data_ptr())
+            c1.unpack([(fp, fS)])
+            c_.record(stream)
+            if i >= warmup:
+                evs.append((a, b_, c_))
+        torch.cuda.synchronize()
+        tp = float(np.median([a.elapsed_time(b_) for a, b_, _ in evs])) / 1e3
+        tu = float(np.median([b_.elapsed_time(c_) for _, b_, c_ in evs])) / 1e3
+        out[k] = {"packed_bytes": fS, "pack_us": round(tp * 1e6, 2), "unpack_us": round(tu * 1e6, 2),
+                  "GiBs": round(2 * fS / (tp + tu) / GiB, 1), "frac": round(4 * fS / (tp + tu) / HBM_PEAK, 4)}
+        del fp
+    del user
+    torch.cuda.empty_cache()
+    return out
+
+
 # ------------------------------------------------------------------ main
 def main():
     ap = argparse.ArgumentParser()
@@ -221,7 +266,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--faces", action="store_true", help="also time each face type alone")
+    ap.add_argument("--no-faces", action="store_true", help="skip the per-face measurement")
+    ap.add_argument("--face-fields", type=int, default=512,
+                    help="fields per face launch for the per-face figure (512: beyond the Infinity Cache)")
     ap.add_argument("--no-graph", action="store_true", help="skip the HIP-graph replay measurement")
     ap.add_argument("--event-every", type=int, default=10,
                     help="bracket every Nth timed step with HIP events (kernel durations)")
@@ -391,33 +438,11 @@ def main():
     if rank == 0 and args.config == "cfg2" and not args.no_latency:
         result["single_face_latency_us"] = single_face_latency(dev, stream, user, origin)
 
-    if args.faces and rank == 0:
-        faces = {}
-        for k, frec in (face_recipes().items() if args.config == "cfg2" else []):
-            ft = ER.build_committed(frec)
-            fS = ft.info()["size"] * count
-            fp = torch.empty(fS, dtype=torch.uint8, device=dev)
-            c1 = ompi_amd.Convertor()
-            c1.set_stream(stream, True)
-            evs = []
-            for i in range(args.warmup + args.steps):
-                a, b_, c_ = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-                a.record(stream)
-                c1.prepare_for_send(ft, count, user.data_ptr())
-                c1.pack([(fp, fS)])
-                b_.record(stream)
-                c1.prepare_for_recv(ft, count, user.data_ptr())
-                c1.unpack([(fp, fS)])
-                c_.record(stream)
-                if i >= args.warmup:
-                    evs.append((a, b_, c_))
-            torch.cuda.synchronize()
-            fp_t = float(np.mean([a.elapsed_time(b_) for a, b_, _ in evs])) / 1e3
-            fu_t = float(np.mean([b_.elapsed_time(c_) for _, b_, c_ in evs])) / 1e3
-            faces[k] = {"GiBs": round(2 * fS / (fp_t + fu_t) / GiB, 2),
-                        "frac": round(4 * fS / (fp_t + fu_t) / HBM_PEAK, 4),
-                        "pack_us": round(fp_t * 1e6, 2), "unpack_us": round(fu_t * 1e6, 2)}
-        result["faces"] = faces
+    if rank == 0 and args.config == "cfg2" and not args.no_faces:
+        # per-face figure of the north star: each face type alone, batched over many fields
+        # (beyond the Infinity Cache), and at the bench's own 16 fields (launch-bound)
+        result["faces"] = face_throughput(dev, args.face_fields, max(5, min(args.steps, 20)))
+        result["faces_at_bench_fields"] = face_throughput(dev, count, max(5, min(args.steps, 20)))
 
     if rank == 0 and base_sample is not None:
         srec, scount, what, host_user, gpu_prefix = base_sample

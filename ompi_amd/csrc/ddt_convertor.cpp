@@ -56,6 +56,27 @@ MemKind classify(const void *p)
     return MEM_HOST;
 }
 
+// Pinned (page-locked, device-mapped) host memory: the device address of [p, p + n), or 0
+// for pageable memory, device memory or a range whose two ends do not map contiguously.
+uint64_t pinned_device_range(const void *p, uint64_t n)
+{
+    auto dev_of = [](const void *q) -> uint64_t {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void) hipGetLastError();
+            return 0;
+        }
+        if (a.type != hipMemoryTypeHost || !a.devicePointer)
+            return 0;
+        return uint64_t(uintptr_t(a.devicePointer));
+    };
+    const uint64_t d0 = dev_of(p);
+    if (!d0 || n == 0)
+        return d0;
+    const uint64_t d1 = dev_of(static_cast<const char *>(p) + (n - 1));
+    return d1 == d0 + (n - 1) ? d0 : 0;
+}
+
 struct Window {
     uint64_t w0, w1;   // packed-stream byte range
     uint64_t ptr;      // device pointer holding byte w0
@@ -63,7 +84,7 @@ struct Window {
 
 constexpr size_t kCacheEntries = 32;
 constexpr size_t kRetiredMax = 64;
-constexpr uint64_t kStageChunk = 16ull << 20;   // host staging pipeline chunk
+uint64_t stage_bytes() { return uint64_t(tuning().stage_mb) << 20; }   // host staging slot
 
 bool capturing(hipStream_t s)
 {
@@ -301,6 +322,7 @@ struct ddt_convertor {
     // (ev_k), possibly queued by an earlier asynchronous call on another stream -- has
     // passed (pml_ob1_recvreq.c:627-663 issues such back-to-back async unpacks).
     void *stage[2] = {nullptr, nullptr};
+    uint64_t stage_size = 0;
     hipStream_t copy_stream = nullptr;
     hipEvent_t ev_k[2] = {nullptr, nullptr}, ev_c[2] = {nullptr, nullptr};
     bool rec_k[2] = {false, false}, rec_c[2] = {false, false};
@@ -325,8 +347,9 @@ struct ddt_convertor {
         if (copy_stream)
             return DDT_SUCCESS;
         HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+        stage_size = stage_bytes();
         for (int i = 0; i < 2; ++i) {
-            HIPCHK(hipMalloc(&stage[i], kStageChunk));
+            HIPCHK(hipMalloc(&stage[i], stage_size));
             HIPCHK(hipEventCreateWithFlags(&ev_k[i], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&ev_c[i], hipEventDisableTiming));
         }
@@ -347,10 +370,10 @@ namespace {
 
 // Chunk schedule of a staged window: a short first chunk (the copy engine starts while
 // the first kernel is still short), then full slots.
-uint64_t stage_chunk(uint64_t done, uint64_t left)
+uint64_t stage_chunk(uint64_t slot, uint64_t done, uint64_t left)
 {
-    const uint64_t want = done == 0 ? (kStageChunk >> 3) : kStageChunk;
-    return std::min<uint64_t>(want, left);
+    const uint64_t want = done == 0 ? std::max<uint64_t>(slot >> 4, 1u << 20) : slot;
+    return std::min<uint64_t>(std::min<uint64_t>(want, slot), left);
 }
 
 // Move the packed windows of a convertor call: device iovecs in one launch, host iovecs
@@ -368,7 +391,7 @@ int execute(ddt_convertor *c, const std::vector<Window> &dev_wins,
         for (const auto &hw : host_wins) {
             for (uint64_t off = hw.first.w0; off < hw.first.w1;) {
                 const int s = int(c->next_slot++ & 1u);
-                const uint64_t n = stage_chunk(off - hw.first.w0, hw.first.w1 - off);
+                const uint64_t n = stage_chunk(c->stage_size, off - hw.first.w0, hw.first.w1 - off);
                 char *hp = static_cast<char *>(hw.second) + (off - hw.first.w0);
                 std::vector<Window> w{{off, off + n, uint64_t(uintptr_t(c->stage[s]))}};
                 if (dir == 0) {   // pack: kernel -> D2H
@@ -470,8 +493,11 @@ int32_t advance(ddt_convertor *c, struct iovec *iov, uint32_t *out_size, size_t 
         if (n) {
             if (!iov[i].iov_base)
                 return fail(DDT_ERR_BAD_PARAM, "null iov_base");
+            uint64_t hd = 0;
             if (classify(iov[i].iov_base) == MEM_DEVICE)
                 dev.push_back({pos, w1, uint64_t(uintptr_t(iov[i].iov_base))});
+            else if ((tuning().hostdirect & (dir == 0 ? 2 : 1)) && (hd = pinned_device_range(iov[i].iov_base, n)) != 0)
+                dev.push_back({pos, w1, hd});   // the kernel reads/writes the pinned pages over PCIe
             else
                 host.push_back({{pos, w1, 0}, iov[i].iov_base});
         }
@@ -1296,6 +1322,14 @@ int ddt_tune(const char *key, long value)
         tuning().sorted = value;
     else if (k == "wt")
         tuning().wt = value < 0 ? -1 : int(value > 2 ? 2 : value);
+    else if (k == "hostdirect")
+        tuning().hostdirect = int(value & 3);
+    else if (k == "stage_mb")
+        tuning().stage_mb = value < 1 ? 1 : value;
+    else if (k == "snt")
+        tuning().snt = value < 0 ? -1 : (value ? 1 : 0);
+    else if (k == "spass")
+        tuning().spass = value < 1 ? 1 : value;
     else if (k == "reset")
         tuning() = Tuning{};
     else

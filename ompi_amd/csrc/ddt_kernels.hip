@@ -146,7 +146,9 @@ template <typename T, bool WT> __device__ __forceinline__ void st(T *p, T v)
     else *p = v;
 }
 
-template <int U, int DIR, int ND, bool NT, bool WT>
+// NT: 0 plain; 1 non-temporal user-side loads (pack of sparse gathers, Item::nt == 1);
+// 2 streaming leaf: every load and store non-temporal (Item::nt == 2).
+template <int U, int DIR, int ND, int NT, bool WT>
 __device__ __forceinline__ void run_affine(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
 {
     using T = typename Vec<U>::T;
@@ -170,13 +172,17 @@ __device__ __forceinline__ void run_affine(const Item *it, Bases bs, uint32_t ub
                 nest_offsets32(n, blk, uo, po);
                 const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
                 dst[k] = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
-                v[k] = ld<T, NT && DIR == 0>(src);   // NT: user side only
+                v[k] = ld<T, (NT == 1 && DIR == 0) || NT == 2>(src);
             }
         }
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            if (dst[k])
-                st<T, WT>(dst[k], v[k]);   // (nt stores measured slower: scatter 51 vs 18 us)
+            if (dst[k]) {
+                if constexpr (NT == 2)
+                    __builtin_nontemporal_store(v[k], dst[k]);
+                else
+                    st<T, WT>(dst[k], v[k]);   // (nt scattered stores measured slower: 51 vs 18 us)
+            }
     }
 }
 
@@ -324,7 +330,7 @@ __device__ __forceinline__ void run_list_var(const Item *it, Bases bs, uint64_t 
 
 // Deep nests (> 4 dims) are rare: their dims are re-read from the (cached) item on every
 // unit instead of being held in registers, which keeps the kernel's SGPR budget small.
-template <int U, int DIR, bool NT, bool WT>
+template <int U, int DIR, int NT, bool WT>
 __device__ __forceinline__ void run_affine_deep(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
 {
     using T = typename Vec<U>::T;
@@ -347,11 +353,11 @@ __device__ __forceinline__ void run_affine_deep(const Item *it, Bases bs, uint32
         po += int64_t(blk) * it->pstr[0];
         const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
         T *dst = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
-        st<T, WT>(dst, ld<T, NT && DIR == 0>(src));
+        st<T, WT>(dst, ld<T, NT == 1 && DIR == 0>(src));
     }
 }
 
-template <int U, int DIR, bool NT, bool WT>
+template <int U, int DIR, int NT, bool WT>
 __device__ __forceinline__ void dispatch_affine_u(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
 {
     switch (it->ndim) {
@@ -363,7 +369,7 @@ __device__ __forceinline__ void dispatch_affine_u(const Item *it, Bases bs, uint
     }
 }
 
-template <int DIR, bool NT, bool WT>
+template <int DIR, int NT, bool WT>
 __device__ __forceinline__ void dispatch_affine(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
 {
     switch (it->U) {
@@ -439,12 +445,14 @@ __device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32
             default: run_affine64<1, DIR>(it, bs, ub, ue); break;
             }
         } else {
-            if (wt_stores<DIR>(it)) {
-                if (DIR == 0 && it->nt) dispatch_affine<DIR, true, true>(it, bs, uint32_t(ub), uint32_t(ue));
-                else dispatch_affine<DIR, false, true>(it, bs, uint32_t(ub), uint32_t(ue));
+            if (it->nt == 2 && it->U == 16) {
+                dispatch_affine_u<16, DIR, 2, false>(it, bs, uint32_t(ub), uint32_t(ue));
+            } else if (wt_stores<DIR>(it)) {
+                if (DIR == 0 && it->nt == 1) dispatch_affine<DIR, 1, true>(it, bs, uint32_t(ub), uint32_t(ue));
+                else dispatch_affine<DIR, 0, true>(it, bs, uint32_t(ub), uint32_t(ue));
             } else {
-                if (DIR == 0 && it->nt) dispatch_affine<DIR, true, false>(it, bs, uint32_t(ub), uint32_t(ue));
-                else dispatch_affine<DIR, false, false>(it, bs, uint32_t(ub), uint32_t(ue));
+                if (DIR == 0 && it->nt == 1) dispatch_affine<DIR, 1, false>(it, bs, uint32_t(ub), uint32_t(ue));
+                else dispatch_affine<DIR, 0, false>(it, bs, uint32_t(ub), uint32_t(ue));
             }
         }
         break;

@@ -446,6 +446,23 @@ uint32_t use_wt(uint32_t U, uint64_t blen, const std::vector<LeafDim> *dims)
     return 1;
 }
 
+// Streaming leaves move every byte with non-temporal loads and stores when their blocks are
+// long contiguous runs (>= 64 KiB: z faces, planes): the chip's copy ceiling is 6.2 TB/s
+// r+w that way against 5.6-5.9 TB/s with default policies (scripts/ubench_copy.hip,
+// profiles/r2_ubench_copy.log); a z face of 512 fields went from 0.683 to 0.717 of 8 TB/s
+// pack+unpack.  Shorter runs (the y face's 2 KiB rows) measured slower with it (0.751 ->
+// 0.697), and so did the halo's pack (profiles/r2_ab_stream_policy.jsonl).
+// ddt_tune("snt") forces it for every leaf with blocks >= 256 B.
+bool use_snt(uint32_t U, uint64_t blen)
+{
+    const int force = tuning().snt;
+    if (U != 16)
+        return false;
+    if (force >= 0)
+        return force == 1 && blen >= 256;
+    return blen >= (64u << 10);
+}
+
 uint64_t units_per_task(uint32_t U)
 {
     uint64_t u = (32u << 10) / U;   // provisional; assign_tasks() sets the final size
@@ -549,7 +566,7 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
             it.idx64 = (big || total_units >= 0xffffffffull) ? 1 : 0;
             if (u1 * U > leaf_total || total_units * U != leaf_total)
                 throw std::runtime_error("plan: affine unit range outside its leaf");
-            it.nt = use_nt(U, blen, sd) ? 1 : 0;
+            it.nt = use_snt(U, blen) ? 2 : (use_nt(U, blen, sd) ? 1 : 0);
             it.wt = use_wt(U, blen, &sd);
             it.u0 = u0;
             it.u1 = u1;
@@ -685,11 +702,12 @@ void assign_tasks(std::vector<Item> &items)
                 it.units_per_task = u < THREADS ? THREADS : u;
             }
     } else {
-        // ~1024 tasks (4 per CU) for the whole launch, 4..64 KiB each; a sparse affine
-        // leaf (blocks <= 64 B: one DRAM burst per unit) caps its task at ONE unrolled
-        // pass of the workgroup (THREADS*K units), a streaming leaf at four passes.
-        // Measured on the 6-face halo: 8 KiB tasks 99/82 us, 64 KiB 92/78 us, and the
-        // x-face alone is best at one pass (scripts/ab.py).
+        // ~1024 tasks (4 per CU) for the whole launch, 4..64 KiB each; an affine leaf caps
+        // its task at ONE unrolled pass of the workgroup (THREADS*K units: 16 KiB of 16-byte
+        // units), sparse or streaming (tuning().spass passes for streams).  One-pass
+        // streaming tasks against four (profiles/r2_ab_stream_policy.jsonl): y face of 512
+        // fields 0.691 -> 0.751 of 8 TB/s, z face 0.624 -> 0.683, halo 177.7 -> 174.9 us;
+        // the copy microbenchmark agrees (16 KiB chunks 5.9 TB/s, 64 KiB 5.6 TB/s).
         uint64_t tb = 4096;
         while (tb < (64u << 10) && tb * 1024 < total)
             tb *= 2;
@@ -700,7 +718,7 @@ void assign_tasks(std::vector<Item> &items)
             if (it.kind == ITEM_AFFINE) {
                 const uint64_t pass = uint64_t(THREADS) * unroll_of(it.U) * it.U;
                 const bool sparse = it.upb * it.U <= 64;
-                cap = pass * (sparse ? 1 : 4);
+                cap = pass * uint64_t(sparse ? 1 : std::max<long>(1, tuning().spass));
             }
             const uint64_t b = tb < cap ? tb : cap;
             uint64_t u = b / it.U;

@@ -24,6 +24,12 @@ struct Tuning {
     int ptr = 1;          // 1: a reused inline descriptor set is launched by pointer; 0: always inline
     int xcd = -1;         // XCD-contiguous task slabs: -1 auto (line-dense affine items), 0 off, 1 all
     long xchunk = 0;      // tasks per XCD run for slab items: 0 = one slab per XCD
+    int snt = -1;         // streaming leaves (U = 16, blocks >= 256 B): non-temporal loads and
+                          // stores; -1 auto (blocks >= 64 KiB), 0 off, 1 on
+    long spass = 1;       // task of a streaming leaf: this many unrolled workgroup passes
+    int hostdirect = 3;   // pinned host iovecs moved by the kernel itself over PCIe (no HBM
+                          // staging): bit 0 unpack, bit 1 pack (end to end)
+    long stage_mb = 64;   // HBM staging slot (two per convertor) for pageable host iovecs
 };
 Tuning &tuning();
 // Synchronous host -> device copy on a library-private stream (capture-safe).

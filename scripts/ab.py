@@ -32,6 +32,7 @@ def main():
                     help="timing only: unpack with a type that writes the same bytes in reverse order "
                          "(fields, faces and rows reversed; xx and cfg2), to test Infinity Cache reuse")
     ap.add_argument("--prewarm", type=float, default=0.0, help="seconds of HBM copies first")
+    ap.add_argument("--count", type=int, default=0, help="override the instance (field) count")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     faces = bench.face_recipes()
@@ -50,6 +51,8 @@ def main():
         recipe, count = faces[args.config], 16
     else:
         recipe, count, _ = bench.make_workload(args.config)
+    if args.count:
+        count = args.count
     rev_recipe = None
     if args.unpack_rev:
         d8 = ("basic", 16)

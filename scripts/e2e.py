@@ -44,8 +44,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--stage-mb", type=int, default=0, help="ddt_tune('stage_mb'): staging slot MiB")
+    ap.add_argument("--tune", default="", help="extra ddt_tune settings, k=v;k=v")
+    ap.add_argument("--hostdirect", type=int, default=-1,
+                    help="ddt_tune('hostdirect'): 1 = kernel moves pinned host bytes itself, 0 = HBM staging")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
+    if args.hostdirect >= 0:
+        ompi_amd.lib().ddt_tune(b"hostdirect", args.hostdirect)
+    if args.stage_mb:
+        ompi_amd.lib().ddt_tune(b"stage_mb", args.stage_mb)
+    for kv in filter(None, args.tune.split(";")):
+        k, v = kv.split("=")
+        ompi_amd.lib().ddt_tune(k.encode(), int(v))
     recipe, count, desc = bench.make_workload(args.config)
     dt = ER.build_committed(recipe)
     info = dt.info()
@@ -96,8 +107,21 @@ def main():
     pack_ovl()
     torch.cuda.synchronize()
     same = bool(torch.equal(ref.cpu(), hpk))
+    # and the overlapped unpack must restore what the device path restores
+    keep = user.clone()
+    user.fill_(0xA5)
+    unpack_ovl()
+    torch.cuda.synchronize()
+    got_o = user.clone()
+    user.fill_(0xA5)
+    dpk.copy_(hpk)
+    unpack_dev()
+    torch.cuda.synchronize()
+    same_u = bool(torch.equal(got_o, user))
+    user.copy_(keep)
     out = {"config": args.config, "workload": desc["workload"], "packed_bytes": S,
-           "overlapped_matches_device_path": same,
+           "hostdirect": int(args.hostdirect), "stage_mb": args.stage_mb, "tune": args.tune,
+           "overlapped_matches_device_path": same, "overlapped_unpack_matches": same_u,
            "GiBs": {k: round(S / v / GiB, 2) for k, v in t.items()},
            "us": {k: round(v * 1e6, 1) for k, v in t.items()},
            "pack+unpack_GiBs": {

@@ -355,12 +355,16 @@ def test_bridge_async_stream_host_fragments(device):
     ot.destruct()
 
 
-def test_engine_async_unpack_slot_reuse_across_calls(device):
+@pytest.mark.parametrize("mode", ["pinned-direct", "pinned-staged", "pageable-staged"])
+def test_engine_async_unpack_slot_reuse_across_calls(device, mode):
     """back-to-back asynchronous unpacks from host buffers through ONE
     engine convertor, each call reusing both staging slots while the previous call's
-    kernels may still run; bytes must match the oracle."""
+    kernels may still run; bytes must match the oracle.  Pinned host memory is read by the
+    kernel itself by default (hostdirect); staging is forced for the pinned-staged case and
+    is the only path for pageable memory."""
     import torch
     import ompi_amd
+    ompi_amd.lib().ddt_tune(b"hostdirect", 0 if mode == "pinned-staged" else 3)
     rec = ("vector", 1 << 19, 16, 24, ("basic", FLOAT4))   # 32 MiB packed
     b = R.Built(rec)
     e = b.engine()
@@ -369,7 +373,10 @@ def test_engine_async_unpack_slot_reuse_across_calls(device):
     span, origin = R.layout(info, 1)
     host = R.fill(span, 17)
     ref = np.frombuffer(b.o.pack(1, host, origin, 0, size, element_granular=False), dtype=np.uint8)
-    src = [torch.from_numpy(ref.copy()).pin_memory() for _ in range(2)]
+    if mode.startswith("pinned"):
+        src = [torch.from_numpy(ref.copy()).pin_memory() for _ in range(2)]
+    else:
+        src = [torch.from_numpy(ref.copy()) for _ in range(2)]
     s = torch.cuda.Stream(device)
     outs = [torch.full((span,), 0xA5, dtype=torch.uint8, device=device) for _ in range(3)]
     c = ompi_amd.Convertor()
@@ -383,6 +390,7 @@ def test_engine_async_unpack_slot_reuse_across_calls(device):
     s.synchronize()
     want = np.full(span, 0xA5, dtype=np.uint8)
     b.o.unpack(1, want, origin, 0, ref.tobytes())
+    ompi_amd.lib().ddt_tune(b"hostdirect", 3)
     for out in outs:
         np.testing.assert_array_equal(_host(out), want)
 
