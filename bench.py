@@ -131,7 +131,7 @@ def sample_recipe(name, recipe, count):
     if name == "cfg2":
         return recipe, 2, "2 of 16 fields"
     if name == "cfg3":
-        return recipe, 1, "1 of 8 fields"
+        return recipe, 1, f"1 of {count} fields"
     if name == "cfg4":
         n = 1 << 20
         return ("indexed_block", 1, recipe[2][:n], recipe[3]), 1, \
@@ -267,6 +267,12 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-faces", action="store_true", help="skip the per-face measurement")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="skip the post-run all-gather of the packed shards (N > 1)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: ONE message of the config's total size split over the ranks "
+                         "(top-level count, outer loop or index prefix: ompi_amd.shard.split_recipe); "
+                         "cfg3 = 64 fields in total")
     ap.add_argument("--face-fields", type=int, default=512,
                     help="fields per face launch for the per-face figure (512: beyond the Infinity Cache)")
     ap.add_argument("--no-graph", action="store_true", help="skip the HIP-graph replay measurement")
@@ -300,10 +306,31 @@ def main():
     from ompi_amd import recipe as ER
 
     recipe, count, desc = make_workload(args.config)
+    split = None
+    if args.strong:
+        # one message of the configuration's total size; each rank commits and moves its
+        # own part, resident in its own HBM, with no data-path collective
+        from ompi_amd import shard
+        if args.config == "cfg3":
+            count = 64
+            desc = dict(desc, workload="512^3 float subarray faces (dim0/dim1/dim2, start 511) as one "
+                                       "struct, 64 fields in total split by top-level count")
+        sp = shard.split_recipe(recipe, count, rank, world)
+        if sp is None:
+            raise SystemExit(f"no strong split for {args.config}")
+        split = {"total_count": count, "method": ("top-level count" if count > 1 else
+                                                  ("outer loop" if recipe[0] in ("vector", "hvector")
+                                                   else "index prefix"))}
+        recipe, count = sp[0], sp[1]
     dt = ER.build_committed(recipe)
     info = dt.info()
     S = info["size"] * count
     span, origin = layout(info, count)
+    S_total = S * world
+    if split and world > 1:
+        t_s = torch.tensor([S], device=dev if backend == "nccl" else "cpu", dtype=torch.int64)
+        dist.all_reduce(t_s)
+        S_total = int(t_s.item())
 
     user = torch.empty(span, dtype=torch.uint8, device=dev)
     user.copy_(torch.randint(1, 255, (span,), dtype=torch.uint8, device=dev))
@@ -398,20 +425,45 @@ def main():
         torch.cuda.synchronize()
         graph_step = g0.elapsed_time(g1) / 1e3 / args.steps
 
+    # The RCCL leg of SURVEY.md §8e, outside the timed region: a consumer that needs the
+    # whole packed stream on one device all-gathers the shards (backend "nccl" = RCCL over
+    # xGMI); every rank checks that its slice of the gathered stream is its own shard.
+    rccl = None
+    if world > 1 and not args.no_gather:
+        from ompi_amd import shard
+        g0 = time.perf_counter()
+        full = shard.gather_packed(packed if backend == "nccl" else packed.cpu())
+        torch.cuda.synchronize()
+        g_s = time.perf_counter() - g0
+        sizes = [torch.zeros(1, dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+                 for _ in range(world)]
+        dist.all_gather(sizes, torch.tensor([S], dtype=torch.int64, device=sizes[0].device))
+        off = sum(int(x.item()) for x in sizes[:rank])
+        ok = torch.tensor([1 if torch.equal(full[off:off + S].to(packed.device), packed) else 0],
+                          dtype=torch.int64, device=sizes[0].device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        rccl = {"backend": backend, "gathered_bytes": int(full.numel()), "ok": bool(ok.item()),
+                "seconds": round(g_s, 4)}
+        del full
+
     result = None
     if rank == 0:
         ms_per_step = wall / args.steps * 1e3
-        value = 2.0 * S * world * args.steps / wall / GiB
+        value = 2.0 * S_total * args.steps / wall / GiB
         achieved = 4.0 * S / (tp + tu)
         result = {
             "metric": "pack+unpack GiB/s/GPU (device-resident), 256^3 double 3D-vector; %HBM peak",
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "strong" if split else "weak", "vs_baseline": None,
             "dtype": "u8", "data": "synthetic",
             "config": dict(desc, config=args.config, packed_bytes_per_gpu=S,
-                           parallelism=f"replicas x{world} (fields sharded by count, no collective)"),
+                           parallelism=(f"strong split over {world} ranks by {split['method']} "
+                                        f"({split['total_count']} instances in total, no collective)"
+                                        if split else
+                                        f"replicas x{world} (fields sharded by count, no collective)")),
             "per_gpu_GiBs": round(2.0 * S / (tp + tu) / GiB, 3),
+            "all_gather_check": rccl,
             "kernel_ms": {"pack": round(tp * 1e3, 4), "unpack": round(tu * 1e3, 4)},
             "graph_replay_GiBs_per_gpu": (round(2.0 * S / graph_step / GiB, 3) if graph_step else None),
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 2), "peak": 8000.0,

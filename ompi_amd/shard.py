@@ -57,6 +57,59 @@ def pack_shard(dt, count: int, buf, rank: int, world: int, out, stream=None) -> 
     return pack_window(dt, n, addr(buf) + uoff, 0, out, n * size, stream=stream)
 
 
+def _engine_info(recipe):
+    from .recipe import build_committed
+    i = build_committed(recipe).info()
+    return i["size"], i["ub"] - i["lb"]
+
+
+def split_recipe(recipe, count: int, rank: int, world: int, info=_engine_info):
+    """This rank's share of a `count`-instance message of `recipe`, as a message of its own:
+    (recipe_r, count_r, user_offset, packed_offset).  Packing recipe_r x count_r at
+    buf + user_offset produces bytes [packed_offset, packed_offset + len) of the whole
+    message's stream, so the shards concatenate to it with no exchange.
+
+      count > 1             -> split the top-level count (instances first .. first+n)
+      vector / hvector x 1  -> split the outer loop (blocks first .. first+n)
+      indexed* x 1          -> split the index list by the prefix sum of block lengths
+    The reference's own precedent is ob1's multi-BTL scheduling, which hands each BTL a
+    byte range through opal_convertor_set_position (pml_ob1_sendreq.c:1184-1194).  Other
+    count-1 shapes return None: the caller shards the byte stream with position_shards and
+    windows (ddt_pack_window).  `info(recipe) -> (size, extent)`."""
+    if count > 1 or count == 0:
+        size, ext = info(recipe)
+        first, n = count_shards(count, world)[rank]
+        return recipe, n, first * ext, first * size
+    k = recipe[0]
+    if k in ("vector", "hvector"):
+        _, cnt, blen, stride, sub = recipe
+        ssize, sext = info(sub)
+        first, n = count_shards(cnt, world)[rank]
+        step = stride * sext if k == "vector" else stride
+        return (k, n, blen, stride, sub), 1, first * step, first * blen * ssize
+    if k in ("indexed_block", "hindexed_block"):
+        _, blen, disps, sub = recipe
+        ssize, _ = info(sub)
+        first, n = count_shards(len(disps), world)[rank]
+        return (k, blen, disps[first:first + n], sub), 1, 0, first * blen * ssize
+    if k in ("indexed", "hindexed"):
+        _, blens, disps, sub = recipe
+        ssize, _ = info(sub)
+        total = sum(blens)
+        # block boundaries nearest to r * total / world (prefix sum of lengths)
+        bounds, acc, r = [0], 0, 1
+        for i, b in enumerate(blens):
+            acc += b
+            while r < world and acc * world >= r * total:
+                bounds.append(i + 1)
+                r += 1
+        while len(bounds) < world + 1:
+            bounds.append(len(blens))
+        a, c = bounds[rank], bounds[rank + 1]
+        return (k, blens[a:c], disps[a:c], sub), 1, 0, sum(blens[:a]) * ssize
+    return None
+
+
 def gather_packed(local, group=None):
     """All-gather equal-size packed shards into the full stream (torch.distributed;
     backend 'nccl' is RCCL on ROCm).  `local` is a 1-D uint8 tensor; shards are padded to

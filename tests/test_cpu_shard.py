@@ -33,6 +33,56 @@ def test_position_shards():
                 assert all(a % g == 0 for a, n in s if n)
 
 
+def _oinfo(recipe):
+    from tests import recipes as R
+    i = R.Built(recipe).o.info()
+    return i["size"], i["ub"] - i["lb"]
+
+
+SPLIT_CASES = [
+    # count > 1: top-level count split (cfg2/cfg3 shape)
+    (("resized", ("vector", 16, 1, 8, ("basic", 16)), 0, 1024), 7),
+    # count 1: outer-loop split of an hvector of structs (cfg5 shape) and of a vector
+    (("hvector", 1001, 1, 32, ("struct", [1, 3], [0, 8], [("basic", 16), ("basic", 6)])), 1),
+    (("vector", 999, 3, 5, ("basic", 15)), 1),
+    # count 1: index-prefix split (cfg4 shape: unique LCG displacements) and variable lengths
+    (("indexed_block", 1, [(1664525 * i + 1013904223) % 4099 for i in range(1500)], ("basic", 15)), 1),
+    (("indexed", [1 + (i * 7) % 5 for i in range(800)], [i * 11 for i in range(800)], ("basic", 16)), 1),
+]
+
+
+@pytest.mark.parametrize("case", range(len(SPLIT_CASES)))
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_split_recipe_shards_concatenate_to_the_message(case, world):
+    """SURVEY.md §8e partitioning: each rank's (recipe, count, user offset) packs exactly
+    its byte range of the whole stream; the ranges tile the stream in rank order, and the
+    shards' unpacks together rebuild the whole unpack (oracle on both sides)."""
+    from tests import recipes as R
+    rec, count = SPLIT_CASES[case]
+    b = R.Built(rec)
+    info = b.o.info()
+    total = info["size"] * count
+    span, origin = R.layout(info, count)
+    host = R.fill(span, 9)
+    whole = b.o.pack(count, host, origin, 0, total, element_granular=False)
+    parts, pos = [], 0
+    out = np.full(span, 0xA5, dtype=np.uint8)
+    for r in range(world):
+        sr, n, uoff, poff = shard.split_recipe(rec, count, r, world, info=_oinfo)
+        assert poff == pos
+        sb = R.Built(sr)
+        ln = sb.o.info()["size"] * n
+        part = sb.o.pack(n, host, origin + uoff, 0, ln, element_granular=False) if ln else b""
+        parts.append(part)
+        if ln:
+            sb.o.unpack(n, out, origin + uoff, 0, part)
+        pos += ln
+    assert pos == total and b"".join(parts) == whole
+    want = np.full(span, 0xA5, dtype=np.uint8)
+    b.o.unpack(count, want, origin, 0, whole)
+    np.testing.assert_array_equal(out, want)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
