@@ -205,6 +205,11 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         } catch (const std::exception &ex) {
             return fail(DDT_ERR_OUT_OF_RESOURCE, ex.what());
         }
+        // every instance must keep the element alignment the address-ordered kernels load
+        // with (sorted_plan checked instance 0): a resized extent that is not a multiple of
+        // the element size sends instance i > 0 to the per-block kernel instead
+        if (SL && count > 1 && uint64_t(t->extent() < 0 ? -t->extent() : t->extent()) % SL->esz != 0)
+            SL = nullptr;
         if (SL) {
             const Leaf &L = P.leaves[0];
             for (uint64_t i = 0; i < count; ++i) {

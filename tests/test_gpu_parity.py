@@ -632,6 +632,20 @@ def test_sorted_list_engine(device, sorted_from, esz, count, density):
     assert st["sorted"] == 1 and st["chunks"] == (n + ch - 1) // ch, st
 
 
+def test_sorted_list_engine_misaligned_instances(device, sorted_from):
+    """count > 1 with a resized extent that is not a multiple of the
+    element size.  Instance 1 would start 2 bytes off the 4-byte element grid the
+    address-ordered kernels load with; the whole message must still be bit-exact (the
+    engine moves such a message with the per-block kernel)."""
+    sorted_from(1)
+    rng = np.random.default_rng(77)
+    n = (128 << 10) // 4 + 999
+    disps = rng.permutation(3 * n)[:n].astype(np.int64)
+    inner = ("indexed_block", 1, disps.tolist(), ("basic", 15))
+    b = R.Built(("resized", inner, 0, 4 * 3 * n + 2))
+    _roundtrip(b, 3, device, 31)
+
+
 def test_sorted_list_engine_falls_back(device, sorted_from):
     """Overlapping blocks, windows and misaligned buffers keep the per-block kernel (type-map
     order); a list of merged multi-element blocks still takes the engine.  All bit-exact."""
