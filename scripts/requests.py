@@ -8,9 +8,12 @@ read issues one RDREQ per 128 B line, a streaming store one 64 B WRREQ per 64 B;
 gather one RDREQ per element; an 8-byte scatter one WRREQ (not 64 B) per element, which the
 memory side completes as a read-modify-write of its sector.  So a step costs
     rd + wr + partial   memory-side operations,  partial = wr - wr64,
-and the highest request rate measured for any access pattern is a 16 B/lane streaming
-copy's: 4.19 M reads + 8.39 M writes in 204.0 us = 61.7 G requests/s (copy16); a pure
-streaming read reaches 45 G/s (read16: 4.19 M requests in 93.2 us).
+and the highest request rate measured for any access pattern is a streaming copy's.  Round 2
+re-measured that ceiling (scripts/ubench_copy.hip, profiles/r2_ubench_copy.log and
+profiles/r2_copy_requests.log): every copy variant issues one RDREQ per 128 B read and one
+64 B WRREQ per 64 B written (3B/128 requests for B bytes), and the fastest (16 KiB chunks,
+non-temporal loads and stores) copies at 6.2 TB/s r+w: 72.7 G requests/s.  (Round 1 quoted
+61.7 G/s from a slower 5.2 TB/s copy.)
 
 usage: python scripts/requests.py PMC.csv CONFIG > profiles/requests_CONFIG.json
 """
@@ -29,7 +32,7 @@ def family(kernel_name):
             return f
     return "move"
 
-CEILING = 61.7e9   # requests/s of a 16 B/lane streaming copy (copy16, ubench4)
+CEILING = 72.7e9   # requests/s of the 6.2 TB/s streaming copy (ubench_copy, r2)
 
 
 def main():
