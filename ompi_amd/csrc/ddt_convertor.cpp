@@ -484,11 +484,16 @@ int32_t advance(ddt_convertor *c, struct iovec *iov, uint32_t *out_size, size_t 
     std::vector<std::pair<Window, void *>> host;
     uint64_t pos = c->bConverted, total = 0;
     uint32_t used = 0;
+    // A NO_OP convertor (OPAL_CONVERTOR_PREPARE, opal_convertor.c:562-567: a type without
+    // gaps, or one contiguous instance) is moved by opal_convertor_pack's memcpy loop
+    // (:262-302), which fills every iovec to the byte; other types go through the movers,
+    // which never split a predefined element (_pack_accelerator.c:52-58).
+    const bool no_op = (c->dt->flags & F_NO_GAPS) || ((c->dt->flags & F_CONTIGUOUS) && c->count == 1);
     for (uint32_t i = 0; i < *out_size; ++i) {
         if (pos >= c->local_size)
             break;
         uint64_t w1 = std::min<uint64_t>(pos + iov[i].iov_len, c->local_size);
-        if (dir == 0 && w1 < c->local_size) {   // pack never splits a predefined element
+        if (dir == 0 && w1 < c->local_size && !no_op) {   // pack never splits a predefined element
             uint64_t s = snap_down_to_element(c->dt, w1);
             w1 = std::max(s, pos);
         }

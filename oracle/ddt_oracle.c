@@ -639,12 +639,20 @@ static void ort_locate(const ort_type *t, int64_t p, int64_t *inst, int64_t *run
  * instances at `base` into `out`.  Stops early rather than split a basic element
  * (opal_datatype_pack_accelerator.c:52-58).  Returns the bytes produced.
  */
+int64_t ort_pack_bytes(ort_type *t, int64_t count, const void *base, int64_t position, void *out,
+                       int64_t len);
+
 int64_t ort_pack(ort_type *t, int64_t count, const void *base, int64_t position, void *out,
                  int64_t len)
 {
     const int64_t total = count * t->size;
     if (t->size == 0 || position >= total || len <= 0)
         return 0;
+    /* a NO_OP convertor (OPAL_CONVERTOR_PREPARE, opal_convertor.c:562-567: no gaps, or one
+     * contiguous instance) is packed by opal_convertor_pack's memcpy loop (:262-302), which
+     * fills every iovec to the byte: no element snapping */
+    if ((t->flags & ORT_FLAG_NO_GAPS) || ((t->flags & ORT_FLAG_CONTIGUOUS) && count == 1))
+        return ort_pack_bytes(t, count, base, position, out, len);
     ort_prefix(t);
     const int64_t ext = ort_extent(t);
     int64_t inst, run, within, done = 0;

@@ -632,6 +632,37 @@ def test_sorted_list_engine(device, sorted_from, esz, count, density):
     assert st["sorted"] == 1 and st["chunks"] == (n + ch - 1) // ch, st
 
 
+@pytest.mark.parametrize("name", ["contig16", "adv_mixed_promote", "one_contig_instance"])
+def test_no_op_types_fill_fragments_to_the_byte(device, name):
+    """A convertor the reference marks NO_OP (OPAL_CONVERTOR_PREPARE, opal_convertor.c:
+    562-567: no gaps, or count 1 of a contiguous type) is packed by opal_convertor_pack's
+    memcpy loop (:262-302): every fragment is filled to the byte, elements split included
+    (adv_mixed_promote's int/float run, whose optimised carrier would be UINT8).  The
+    engine and the oracle both follow it; a gapped type still snaps to elements."""
+    import torch
+    import ompi_amd
+    recs = {"contig16": (("contig", 16, ("basic", 6)), 5),
+            "adv_mixed_promote": (_corpus.adv_mixed_promote()[0], 7),
+            "one_contig_instance": (("resized", ("contig", 5, ("basic", 16)), 0, 48), 1)}
+    rec, count = recs[name]
+    b = R.Built(rec)
+    info = b.o.info()
+    size = info["size"] * count
+    span, origin = R.layout(info, count)
+    host = R.fill(span, 3)
+    user = _dev(host, device)
+    packed = torch.zeros(size, dtype=torch.uint8, device=device)
+    conv = ompi_amd.Convertor().prepare_for_send(b.engine(), count, user.data_ptr() + origin)
+    pos, rc = 0, 0
+    while rc == 0:
+        cap = min(7, size - pos)
+        rc, _, md = conv.pack([(packed.data_ptr() + pos, cap)])
+        assert md == cap == len(b.o.pack(count, host, origin, pos, cap, element_granular=True))
+        pos += md
+    ref = np.frombuffer(b.o.pack(count, host, origin, 0, size, element_granular=False), dtype=np.uint8)
+    np.testing.assert_array_equal(_host(packed), ref)
+
+
 def test_sorted_list_engine_misaligned_instances(device, sorted_from):
     """count > 1 with a resized extent that is not a multiple of the
     element size.  Instance 1 would start 2 bytes off the 4-byte element grid the
