@@ -146,6 +146,12 @@ int ddt_type_info(const ddt_datatype_t *type, int64_t *out8);
 int ddt_type_from_opal_desc(const void *desc, size_t used, size_t size, ptrdiff_t lb, ptrdiff_t ub,
                             ptrdiff_t true_lb, ptrdiff_t true_ub, ddt_datatype_t **newtype);
 
+/* The inverse, for tests and tools: the uncommitted type map of `type` as dt_elem_desc_t
+ * entries (DATA per block run, LOOP/END_LOOP pairs, item counts as CREATE_LOOP_START/END
+ * write them, opal_datatype_internal.h:171-189), without the END_LOOP sentinel.  Returns the
+ * entry count, or minus the count needed when `cap` entries do not fit. */
+int64_t ddt_type_to_opal_desc(const ddt_datatype_t *type, void *out, size_t cap);
+
 /* ================= convertor (opal/datatype/opal_convertor.h) ================= */
 
 ddt_convertor_t *ddt_convertor_create(void);                   /* opal_convertor_create */

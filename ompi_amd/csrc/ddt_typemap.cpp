@@ -1261,6 +1261,83 @@ bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<
 }
 }  // namespace
 
+namespace {
+// One entry per DATA block run / LOOP marker of the uncommitted type map, in the
+// dt_elem_desc_t layout (opal_datatype_internal.h:119-169) the import reads.
+void put_entry(std::vector<unsigned char> &out, uint16_t flags, uint16_t type, uint32_t a, uint32_t b,
+               uint64_t c, int64_t d, int64_t e)
+{
+    unsigned char p[32] = {0};
+    std::memcpy(p, &flags, 2);
+    std::memcpy(p + 2, &type, 2);
+    std::memcpy(p + 4, &a, 4);
+    if (type == 0 || type == 1) {   // LOOP: items, loops, unused, extent; END_LOOP: items, unused, size, first disp
+        std::memcpy(p + 8, &b, 4);
+        std::memcpy(p + 16, &c, 8);
+        std::memcpy(p + 24, type == 0 ? &d : &e, 8);
+    } else {                        // DATA: count, blocklen, extent, disp
+        std::memcpy(p + 8, &c, 8);
+        std::memcpy(p + 16, &d, 8);
+        std::memcpy(p + 24, &e, 8);
+    }
+    out.insert(out.end(), p, p + 32);
+}
+
+bool export_nodes(const std::vector<Node> &nodes, std::vector<unsigned char> &out)
+{
+    for (const Node &n : nodes) {
+        switch (n.kind) {
+        case Node::DATA: {
+            const uint16_t type = n.tid ? n.tid : 9;   // a mixed run travels as UINT1 bytes
+            const uint64_t es = n.tid ? uint64_t(kSize[n.tid]) : 1;
+            if (n.count > 0xffffffffull || n.blen % es)
+                return false;
+            put_entry(out, uint16_t(F_DATA), type, uint32_t(n.count), 0, n.blen / es, n.extent, n.disp);
+            break;
+        }
+        case Node::LIST: {
+            const IndexList &X = *n.list;
+            const uint16_t type = n.tid ? n.tid : 9;
+            const uint64_t es = n.tid ? uint64_t(kSize[n.tid]) : 1;
+            for (size_t k = 0; k < X.nblk(); ++k) {
+                const uint64_t len = X.len.empty() ? X.ulen : X.len[k];
+                if (len % es)
+                    return false;
+                put_entry(out, uint16_t(F_DATA), type, 1, 0, len / es, int64_t(len), n.disp + X.disp[k]);
+            }
+            break;
+        }
+        case Node::LOOP: {
+            const size_t at = out.size();
+            put_entry(out, 0, 0, 0, uint32_t(n.count), ~uint64_t(0), n.extent, 0);
+            if (n.count > 0xffffffffull || !export_nodes(n.body, out))
+                return false;
+            const uint32_t items = uint32_t((out.size() - at) / 32);   // LOOP + body entries
+            std::memcpy(&out[at + 4], &items, 4);
+            put_entry(out, 0, 1, items, 0xffffffffu, n.body_size, 0, 0);
+            break;
+        }
+        }
+    }
+    return true;
+}
+}  // namespace
+
+int64_t ddt_type_to_opal_desc(const ddt_datatype_t *t, void *out, size_t cap)
+{
+    if (!t)
+        return DDT_ERR_BAD_PARAM;
+    std::vector<unsigned char> buf;
+    if (!export_nodes(t->desc, buf))
+        return DDT_ERR_NOT_SUPPORTED;
+    const size_t used = buf.size() / 32;
+    if (used > cap)
+        return -int64_t(used);
+    if (out && used)
+        std::memcpy(out, buf.data(), buf.size());
+    return int64_t(used);
+}
+
 int ddt_type_from_opal_desc(const void *desc, size_t used, size_t size, ptrdiff_t lb, ptrdiff_t ub,
                             ptrdiff_t true_lb, ptrdiff_t true_ub, ddt_datatype_t **out)
 {

@@ -116,6 +116,17 @@ class Datatype:
         check(lib().ddt_type_engine_info(self.handle, out), "ddt_type_engine_info")
         return dict(zip(("sorted", "device_bytes", "chunks", "slots"), list(out)))
 
+    def to_opal_desc(self) -> bytes:
+        """The uncommitted type map as Open MPI dt_elem_desc_t entries (ddt_type_to_opal_desc)."""
+        n = lib().ddt_type_to_opal_desc(self.handle, None, 0)
+        if n >= 0:
+            need = n
+        else:
+            need = -n
+        buf = ctypes.create_string_buffer(max(need, 1) * 32)
+        got = check(lib().ddt_type_to_opal_desc(self.handle, buf, need), "ddt_type_to_opal_desc")
+        return buf.raw[:got * 32]
+
     def cache_info(self) -> dict:
         """Descriptor-set cache of the plan (ddt_type_cache_info)."""
         out = (ctypes.c_int64 * 4)()

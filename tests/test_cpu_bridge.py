@@ -126,3 +126,27 @@ def test_flat_descriptions_of_corpus_types_import():
         rc = c.prepare(t, 2, 0x7000_0000_0000, send=True)
         assert rc == S.OPAL_SUCCESS, name
         t.destruct()
+
+
+def test_exported_descriptions_round_trip():
+    """ddt_type_to_opal_desc writes the uncommitted type map as dt_elem_desc_t entries
+    (LOOP/END_LOOP pairs as CREATE_LOOP_START/END make them); importing that description
+    gives the same type map as the oracle on 600 random recipes (every constructor, nesting
+    depth 3, negative strides, resized bounds)."""
+    import random
+    import numpy as np
+    from ompi_amd import datatype as D
+    from tests import plan_emu as E
+    rng = random.Random(2024)
+    loops = 0
+    for _ in range(600):
+        rec = R.random_recipe(rng)
+        b = R.Built(rec)
+        info = b.o.info()
+        if info["size"] == 0:
+            continue
+        desc = b.engine().to_opal_desc()
+        loops += any(desc[32 * i + 2] == 0 and desc[32 * i + 3] == 0 for i in range(len(desc) // 32))
+        t = D.from_opal_desc(desc, info["size"], info["lb"], info["ub"], info["true_lb"], info["true_ub"])
+        np.testing.assert_array_equal(E.engine_blocks(t), E.oracle_blocks(b.o))
+    assert loops > 50

@@ -307,6 +307,55 @@ def test_bridge_ddt_raw2_description(device):
     ot.destruct()
 
 
+# ------------------------------------------------------------------ fuzz through the bridge
+@pytest.mark.parametrize("seed", range(int(os.environ.get("DDT_BRIDGE_FUZZ_SEEDS", "3"))))
+def test_bridge_fuzz_descriptions(device, seed):
+    """Random recipes handed to the bridge as Open MPI descriptions in two forms -- the flat
+    one (one DATA entry per run of the oracle's type map) and the LOOP-structured one the
+    engine exports (ddt_type_to_opal_desc) -- packed in random fragments (element-granular
+    max_data == oracle) and unpacked in shuffled windows, counts 1-3; bytes == oracle."""
+    import torch
+    rng = random.Random(1000 + seed)
+    done = 0
+    while done < 20:
+        rec = R.random_recipe(rng)
+        b = R.Built(rec)
+        info = b.o.info()
+        count = rng.choice([1, 2, 3])
+        size = info["size"] * count
+        if size == 0 or size > (1 << 20):
+            continue
+        span, origin = R.layout(info, count)
+        host = R.fill(span, seed * 31 + done)
+        user = _dev(host, device)
+        ref = np.frombuffer(b.o.pack(count, host, origin, 0, size, element_granular=False), dtype=np.uint8)
+        overlap = _overlaps(b.o.runs(), count, info["ub"] - info["lb"])
+        flat = S.flat_from_oracle(b.o)
+        ents = b.engine().to_opal_desc()
+        looped = S.OpalType([ents[32 * i:32 * i + 32] for i in range(len(ents) // 32)], info["size"],
+                            info["lb"], info["ub"], info["true_lb"], info["true_ub"],
+                            flags=flat.dt.flags & (S.F_CONTIGUOUS | S.F_NO_GAPS))
+        for ot in (flat, looped):
+            packed = torch.zeros(size, dtype=torch.uint8, device=device)
+            conv = S.Convertor()
+            assert conv.prepare(ot, count, user.data_ptr() + origin, send=True) == S.OPAL_SUCCESS
+            exp = None if conv.c.flags & S.CONVERTOR_NO_OP else \
+                (lambda p, c: len(b.o.pack(count, host, origin, p, c, element_granular=True)))
+            wins = _pack_fragments(conv, packed.data_ptr(), size, rng.choice([5, 12, 40, 333, size]), exp,
+                                   limit=4096)
+            np.testing.assert_array_equal(_host(packed), ref)
+            if not overlap:
+                out = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
+                cu = S.Convertor()
+                cu.prepare(ot, count, out.data_ptr() + origin, send=False)
+                _unpack_windows(cu, packed.data_ptr(), wins, rng)
+                want = np.full(span, 0xA5, dtype=np.uint8)
+                b.o.unpack(count, want, origin, 0, ref.tobytes())
+                np.testing.assert_array_equal(_host(out), want)
+            ot.destruct()
+        done += 1
+
+
 # ------------------------------------------------------------------ async + staging
 def test_bridge_async_stream_host_fragments(device):
     """CONVERTOR_ACCELERATOR_ASYNC with convertor->stream (pml_ob1_recvfrag.c:761-769): the
