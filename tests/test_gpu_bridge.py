@@ -325,6 +325,12 @@ def test_bridge_fuzz_descriptions(device, seed):
         size = info["size"] * count
         if size == 0 or size > (1 << 20):
             continue
+        if (info["flags"] & S.F_NO_GAPS) and info["ub"] - info["lb"] != info["size"] and count > 1:
+            # a reference quirk, not a parity case: adding an empty sub-type moves lb/ub but
+            # returns before the flags are recomputed (opal_datatype_add.c:255, :285), so NO_GAPS
+            # survives with extent != size, and the NO_OP path (opal_convertor.c:262-302) would
+            # copy count*size contiguous bytes instead of the type map; the engine follows the map
+            continue
         span, origin = R.layout(info, count)
         host = R.fill(span, seed * 31 + done)
         user = _dev(host, device)
@@ -335,15 +341,18 @@ def test_bridge_fuzz_descriptions(device, seed):
         looped = S.OpalType([ents[32 * i:32 * i + 32] for i in range(len(ents) // 32)], info["size"],
                             info["lb"], info["ub"], info["true_lb"], info["true_ub"],
                             flags=flat.dt.flags & (S.F_CONTIGUOUS | S.F_NO_GAPS))
-        for ot in (flat, looped):
+        for form, ot in (("flat", flat), ("looped", looped)):
             packed = torch.zeros(size, dtype=torch.uint8, device=device)
             conv = S.Convertor()
             assert conv.prepare(ot, count, user.data_ptr() + origin, send=True) == S.OPAL_SUCCESS
             exp = None if conv.c.flags & S.CONVERTOR_NO_OP else \
                 (lambda p, c: len(b.o.pack(count, host, origin, p, c, element_granular=True)))
-            wins = _pack_fragments(conv, packed.data_ptr(), size, rng.choice([5, 12, 40, 333, size]), exp,
-                                   limit=4096)
-            np.testing.assert_array_equal(_host(packed), ref)
+            frag = rng.choice([5, 12, 40, 333, size])
+            wins = _pack_fragments(conv, packed.data_ptr(), size, frag, exp, limit=4096)
+            got = _host(packed)
+            bad = np.nonzero(got != ref)[0]
+            assert len(bad) == 0, (form, rec, count, frag, size, info, bad[:16].tolist(), len(bad),
+                                   wins[:8], (user.data_ptr() + origin) % 64, packed.data_ptr() % 64)
             if not overlap:
                 out = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
                 cu = S.Convertor()
