@@ -1334,6 +1334,8 @@ int ddt_tune(const char *key, long value)
         tuning().wt = value < 0 ? -1 : int(value > 2 ? 2 : value);
     else if (k == "hostdirect")
         tuning().hostdirect = int(value & 3);
+    else if (k == "sseg")
+        tuning().sseg = value == 128 ? 128 : 64;
     else if (k == "stage_mb")
         tuning().stage_mb = value < 1 ? 1 : value;
     else if (k == "snt")

@@ -283,12 +283,17 @@ SortedList *sorted_plan(const ddt_datatype *t, Plan &P, uint64_t user, hipStream
     const uint64_t min_blocks = knob > 0 ? uint64_t(knob) : (1ull << 20);
     const uint64_t g = X.disp_gcd | (X.len.empty() ? X.ulen : X.len_gcd);
     uint64_t esz = 0, ne = 0;
-    for (uint64_t e = 16; e >= 4 && !esz; e /= 2) {
-        const uint64_t ch = (128ull << 10) / e;
-        if (g % e == 0 && X.total / e <= 2 * ch * ch / (64 / e)) {
-            esz = e;
-            ne = X.total / e;
+    uint64_t segb = tuning().sseg == 128 ? 128 : 64;
+    for (int pass = 0; pass < 2 && !esz; ++pass) {
+        for (uint64_t e = 16; e >= 4 && !esz; e /= 2) {
+            const uint64_t ch = (128ull << 10) / e;
+            if (g % e == 0 && X.total / e <= 2 * ch * ch / (segb / e)) {
+                esz = e;
+                ne = X.total / e;
+            }
         }
+        if (!esz)
+            segb = 64;   // too many elements for the longer segments: the 64-byte form
     }
     if (!esz || nblk < min_blocks || X.total > 32 * nblk || !D.disp32) {
         P.sorted_state = -1;
@@ -331,7 +336,7 @@ SortedList *sorted_plan(const ddt_datatype *t, Plan &P, uint64_t user, hipStream
         auto S = std::make_unique<SortedList>();
         bool ok = false;
         try {
-            ok = S->build(ed, uint32_t(ne), uint32_t(esz), span_elems, stream);
+            ok = S->build(ed, uint32_t(ne), uint32_t(esz), span_elems, uint32_t(segb), stream);
         } catch (...) {
             if (tmp) (void) hipFree(tmp);
             throw;

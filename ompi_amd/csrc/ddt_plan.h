@@ -30,6 +30,7 @@ struct Tuning {
     int hostdirect = 3;   // pinned host iovecs moved by the kernel itself over PCIe (no HBM
                           // staging): bit 0 unpack, bit 1 pack (end to end)
     long stage_mb = 64;   // HBM staging slot (two per convertor) for pageable host iovecs
+    long sseg = 64;       // address-ordered engine: U segment bytes (64 or 128), read at plan build
 };
 Tuning &tuning();
 // Synchronous host -> device copy on a library-private stream (capture-safe).

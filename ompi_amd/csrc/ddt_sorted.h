@@ -13,7 +13,8 @@ struct SortedList {
     uint32_t n = 0;          // blocks (one element each)
     uint32_t esz = 0;        // element bytes: 4, 8 or 16
     uint32_t ch = 0;         // elements per chunk (address order) == per bucket (packed order)
-    uint32_t seg = 0;        // elements per 64-byte segment of U
+    uint32_t seg = 0;        // elements per segment of U
+    uint32_t segb = 64;      // segment bytes: 64 or 128
     uint32_t nc = 0, nb = 0; // chunks, buckets
     uint64_t slots = 0;      // U slots, runs padded to whole segments
     uint64_t dev_bytes = 0;  // device bytes held (tables + U)
@@ -33,7 +34,8 @@ struct SortedList {
     bool used = false;
     std::mutex mu;               // run() from several host threads: one launch sequence at a time
     ~SortedList();
-    bool build(const int32_t *disp, uint32_t n, uint32_t esz, uint64_t span_elems, hipStream_t stream);
+    bool build(const int32_t *disp, uint32_t n, uint32_t esz, uint64_t span_elems, uint32_t segb,
+               hipStream_t stream);
     // pol: access policy bits (POL_* in ddt_sorted.hip; ddt_tune "spol")
     hipError_t run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol, hipStream_t stream);
 };

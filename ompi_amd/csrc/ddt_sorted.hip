@@ -49,8 +49,10 @@ template <> struct Elem<16> { using T = u32x4; };
 constexpr int PT = 1024;               // threads per pass workgroup (16 wave64)
 constexpr int BT = 256;                // threads per build workgroup
 constexpr uint32_t LDS_BYTES = 128u << 10;
-constexpr uint32_t SEG_BYTES = 64;     // U runs are padded to whole segments of this many bytes
-                                       // (32 B segments: less padding, but cfg4 1461 -> 1512 us)
+// U runs are padded to whole segments of SEGB bytes (a plan's choice, SortedList::segb): 64 B
+// (round 1; 32 B segments: less padding, but cfg4 1461 -> 1512 us) or 128 B (round 2: half the
+// memory requests of the scattered run writes and reads, more padding; ddt_tune("sseg")).
+constexpr uint32_t SEG_DEFAULT = 64;
 constexpr uint16_t PAD = 0xFFFF;       // upos of a padding slot
 
 // Access policy bits of one run (SortedList::run, ddt_tune("spol")):
@@ -245,14 +247,14 @@ __device__ __forceinline__ void stage_tables(const uint16_t *__restrict__ off16,
 }
 
 // pack pass 1: gather the chunk in address order into LDS, emit its runs bucket by bucket
-template <int E>
+template <int E, int SEGB>
 __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, const AddrList al,
                                               const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
                                               const uint32_t *__restrict__ ub, uint8_t *__restrict__ U, uint32_t n,
                                               uint32_t nb, uint32_t pol)
 {
     using T = typename Elem<E>::T;
-    constexpr uint32_t CH = LDS_BYTES / E, SEG = SEG_BYTES / E;
+    constexpr uint32_t CH = LDS_BYTES / E, SEG = SEGB / E;
     const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS, ntu = pol & POL_USER_NTL;
     __shared__ T lds[CH + SEG];
     __shared__ uint16_t toff[MAXNB + 1];
@@ -373,14 +375,14 @@ __global__ __launch_bounds__(PT) void k_unpack2(const uint8_t *__restrict__ pack
 }
 
 // unpack pass 1': the chunk's runs into LDS, then scattered to the user side in address order
-template <int E>
+template <int E, int SEGB>
 __global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, const AddrList al,
                                                 const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
                                                 const uint32_t *__restrict__ ub, const uint8_t *__restrict__ U,
                                                 uint32_t n, uint32_t nb, uint32_t pol)
 {
     using T = typename Elem<E>::T;
-    constexpr uint32_t CH = LDS_BYTES / E, SEG = SEG_BYTES / E, NSUB = PT / SEG;
+    constexpr uint32_t CH = LDS_BYTES / E, SEG = SEGB / E, NSUB = PT / SEG;
     const bool ntl = pol & POL_STREAM_NTL, wt = pol & POL_USER_WT;
     __shared__ T lds[CH];
     __shared__ uint16_t toff[MAXNB + 1];
@@ -475,12 +477,14 @@ SortedList::~SortedList()
 // Build the plan on `stream` from the device displacement list (int32, relative to the
 // list's minimum displacement, every value a multiple of esz).  Returns false (and leaves
 // nothing allocated) when the displacements repeat.
-bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t span_elems, hipStream_t stream)
+bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t span_elems, uint32_t segb_,
+                       hipStream_t stream)
 {
     n = n_;
     esz = esz_;
+    segb = segb_ == 128 ? 128 : SEG_DEFAULT;
     ch = LDS_BYTES / esz;
-    seg = SEG_BYTES / esz;
+    seg = segb / esz;
     nc = (n + ch - 1) / ch;
     nb = nc;   // RG == CH
     uint32_t shift = 0;
@@ -591,20 +595,30 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol
     const dim3 gc(nc), gb(nb), blk(PT);
     const AddrList al{A, A16, Abase};
     uint8_t *u8 = static_cast<uint8_t *>(U);
-#define DDT_SORTED_LAUNCH(E)                                                                              \
-    if (dir == 0) {                                                                                       \
-        hipLaunchKernelGGL((k_pack1<E>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);   \
-        hipLaunchKernelGGL((k_pack2<E>), gb, blk, 0, stream, u8, upos, bstart, packed, n, pol);                \
-    } else {                                                                                              \
-        hipLaunchKernelGGL((k_unpack2<E>), gb, blk, 0, stream, packed, upos, bstart, u8, n, pol);              \
-        hipLaunchKernelGGL((k_unpack1<E>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol); \
+#define DDT_SORTED_LAUNCH(E, SB)                                                                                \
+    if (dir == 0) {                                                                                             \
+        hipLaunchKernelGGL((k_pack1<E, SB>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);     \
+        hipLaunchKernelGGL((k_pack2<E>), gb, blk, 0, stream, u8, upos, bstart, packed, n, pol);                 \
+    } else {                                                                                                    \
+        hipLaunchKernelGGL((k_unpack2<E>), gb, blk, 0, stream, packed, upos, bstart, u8, n, pol);               \
+        hipLaunchKernelGGL((k_unpack1<E, SB>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);   \
     }
-    if (esz == 4) {
-        DDT_SORTED_LAUNCH(4)
-    } else if (esz == 8) {
-        DDT_SORTED_LAUNCH(8)
+    if (segb == 128) {
+        if (esz == 4) {
+            DDT_SORTED_LAUNCH(4, 128)
+        } else if (esz == 8) {
+            DDT_SORTED_LAUNCH(8, 128)
+        } else {
+            DDT_SORTED_LAUNCH(16, 128)
+        }
     } else {
-        DDT_SORTED_LAUNCH(16)
+        if (esz == 4) {
+            DDT_SORTED_LAUNCH(4, 64)
+        } else if (esz == 8) {
+            DDT_SORTED_LAUNCH(8, 64)
+        } else {
+            DDT_SORTED_LAUNCH(16, 64)
+        }
     }
 #undef DDT_SORTED_LAUNCH
     hipError_t e = hipGetLastError();
