@@ -578,3 +578,17 @@ def test_descriptor_sets_follow_shape_not_buffers_and_survive_capture(device):
     torch.cuda.synchronize()
     for k in range(2):
         np.testing.assert_array_equal(_host(pks[k])[:100 * W], refs[k][:100 * W])
+
+
+def test_bridge_from_c(device):
+    """bridge/bridge_demo.c: the same drop-in driven from C on opal_datatype_t /
+    opal_convertor_t structs compiled against include/opal_layout.h -- prepare as
+    OPAL_CONVERTOR_PREPARE does, opal_hip_bridge_attach, fAdvance in 7000-byte fragments,
+    fPosition + fAdvance in 4099-byte windows last to first -- checked against the closed form
+    of the x face on the host."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(HERE), "bridge", "bridge_demo")
+    assert os.path.exists(exe), "build() compiles bridge/bridge_demo"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "bridge_demo ok" in r.stdout
