@@ -1339,7 +1339,7 @@ int ddt_tune(const char *key, long value)
     else if (k == "stage_mb")
         tuning().stage_mb = value < 1 ? 1 : value;
     else if (k == "snt")
-        tuning().snt = value < 0 ? -1 : (value ? 1 : 0);
+        tuning().snt = value < -1 ? -2 : (value < 0 ? -1 : (value >= 3 && value <= 5 ? int(value) : (value ? 1 : 0)));
     else if (k == "spass")
         tuning().spass = value < 1 ? 1 : value;
     else if (k == "reset")

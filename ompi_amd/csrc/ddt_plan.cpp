@@ -451,21 +451,25 @@ uint32_t use_wt(uint32_t U, uint64_t blen, const std::vector<LeafDim> *dims)
     return 1;
 }
 
-// Streaming leaves move every byte with non-temporal loads and stores when their blocks are
-// long contiguous runs (>= 64 KiB: z faces, planes): the chip's copy ceiling is 6.2 TB/s
-// r+w that way against 5.6-5.9 TB/s with default policies (scripts/ubench_copy.hip,
-// profiles/r2_ubench_copy.log); a z face of 512 fields went from 0.683 to 0.717 of 8 TB/s
-// pack+unpack.  Shorter runs (the y face's 2 KiB rows) measured slower with it (0.751 ->
-// 0.697), and so did the halo's pack (profiles/r2_ab_stream_policy.jsonl).
-// ddt_tune("snt") forces it for every leaf with blocks >= 256 B.
-bool use_snt(uint32_t U, uint64_t blen)
+// Cache policy of streaming leaves (16-byte units, blocks >= 256 B), Item::nt 2..5.  Measured
+// on single face types of 512 256^3-double fields (beyond the Infinity Cache), pack+unpack
+// loop (profiles/r2_ab_y_policy.log, r2_ab_z_policy.log, r2_ab_stream_nt_modes.jsonl):
+//   z face (512 KiB planes): non-temporal LOADS only (3): 0.818 of 8 TB/s, against 0.686
+//     plain and 0.717 with non-temporal loads and stores (2, the first round-2 rule);
+//   y face (2 KiB rows): non-temporal loads in the PACK only (5): 0.757, plain 0.716;
+//     non-temporal loads in the unpack too cost it 82 -> 90 us, stores 0.680.
+// The halo and cfg3 (x/dim-2 gathers in the same launch) move by <= 1 % either way.
+// ddt_tune("snt"): -1 this rule, -2 the first rule, 0 off, 1 / 3 / 4 / 5 forced.
+uint32_t use_snt(uint32_t U, uint64_t blen)   // Item::nt of a streaming leaf, 0 = none
 {
     const int force = tuning().snt;
     if (U != 16)
-        return false;
-    if (force >= 0)
-        return force == 1 && blen >= 256;
-    return blen >= (64u << 10);
+        return 0;
+    if (force >= 0)   // 1 both, 3 loads only, 4 stores only, 5 pack loads only
+        return force && blen >= 256 ? (force == 1 ? 2u : uint32_t(force)) : 0u;
+    if (force == -2)  // round-2 first rule: long runs every access non-temporal
+        return blen >= (64u << 10) ? 2u : 0u;
+    return blen >= (64u << 10) ? 3u : (blen >= 256 ? 5u : 0u);
 }
 
 uint64_t units_per_task(uint32_t U)
@@ -571,7 +575,7 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
             it.idx64 = (big || total_units >= 0xffffffffull) ? 1 : 0;
             if (u1 * U > leaf_total || total_units * U != leaf_total)
                 throw std::runtime_error("plan: affine unit range outside its leaf");
-            it.nt = use_snt(U, blen) ? 2 : (use_nt(U, blen, sd) ? 1 : 0);
+            it.nt = use_snt(U, blen) ? use_snt(U, blen) : (use_nt(U, blen, sd) ? 1 : 0);
             it.wt = use_wt(U, blen, &sd);
             it.u0 = u0;
             it.u1 = u1;
