@@ -6,7 +6,8 @@ FETCH_SIZE and WRITE_SIZE are KiB.  gfx950 correction: FETCH_SIZE tallies each 1
 request at 64 B (exactly half of a 16-B/lane streaming read, guide + our own calibration
 with scripts/kbench.py on a contiguous copy), so read bytes = 2 x FETCH_SIZE.  For the
 8-B x-face gathers one request per element is issued, so the same factor prices each at a
-128-B line.  WRITE_SIZE is taken as is (exact for streaming stores; scattered 8-B stores
+128-B line -- verified in round 2 (scripts/ubench_gran.hip, profiles/r2_ubench_gran.log): an
+8-byte gather per line costs the same request, FETCH_SIZE and time as a whole 128-byte line.  WRITE_SIZE is taken as is (exact for streaming stores; scattered 8-B stores
 are tallied as 32-B sectors, which is what the memory side receives).
 
 usage: python scripts/traffic.py FETCH.csv WRITE.csv CONFIG > profiles/traffic_CONFIG.json
