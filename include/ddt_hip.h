@@ -12,8 +12,9 @@
  * memory (hipMalloc / hipMallocManaged) -- this is the accelerator slot of the
  * convertor, selected by opal_convertor_prepare_for_{send,recv} when
  * check_addr reports a device pointer (opal_convertor.c:593-608).  The packed
- * iovec buffers may be device or host memory; host iovecs are staged through
- * HBM with hipMemcpyAsync.
+ * iovec buffers may be device or host memory: pinned host iovecs are read or
+ * written by the kernel itself over PCIe, pageable ones are staged through HBM
+ * slots with hipMemcpyAsync on a copy stream.
  */
 #ifndef DDT_HIP_H
 #define DDT_HIP_H
@@ -302,7 +303,14 @@ int64_t ddt_type_plan_list(const ddt_datatype_t *type, size_t leaf, int64_t *dis
  * (1, default) or always from the kernel-argument segment (0); "xcd" = mapping of workgroups to
  * tasks (-1, default: each XCD runs a contiguous slab of a streaming or line-dense leaf, sparse
  * gathers stay round-robin; 0: all round-robin; 1: all slabs); "xchunk" = tasks per XCD run for
- * slab items (0, default: one slab per XCD);
+ * slab items (0, default: one slab per XCD); "snt" = cache policy of streaming leaves (-1 auto,
+ * else an Item::nt mode 0-5); "spass" = workgroup passes per streaming task; "hostdirect" =
+ * pinned host iovecs moved by the kernel over PCIe (bit 0 unpack, bit 1 pack; 3 default, 0 =
+ * HBM staging); "hd_grid" / "hd_grid_pack" = workgroup cap of such an unpack / pack launch (256 / 0 default,
+ * 0 none); "stage_mb" =
+ * staging slot MiB for pageable host iovecs (read when a convertor first stages); "sseg" =
+ * address-ordered engine segment bytes (64 or 128); "sunroll" = its pack-1 elements per
+ * thread in flight (4, 8, 16 default);
  * "reset" = restore the defaults.
  * Environment: DDT_NT, DDT_TASK_KB, DDT_WT, DDT_XCD. */
 int ddt_tune(const char *key, long value);

@@ -165,7 +165,8 @@ void retire(Plan &P, const std::shared_ptr<ItemSet> &S)   // P.mu held
 // double-buffered halo, a fragment stream or the staging slots of a host pipeline hit the
 // same set whatever buffers they use.
 int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
-                const std::vector<Window> &wins, bool same_layout, int dir, hipStream_t stream)
+                const std::vector<Window> &wins, bool same_layout, int dir, hipStream_t stream,
+                uint32_t grid_cap = 0)
 {
     if (wins.empty())
         return DDT_SUCCESS;
@@ -216,7 +217,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                 uint8_t *u = reinterpret_cast<uint8_t *>(user + uint64_t(L.list_shift) + uint64_t(P.dev[0].disp_base)
                                                          + i * uint64_t(t->extent()));
                 uint8_t *pk = reinterpret_cast<uint8_t *>(wins[0].ptr + i * uint64_t(t->size));
-                HIPCHK(SL->run(u, pk, dir, uint32_t(tuning().spol), stream));
+                HIPCHK(SL->run(u, pk, dir, uint32_t(tuning().spol), stream, uint32_t(tuning().sunroll)));
             }
             return DDT_SUCCESS;
         }
@@ -300,10 +301,10 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         }
     }
     if (!d_items)
-        HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, ubase, pbase, stream));
+        HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, ubase, pbase, stream, grid_cap));
     else
         HIPCHK(launch_move(d_items, uint32_t(S->items.size()), S->ntasks, dir, S->has_lists, ubase, pbase,
-                           stream));
+                           stream, grid_cap));
     return DDT_SUCCESS;
 }
 
@@ -384,9 +385,14 @@ uint64_t stage_chunk(uint64_t slot, uint64_t done, uint64_t left)
 // Move the packed windows of a convertor call: device iovecs in one launch, host iovecs
 // through the HBM staging pipeline (kernel on the user stream, copies on copy_stream).
 int execute(ddt_convertor *c, const std::vector<Window> &dev_wins,
-            const std::vector<std::pair<Window, void *>> &host_wins, int dir)
+            const std::vector<std::pair<Window, void *>> &host_wins, int dir, bool pcie = false)
 {
-    int rc = run_windows(c->dt, *c->plan, c->count, c->base, dev_wins, false, dir, c->stream);
+    // a window in pinned host memory: PCIe is the limit, and a capped grid keeps the reads
+    // of an unpack at the link rate where thousands of workgroups contending for it lose 5 %
+    // (scripts/ubench_pcie.hip); a multiple of 8 keeps the XCD slab mapping
+    const long capv = dir == 0 ? tuning().hd_grid_pack : tuning().hd_grid;
+    const uint32_t cap = pcie ? uint32_t(std::max<long>(capv, 0) & ~7L) : 0;
+    int rc = run_windows(c->dt, *c->plan, c->count, c->base, dev_wins, false, dir, c->stream, cap);
     if (rc != DDT_SUCCESS)
         return rc;
     if (!host_wins.empty()) {
@@ -484,6 +490,7 @@ int32_t advance(ddt_convertor *c, struct iovec *iov, uint32_t *out_size, size_t 
     std::vector<std::pair<Window, void *>> host;
     uint64_t pos = c->bConverted, total = 0;
     uint32_t used = 0;
+    bool pcie = false;
     // A NO_OP convertor (OPAL_CONVERTOR_PREPARE, opal_convertor.c:562-567: a type without
     // gaps, or one contiguous instance) is moved by opal_convertor_pack's memcpy loop
     // (:262-302), which fills every iovec to the byte; other types go through the movers,
@@ -506,15 +513,17 @@ int32_t advance(ddt_convertor *c, struct iovec *iov, uint32_t *out_size, size_t 
             uint64_t hd = 0;
             if (classify(iov[i].iov_base) == MEM_DEVICE)
                 dev.push_back({pos, w1, uint64_t(uintptr_t(iov[i].iov_base))});
-            else if ((tuning().hostdirect & (dir == 0 ? 2 : 1)) && (hd = pinned_device_range(iov[i].iov_base, n)) != 0)
+            else if ((tuning().hostdirect & (dir == 0 ? 2 : 1)) && (hd = pinned_device_range(iov[i].iov_base, n)) != 0) {
                 dev.push_back({pos, w1, hd});   // the kernel reads/writes the pinned pages over PCIe
+                pcie = true;
+            }
             else
                 host.push_back({{pos, w1, 0}, iov[i].iov_base});
         }
         pos = w1;
         total += n;
     }
-    int rc = execute(c, dev, host, dir);
+    int rc = execute(c, dev, host, dir, pcie);
     if (rc != DDT_SUCCESS)
         return rc;
     c->bConverted = pos;
@@ -1334,6 +1343,12 @@ int ddt_tune(const char *key, long value)
         tuning().wt = value < 0 ? -1 : int(value > 2 ? 2 : value);
     else if (k == "hostdirect")
         tuning().hostdirect = int(value & 3);
+    else if (k == "hd_grid")
+        tuning().hd_grid = value < 0 ? 0 : value;
+    else if (k == "hd_grid_pack")
+        tuning().hd_grid_pack = value < 0 ? 0 : value;
+    else if (k == "sunroll")
+        tuning().sunroll = value >= 16 ? 16 : (value >= 8 ? 8 : 4);
     else if (k == "sseg")
         tuning().sseg = value == 128 ? 128 : 64;
     else if (k == "stage_mb")

@@ -99,7 +99,7 @@ constexpr uint32_t INLINE_ITEMS = 7;
 template <uint32_t NI>
 struct ItemBlockN {
     uint32_t n;
-    uint32_t pad;
+    uint32_t ntasks;        // tasks of the launch (a capped grid loops over them)
     uint64_t ubase, pbase;  // the launch's base pointers (Item::user / Item::packed are relative)
     uint64_t pad2;
     Item items[NI];

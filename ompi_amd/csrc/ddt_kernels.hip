@@ -404,9 +404,8 @@ __device__ __forceinline__ void dispatch_list_uni(const Item *it, Bases bs, uint
 // LISTS = false: affine + fragment items only (vector/hvector/subarray/struct nests), a
 // lean register budget; LISTS = true adds the index-list paths.
 template <int DIR, bool LISTS>
-__device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32_t nitems, Bases bs)
+__device__ __forceinline__ void move_task(const Item *__restrict__ items, uint32_t nitems, Bases bs, uint32_t b)
 {
-    const uint32_t b = blockIdx.x;
     uint32_t lo = 0, hi = nitems - 1;
     while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
@@ -489,11 +488,26 @@ __device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32
     }
 }
 
+// One workgroup per task, or -- when the launch is capped below the task count (a window
+// in pinned host memory, where PCIe and not the CU count is the limit: a few hundred
+// workgroups keep it full, thousands of them contend for it, scripts/ubench_pcie.hip) --
+// a grid-stride loop over the tasks.  A cap that is a multiple of 8 keeps every task on
+// the XCD the slab mapping chose for it.
+template <int DIR, bool LISTS>
+__device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32_t nitems, Bases bs, uint32_t ntasks)
+{
+    for (uint32_t b = blockIdx.x; b < ntasks; b += gridDim.x) {
+        if (b != blockIdx.x)
+            __syncthreads();   // LDS of the previous task (list scans) is free again
+        move_task<DIR, LISTS>(items, nitems, bs, b);
+    }
+}
+
 template <int DIR, bool LISTS>
 __global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restrict__ items, uint32_t nitems,
-                                                           uint64_t ubase, uint64_t pbase)
+                                                           uint64_t ubase, uint64_t pbase, uint32_t ntasks)
 {
-    move_body<DIR, LISTS>(items, nitems, Bases{ubase, pbase});
+    move_body<DIR, LISTS>(items, nitems, Bases{ubase, pbase}, ntasks);
 }
 
 // Small launches carry their descriptors in the kernel-argument segment: no device
@@ -505,69 +519,72 @@ __global__ __launch_bounds__(THREADS) void ddt_move_inline_kernel(ItemBlockN<NI>
     // would copy it to scratch)
     const ItemBlockN<NI> *kb = reinterpret_cast<const ItemBlockN<NI> *>(
         (const void *) __builtin_amdgcn_kernarg_segment_ptr());
-    move_body<DIR, LISTS>(kb->items, kb->n, Bases{kb->ubase, kb->pbase});
+    move_body<DIR, LISTS>(kb->items, kb->n, Bases{kb->ubase, kb->pbase}, kb->ntasks);
 }
 
 template <int DIR, bool LISTS, uint32_t NI>
-static void launch_inline_n(const ItemBlock &blk, uint32_t ntasks, uint64_t ubase, uint64_t pbase,
-                            hipStream_t stream)
+static void launch_inline_n(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, uint64_t ubase,
+                            uint64_t pbase, hipStream_t stream)
 {
     ItemBlockN<NI> b;
     b.n = blk.n;
+    b.ntasks = ntasks;
     b.ubase = ubase;
     b.pbase = pbase;
     for (uint32_t i = 0; i < blk.n; ++i)
         b.items[i] = blk.items[i];
-    hipLaunchKernelGGL((ddt_move_inline_kernel<DIR, LISTS, NI>), dim3(ntasks), dim3(THREADS), 0,
+    hipLaunchKernelGGL((ddt_move_inline_kernel<DIR, LISTS, NI>), dim3(grid), dim3(THREADS), 0,
                        stream, b);
 }
 
 template <int DIR, bool LISTS>
-static void launch_inline(const ItemBlock &blk, uint32_t ntasks, uint64_t ubase, uint64_t pbase,
+static void launch_inline(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, uint64_t ubase, uint64_t pbase,
                           hipStream_t stream)
 {
-    if (blk.n == 1) launch_inline_n<DIR, LISTS, 1>(blk, ntasks, ubase, pbase, stream);
-    else if (blk.n == 2) launch_inline_n<DIR, LISTS, 2>(blk, ntasks, ubase, pbase, stream);
-    else if (blk.n <= 4) launch_inline_n<DIR, LISTS, 4>(blk, ntasks, ubase, pbase, stream);
-    else launch_inline_n<DIR, LISTS, INLINE_ITEMS>(blk, ntasks, ubase, pbase, stream);
+    if (blk.n == 1) launch_inline_n<DIR, LISTS, 1>(blk, ntasks, grid, ubase, pbase, stream);
+    else if (blk.n == 2) launch_inline_n<DIR, LISTS, 2>(blk, ntasks, grid, ubase, pbase, stream);
+    else if (blk.n <= 4) launch_inline_n<DIR, LISTS, 4>(blk, ntasks, grid, ubase, pbase, stream);
+    else launch_inline_n<DIR, LISTS, INLINE_ITEMS>(blk, ntasks, grid, ubase, pbase, stream);
 }
 
 template <int DIR>
-static void launch_dir(const Item *d_items, uint32_t nitems, uint32_t ntasks, bool lists, uint64_t ubase,
-                       uint64_t pbase, hipStream_t stream)
+static void launch_dir(const Item *d_items, uint32_t nitems, uint32_t ntasks, uint32_t grid, bool lists,
+                       uint64_t ubase, uint64_t pbase, hipStream_t stream)
 {
     if (lists)
-        hipLaunchKernelGGL((ddt_move_kernel<DIR, true>), dim3(ntasks), dim3(THREADS), 0, stream,
-                           d_items, nitems, ubase, pbase);
+        hipLaunchKernelGGL((ddt_move_kernel<DIR, true>), dim3(grid), dim3(THREADS), 0, stream,
+                           d_items, nitems, ubase, pbase, ntasks);
     else
-        hipLaunchKernelGGL((ddt_move_kernel<DIR, false>), dim3(ntasks), dim3(THREADS), 0, stream,
-                           d_items, nitems, ubase, pbase);
+        hipLaunchKernelGGL((ddt_move_kernel<DIR, false>), dim3(grid), dim3(THREADS), 0, stream,
+                           d_items, nitems, ubase, pbase, ntasks);
 }
 
 hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, uint64_t ubase,
-                              uint64_t pbase, hipStream_t stream)
+                              uint64_t pbase, hipStream_t stream, uint32_t grid_cap)
 {
     if (ntasks == 0 || blk.n == 0)
         return hipSuccess;
+    const uint32_t g = grid_cap && grid_cap < ntasks ? grid_cap : ntasks;
     if (dir == 0) {
-        if (lists) launch_inline<0, true>(blk, ntasks, ubase, pbase, stream);
-        else launch_inline<0, false>(blk, ntasks, ubase, pbase, stream);
+        if (lists) launch_inline<0, true>(blk, ntasks, g, ubase, pbase, stream);
+        else launch_inline<0, false>(blk, ntasks, g, ubase, pbase, stream);
     } else {
-        if (lists) launch_inline<1, true>(blk, ntasks, ubase, pbase, stream);
-        else launch_inline<1, false>(blk, ntasks, ubase, pbase, stream);
+        if (lists) launch_inline<1, true>(blk, ntasks, g, ubase, pbase, stream);
+        else launch_inline<1, false>(blk, ntasks, g, ubase, pbase, stream);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
-                       uint64_t ubase, uint64_t pbase, hipStream_t stream)
+                       uint64_t ubase, uint64_t pbase, hipStream_t stream, uint32_t grid_cap)
 {
     if (ntasks == 0 || nitems == 0)
         return hipSuccess;
+    const uint32_t g = grid_cap && grid_cap < ntasks ? grid_cap : ntasks;
     if (dir == 0)
-        launch_dir<0>(d_items, nitems, ntasks, lists, ubase, pbase, stream);
+        launch_dir<0>(d_items, nitems, ntasks, g, lists, ubase, pbase, stream);
     else
-        launch_dir<1>(d_items, nitems, ntasks, lists, ubase, pbase, stream);
+        launch_dir<1>(d_items, nitems, ntasks, g, lists, ubase, pbase, stream);
     return hipGetLastError();
 }
 

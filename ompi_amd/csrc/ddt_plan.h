@@ -30,6 +30,11 @@ struct Tuning {
     int hostdirect = 3;   // pinned host iovecs moved by the kernel itself over PCIe (no HBM
                           // staging): bit 0 unpack, bit 1 pack (end to end)
     long stage_mb = 64;   // HBM staging slot (two per convertor) for pageable host iovecs
+    long hd_grid = 256;   // workgroup cap of an unpack launch reading pinned host memory (0 = none):
+                          // PCIe reads lose rate to thousands of workgroups, writes do not
+                          // (scripts/ubench_pcie.hip, profiles/r2_ubench_pcie.log)
+    long hd_grid_pack = 0;   // the same cap for a pack writing pinned host memory
+    long sunroll = 16;    // address-ordered engine: pack 1 elements per thread in flight (4, 8, 16)
     long sseg = 64;       // address-ordered engine: U segment bytes (64 or 128), read at plan build
 };
 Tuning &tuning();
@@ -47,10 +52,11 @@ bool use_slab(const Item &it);
 uint32_t total_tasks(const std::vector<Item> &items);
 
 // ddt_kernels.hip: dir 0 = pack / typed copy (user side -> packed side), 1 = unpack.
+// grid_cap > 0: at most that many workgroups, looping over the tasks (host-direct windows)
 hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, uint64_t ubase,
-                              uint64_t pbase, hipStream_t stream);
+                              uint64_t pbase, hipStream_t stream, uint32_t grid_cap = 0);
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
-                       uint64_t ubase, uint64_t pbase, hipStream_t stream);
+                       uint64_t ubase, uint64_t pbase, hipStream_t stream, uint32_t grid_cap = 0);
 
 // external32 conversion between a native packed stream and its big-endian form.
 hipError_t launch_ext(const ConvSeg *segs, uint32_t nseg, const ConvRun *runs, uint64_t E,

@@ -37,7 +37,9 @@ struct SortedList {
     bool build(const int32_t *disp, uint32_t n, uint32_t esz, uint64_t span_elems, uint32_t segb,
                hipStream_t stream);
     // pol: access policy bits (POL_* in ddt_sorted.hip; ddt_tune "spol")
-    hipError_t run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol, hipStream_t stream);
+    // unroll: elements per thread in flight in pack 1's address-ordered gather (4, 8 or 16)
+    hipError_t run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol, hipStream_t stream,
+                   uint32_t unroll = 16);
 };
 
 }  // namespace ddt

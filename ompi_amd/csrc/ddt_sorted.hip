@@ -60,6 +60,10 @@ constexpr uint32_t POL_USER_WT = 1;    // unpack 1': user-side stores written th
 constexpr uint32_t POL_STREAM_NTS = 2; // stores of U and of the packed side non-temporal
 constexpr uint32_t POL_STREAM_NTL = 4; // loads of A, SL, U, upos and the packed side non-temporal
 constexpr uint32_t POL_USER_NTL = 8;   // pack 1: user-side loads non-temporal
+// timing-only bits (wrong results; scripts/ab.py phase breakdowns): skip the user-side phase
+// of pass 1 / 1' (the address-ordered gather or scatter), or its run phase (emit or load runs)
+constexpr uint32_t POL_SKIP_USER = 16;
+constexpr uint32_t POL_SKIP_RUNS = 32;
 
 template <typename T> __device__ __forceinline__ T ldp(const T *p, bool nt)
 {
@@ -246,8 +250,25 @@ __device__ __forceinline__ void stage_tables(const uint16_t *__restrict__ off16,
         toff[nb] = uint16_t(m);   // m <= CH <= 32 Ki
 }
 
-// pack pass 1: gather the chunk in address order into LDS, emit its runs bucket by bucket
+// pack pass 1, second phase: the chunk image's runs out to U, bucket by bucket
 template <int E, int SEGB>
+__device__ __forceinline__ void emit_runs(const typename Elem<E>::T *lds, const uint16_t *toff, const uint32_t *tub,
+                                          uint8_t *__restrict__ U, uint32_t nb, bool nts)
+{
+    using T = typename Elem<E>::T;
+    constexpr uint32_t SEG = SEGB / E;
+    T *dst = reinterpret_cast<T *>(U);
+    const uint32_t sub = threadIdx.x / SEG, lane = threadIdx.x % SEG;
+    for (uint32_t k = sub; k < nb; k += PT / SEG) {
+        const uint32_t o = toff[k], cn = toff[k + 1] - o;
+        const uint32_t b = tub[k], pn = (cn + SEG - 1) / SEG * SEG;
+        for (uint32_t q = lane; q < pn; q += SEG)
+            stp(&dst[b + q], lds[o + q], nts);   // padding slots carry a neighbour's bytes: whole segments
+    }
+}
+
+// pack pass 1: gather the chunk in address order into LDS, emit its runs bucket by bucket
+template <int E, int SEGB, int K>
 __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, const AddrList al,
                                               const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
                                               const uint32_t *__restrict__ ub, uint8_t *__restrict__ U, uint32_t n,
@@ -263,8 +284,10 @@ __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, 
     const uint32_t m = min(CH, n - j0);
     stage_tables<E>(off16, ub, c, nb, m, toff, tub);
     const T *src = reinterpret_cast<const T *>(user);
-    constexpr int K = 4;
-    for (uint32_t t0 = threadIdx.x; t0 < m; t0 += PT * K) {
+    // K elements per thread in flight: each is a dependent pair (offset, then the user
+    // element), so K sets how many of the chunk's CH / PT per thread share one latency
+    const uint32_t mg = (pol & POL_SKIP_USER) ? 0u : m;
+    for (uint32_t t0 = threadIdx.x; t0 < mg; t0 += PT * K) {
         T v[K];
         uint32_t s[K];
 #pragma unroll
@@ -281,14 +304,7 @@ __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, 
                 lds[s[q]] = v[q];
     }
     __syncthreads();
-    T *dst = reinterpret_cast<T *>(U);
-    const uint32_t sub = threadIdx.x / SEG, lane = threadIdx.x % SEG;
-    for (uint32_t k = sub; k < nb; k += PT / SEG) {
-        const uint32_t o = toff[k], cn = toff[k + 1] - o;
-        const uint32_t b = tub[k], pn = (cn + SEG - 1) / SEG * SEG;
-        for (uint32_t q = lane; q < pn; q += SEG)
-            stp(&dst[b + q], lds[o + q], nts);   // padding slots carry a neighbour's bytes: whole segments
-    }
+    emit_runs<E, SEGB>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, nts);
 }
 
 // pack pass 2: the bucket's runs scatter into LDS by destination, then stream out
@@ -374,30 +390,21 @@ __global__ __launch_bounds__(PT) void k_unpack2(const uint8_t *__restrict__ pack
     }
 }
 
-// unpack pass 1': the chunk's runs into LDS, then scattered to the user side in address order
+// unpack pass 1', first phase: the chunk's runs from U into the LDS chunk image
 template <int E, int SEGB>
-__global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, const AddrList al,
-                                                const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
-                                                const uint32_t *__restrict__ ub, const uint8_t *__restrict__ U,
-                                                uint32_t n, uint32_t nb, uint32_t pol)
+__device__ __forceinline__ void load_runs(typename Elem<E>::T *lds, const uint16_t *toff, const uint32_t *tub,
+                                          const uint8_t *__restrict__ U, uint32_t nb, bool ntl)
 {
     using T = typename Elem<E>::T;
-    constexpr uint32_t CH = LDS_BYTES / E, SEG = SEGB / E, NSUB = PT / SEG;
-    const bool ntl = pol & POL_STREAM_NTL, wt = pol & POL_USER_WT;
-    __shared__ T lds[CH];
-    __shared__ uint16_t toff[MAXNB + 1];
-    __shared__ uint32_t tub[MAXNB];
-    const uint32_t c = blockIdx.x, j0 = c * CH;
-    const uint32_t m = min(CH, n - j0);
-    stage_tables<E>(off16, ub, c, nb, m, toff, tub);
-    __syncthreads();
+    constexpr uint32_t SEG = SEGB / E, NSUB = PT / SEG;
     const T *src = reinterpret_cast<const T *>(U);
-    const uint32_t sub = threadIdx.x / SEG, lane = threadIdx.x % SEG;
-    // B runs per round: their first segments are loaded before any is stored (ILP); the
-    // rarer second and later segments follow
+    // B runs per round: their first two segments are loaded before any is stored (ILP: a
+    // run averages one segment, so about half of them have a second); the rare third and
+    // later segments follow
     constexpr int B = 8;
+    const uint32_t sub = threadIdx.x / SEG, lane = threadIdx.x % SEG;
     for (uint32_t kb = sub; kb < nb; kb += NSUB * B) {
-        T v[B];
+        T v[B], w[B];
         uint32_t o[B], cn[B], bb[B];
 #pragma unroll
         for (int i = 0; i < B; ++i) {
@@ -409,21 +416,46 @@ __global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, cons
                 bb[i] = tub[k];
                 if (lane < cn[i])
                     v[i] = ldp(&src[bb[i] + lane], ntl);
+                if (lane + SEG < cn[i])
+                    w[i] = ldp(&src[bb[i] + lane + SEG], ntl);
             }
         }
 #pragma unroll
-        for (int i = 0; i < B; ++i)
+        for (int i = 0; i < B; ++i) {
             if (lane < cn[i])
                 lds[o[i] + lane] = v[i];
+            if (lane + SEG < cn[i])
+                lds[o[i] + lane + SEG] = w[i];
+        }
 #pragma unroll
         for (int i = 0; i < B; ++i)
-            for (uint32_t q = lane + SEG; q < cn[i]; q += SEG)
+            for (uint32_t q = lane + 2 * SEG; q < cn[i]; q += SEG)
                 lds[o[i] + q] = src[bb[i] + q];
     }
+}
+
+// unpack pass 1': the chunk's runs into LDS, then scattered to the user side in address order
+template <int E, int SEGB, int K>
+__global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, const AddrList al,
+                                                const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
+                                                const uint32_t *__restrict__ ub, const uint8_t *__restrict__ U,
+                                                uint32_t n, uint32_t nb, uint32_t pol)
+{
+    using T = typename Elem<E>::T;
+    constexpr uint32_t CH = LDS_BYTES / E;
+    const bool ntl = pol & POL_STREAM_NTL, wt = pol & POL_USER_WT;
+    __shared__ T lds[CH];
+    __shared__ uint16_t toff[MAXNB + 1];
+    __shared__ uint32_t tub[MAXNB];
+    const uint32_t c = blockIdx.x, j0 = c * CH;
+    const uint32_t m = min(CH, n - j0);
+    stage_tables<E>(off16, ub, c, nb, m, toff, tub);
+    __syncthreads();
+    load_runs<E, SEGB>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, ntl);
     __syncthreads();
     T *dst = reinterpret_cast<T *>(user);
-    constexpr int K = 4;
-    for (uint32_t t0 = threadIdx.x; t0 < m; t0 += PT * K) {
+    const uint32_t ms = (pol & POL_SKIP_USER) ? 0u : m;
+    for (uint32_t t0 = threadIdx.x; t0 < ms; t0 += PT * K) {
         uint32_t a[K];
         T v[K];
 #pragma unroll
@@ -583,7 +615,11 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
 
 // One whole-list pack (dir 0) or unpack (dir 1) of one instance.  `user` points at the
 // list's first element (minimum displacement), `packed` at the instance's packed bytes.
-hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol, hipStream_t stream)
+// `unroll`: elements per thread in flight in pack 1's address-ordered gather (4, 8, 16).  cfg4
+// A/B (profiles/r2_ab_sorted_unroll.log): pack 656 / 617 / 612 us; unpack 1' keeps 4 (its
+// scatter has one dependent load per element; 8 and 16 measured slower, 804 -> 818 / 842 us).
+hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol, hipStream_t stream,
+                           uint32_t unroll)
 {
     // U is one scratch per plan: a launch on another stream waits for the last one
     std::lock_guard<std::mutex> g(mu);
@@ -595,13 +631,23 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol
     const dim3 gc(nc), gb(nb), blk(PT);
     const AddrList al{A, A16, Abase};
     uint8_t *u8 = static_cast<uint8_t *>(U);
-#define DDT_SORTED_LAUNCH(E, SB)                                                                                \
+#define DDT_SORTED_LAUNCH_K(E, SB, K)                                                                           \
     if (dir == 0) {                                                                                             \
-        hipLaunchKernelGGL((k_pack1<E, SB>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);     \
+        hipLaunchKernelGGL((k_pack1<E, SB, K>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);  \
         hipLaunchKernelGGL((k_pack2<E>), gb, blk, 0, stream, u8, upos, bstart, packed, n, pol);                 \
     } else {                                                                                                    \
         hipLaunchKernelGGL((k_unpack2<E>), gb, blk, 0, stream, packed, upos, bstart, u8, n, pol);               \
-        hipLaunchKernelGGL((k_unpack1<E, SB>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);   \
+        hipLaunchKernelGGL((k_unpack1<E, SB, 4>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);\
+    }
+// K * E <= 64 bytes of elements per thread in flight: wider elements at K = 16 (or 16-byte
+// ones at 8) exceed the 128 VGPRs of a 1024-thread workgroup and spill
+#define DDT_SORTED_LAUNCH(E, SB)                                                                                \
+    if (unroll >= 16 && E == 4) {                                                                               \
+        DDT_SORTED_LAUNCH_K(E, SB, (E == 4 ? 16 : 4))                                                           \
+    } else if (unroll >= 8 && E <= 8) {                                                                         \
+        DDT_SORTED_LAUNCH_K(E, SB, (E <= 8 ? 8 : 4))                                                            \
+    } else {                                                                                                    \
+        DDT_SORTED_LAUNCH_K(E, SB, 4)                                                                           \
     }
     if (segb == 128) {
         if (esz == 4) {
@@ -621,6 +667,7 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol
         }
     }
 #undef DDT_SORTED_LAUNCH
+#undef DDT_SORTED_LAUNCH_K
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;

@@ -40,7 +40,9 @@ def _overlapping(otype, count):
     return False
 
 
-def _roundtrip(b: R.Built, count: int, device, seed: int, frags=None):
+def _roundtrip(b: R.Built, count: int, device, seed: int, frags=None, shift=0):
+    """Pack and unpack `count` instances against the oracle; `shift` offsets the user
+    buffer by that many bytes from the allocation's (256-byte aligned) start."""
     import torch
     import ompi_amd
     info = b.o.info()
@@ -49,16 +51,18 @@ def _roundtrip(b: R.Built, count: int, device, seed: int, frags=None):
         return
     span, origin = R.layout(info, count)
     host = R.fill(span, seed)
-    user = _dev(host, device)
+    pad = np.zeros(16, dtype=np.uint8)
+    user = _dev(np.concatenate([pad[:shift], host, pad]), device)
+    uptr = user.data_ptr() + shift + origin
     e = b.engine()
     ref = np.frombuffer(b.o.pack(count, host, origin, 0, size, element_granular=False), dtype=np.uint8)
     packed = torch.zeros(size, dtype=torch.uint8, device=device)
     if frags is None:
-        pos = ompi_amd.pack(user.data_ptr() + origin, count, e, packed, size, 0)
+        pos = ompi_amd.pack(uptr, count, e, packed, size, 0)
         assert pos == size
     else:
         # convertor with fragments: pack never splits a predefined element
-        conv = ompi_amd.Convertor().prepare_for_send(e, count, user.data_ptr() + origin)
+        conv = ompi_amd.Convertor().prepare_for_send(e, count, uptr)
         done, opos, rc = 0, 0, 0
         while rc == 0:
             ln = frags[done % len(frags)]
@@ -75,13 +79,14 @@ def _roundtrip(b: R.Built, count: int, device, seed: int, frags=None):
     np.testing.assert_array_equal(got, ref)
     if _overlapping(b.o, count):
         return
-    out = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
-    exp = np.full(span, 0xA5, dtype=np.uint8)
-    b.o.unpack(count, exp, origin, 0, ref.tobytes())
+    out = torch.full((shift + span + 16,), 0xA5, dtype=torch.uint8, device=device)
+    exp = np.full(shift + span + 16, 0xA5, dtype=np.uint8)
+    b.o.unpack(count, exp[shift:shift + span], origin, 0, ref.tobytes())
+    optr = out.data_ptr() + shift + origin
     if frags is None:
-        ompi_amd.unpack(packed, size, 0, out.data_ptr() + origin, count, e)
+        ompi_amd.unpack(packed, size, 0, optr, count, e)
     else:
-        conv = ompi_amd.Convertor().prepare_for_recv(e, count, out.data_ptr() + origin)
+        conv = ompi_amd.Convertor().prepare_for_recv(e, count, optr)
         opos, k = 0, 0
         while opos < size:
             ln = min(frags[k % len(frags)], size - opos)
@@ -661,6 +666,26 @@ def test_no_op_types_fill_fragments_to_the_byte(device, name):
         pos += md
     ref = np.frombuffer(b.o.pack(count, host, origin, 0, size, element_granular=False), dtype=np.uint8)
     np.testing.assert_array_equal(_host(packed), ref)
+
+
+@pytest.mark.parametrize("esz,shift,count,extra", [(4, 4, 1, 0), (4, 8, 3, 4), (4, 12, 2, 8), (8, 8, 3, 8),
+                                                   (8, 0, 2, 24), (16, 0, 2, 16), (4, 0, 1, 0)])
+def test_sorted_list_engine_origin_phases(device, sorted_from, esz, shift, count, extra):
+    """The address-ordered engine with the list origin at every 16-byte phase: the buffer
+    `shift` bytes off its allocation, and instances an extent apart that is a multiple of the
+    element size but not of 16 (each instance starts at another phase).  Bit-exact vs the
+    oracle, bytes around the span untouched."""
+    sorted_from(1)
+    rng = np.random.default_rng(esz * 7 + shift + count)
+    ch = (128 << 10) // esz
+    n = 2 * ch + 3001
+    unit = ("basic", 15) if esz == 4 else ("basic", 16)
+    per = esz // (4 if esz == 4 else 8)
+    disps = (rng.permutation(3 * n)[:n] * per).astype(np.int64)
+    inner = ("indexed_block", per, disps.tolist(), unit)
+    b = R.Built(("resized", inner, 0, esz * 3 * n + extra))
+    _roundtrip(b, count, device, 40 + esz + shift, shift=shift)
+    assert b.engine().engine_info()["sorted"] == 1
 
 
 def test_sorted_list_engine_misaligned_instances(device, sorted_from):
