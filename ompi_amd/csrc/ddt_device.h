@@ -109,7 +109,8 @@ static_assert(sizeof(Item) == 512, "Item layout is shared with tests/plan_emu.py
 static_assert(sizeof(ItemBlock) <= 4096, "kernel argument segment limit");
 
 // ---- external32 conversion (ddt_external.cpp, ddt_ext_kernel) ----
-enum ConvKind : uint32_t { CONV_COPY = 0, CONV_SWAP = 1, CONV_LONG = 2, CONV_ULONG = 3 };
+// CONV_LDBL: each 16-byte component x87 80-bit (native) <-> IEEE quad big-endian (external)
+enum ConvKind : uint32_t { CONV_COPY = 0, CONV_SWAP = 1, CONV_LONG = 2, CONV_ULONG = 3, CONV_LDBL = 4 };
 
 // `n` consecutive elements of one basic type inside a segment body.
 struct ConvRun {

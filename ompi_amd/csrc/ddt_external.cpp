@@ -9,7 +9,12 @@
 //     unpack (copy_long_heterogeneous :1094-1223, unsigned :1225-1360);
 //   complex types swap each component (COPY_2SAMETYPE_HETEROGENEOUS :776-842);
 //   everything else is byte-swapped whole (opal_dt_swap_bytes :49-70).
-// Long double types convert through build-dependent formats (:121-230) and are refused.
+// Long double types follow the gcc x86-64 build (x87 long double in 16 bytes, _Float128
+// available): FLOAT12 (long double, MPI_LONG_DOUBLE) and FLOAT16 (_Float128) swap their 16
+// bytes whole (COPY_TYPE_HETEROGENEOUS without the long-double flag, :1033-1034, :1058-1059);
+// LONG_DOUBLE_COMPLEX converts each component x87 <-> IEEE quad (:779-842 with ldbl_to_f128 /
+// f128_to_ldbl, :488-590), CONV_LDBL; FLOAT128_COMPLEX, whose reference copy treats quad
+// components as long doubles (:1082-1083), is refused.
 //
 // The engine keeps the type map's element ids on the uncommitted description (Node::tid).
 // This file compresses that sequence into segments: `reps` repetitions of a short body of
@@ -35,7 +40,7 @@ thread_local size_t g_runs = 0;        // runs appended while flattening one typ
 
 // external32 element bytes per OPAL id (-1: no portable form), opal_convertor.c:146-172
 const int kExtSize[29] = {0, 0, 0, 0, 1, 2, 4, 8, 16, 1, 2, 4, 8, 16, 2,
-                          4, 8, -1, -1, 4, 8, 16, -1, 1, 4, 4, 4, -1, 0};
+                          4, 8, 16, 16, 4, 8, 16, 32, 1, 4, 4, 4, -1, 0};
 const int kNatSize[29] = {0, 0, 0, 0, 1, 2, 4, 8, 16, 1, 2, 4, 8, 16, 2,
                           4, 8, 16, 16, 4, 8, 16, 32, 1, 4, 8, 8, 32, 0};
 
@@ -158,8 +163,8 @@ std::shared_ptr<ExtPlan> get_ext_plan(ddt_datatype *t)
                 const int xs = kExtSize[r.tid], ns = kNatSize[r.tid];
                 if (xs < 0) {
                     X->error = DDT_ERR_NOT_SUPPORTED;
-                    X->what = "external32: long double types have no portable form here "
-                              "(opal_copy_functions_heterogeneous.c:121-230)";
+                    X->what = "external32: FLOAT128_COMPLEX is not converted (the reference passes its "
+                              "quad components through ldbl_to_f128, opal_copy_functions_heterogeneous.c:1082)";
                     break;
                 }
                 ConvRun cr{};
@@ -172,6 +177,8 @@ std::shared_ptr<ExtPlan> get_ext_plan(ddt_datatype *t)
                     cr.kind = CONV_LONG;
                 else if (r.tid == 26)
                     cr.kind = CONV_ULONG;
+                else if (r.tid == 22)
+                    cr.kind = CONV_LDBL;
                 else
                     cr.kind = ns == 1 ? CONV_COPY : CONV_SWAP;
                 cr.comp = r.tid == 19 ? 2 : r.tid == 20 ? 4 : r.tid == 21 ? 8 : uint32_t(ns);

@@ -608,9 +608,78 @@ __device__ __forceinline__ bool swap_words(const uint8_t *from, uint8_t *to, uin
     return true;
 }
 
+// One long double component (the external stream is byte aligned: bytewise access).
+// Pack: x87 80-bit -> IEEE quad, exact (libgcc __extendxftf2 semantics: the explicit bit is
+// dropped unchecked, a NaN is quieted).  A pseudo-denormal (exponent 0, explicit bit set) has
+// no single reference answer -- the same libgcc conversion gives exponent 0 on the Intel
+// container and exponent 1 on the GPU box's host -- so it becomes the value it denotes.  Unpack: quad -> x87 rounded to nearest even (__trunctfxf2), then the
+// reference's in-place store: value bytes 0..9, bytes 10..15 keep the quad's.
+template <int DIR>
+__device__ __forceinline__ void convert_ldbl(const uint8_t *from, uint8_t *to)
+{
+    constexpr uint64_t TOP = 1ull << 63, QBIT = 1ull << 62, M63 = TOP - 1;
+    if (DIR == 0) {
+        uint64_t m = 0;
+        for (int k = 0; k < 8; ++k)
+            m |= uint64_t(from[k]) << (8 * k);
+        const uint32_t se = uint32_t(from[8]) | (uint32_t(from[9]) << 8);
+        const uint64_t sign = se >> 15;
+        uint64_t e = se & 0x7FFF, f = m & M63;   // 63 fraction bits
+        if (e == 0x7FFF && f)
+            f |= QBIT;                           // NaN: quieted
+        else if (e == 0 && (m & TOP))
+            e = 1;                               // pseudo-denormal: the normal 1.f x 2^-16382 it denotes
+        const uint64_t lo = f << 49, hi = (f >> 15) | (e << 48) | (sign << 63);
+        for (int k = 0; k < 8; ++k) {
+            to[k] = uint8_t(hi >> (8 * (7 - k)));
+            to[8 + k] = uint8_t(lo >> (8 * (7 - k)));
+        }
+    } else {
+        uint64_t hi = 0, lo = 0;
+        for (int k = 0; k < 8; ++k) {
+            hi = (hi << 8) | from[k];
+            lo = (lo << 8) | from[8 + k];
+        }
+        const uint64_t sign = hi >> 63;
+        uint64_t e = (hi >> 48) & 0x7FFF;
+        const uint64_t fh = hi & ((1ull << 48) - 1);
+        const uint64_t f63 = (fh << 15) | (lo >> 49), rest = lo & ((1ull << 49) - 1);
+        uint64_t m;
+        if (e == 0x7FFF) {
+            m = (fh | lo) ? (TOP | QBIT | f63) : TOP;
+        } else {
+            m = (e ? TOP : 0) | f63;
+            const uint64_t half = 1ull << 48;
+            if (rest > half || (rest == half && (m & 1))) {
+                ++m;
+                if (m == 0) {                    // carried out of a normal: next binade
+                    m = TOP;
+                    ++e;
+                } else if (e == 0 && m == TOP) { // a denormal rounded up to the smallest normal
+                    e = 1;
+                }
+            }
+            if (e == 0x7FFF)
+                m = TOP;                         // rounded past the largest finite: infinity
+        }
+        for (int k = 0; k < 8; ++k)
+            to[k] = uint8_t(m >> (8 * k));
+        const uint32_t se = uint32_t((sign << 15) | e);
+        to[8] = uint8_t(se);
+        to[9] = uint8_t(se >> 8);
+        for (int k = 10; k < 16; ++k)
+            to[k] = uint8_t(hi >> (8 * (k - 8)));
+    }
+}
+
 template <int DIR>
 __device__ __forceinline__ void convert_elem(const ConvRun &r, const uint8_t *from, uint8_t *to)
 {
+    if (r.kind == CONV_LDBL) {
+        for (uint32_t b = 0; b < r.nsz; b += 16)
+            convert_ldbl<DIR>(from + b, to + b);
+        return;
+    }
     if (r.kind == CONV_LONG || r.kind == CONV_ULONG) {
         // external 4 big-endian bytes <-> native 8 little-endian bytes
         for (int k = 0; k < 4; ++k)

@@ -252,8 +252,11 @@ class _Predefs:
         "MPI_LONG": LONG, "MPI_UNSIGNED_LONG": UNSIGNED_LONG, "MPI_LONG_LONG": INT8,
         "MPI_INT8_T": INT1, "MPI_INT16_T": INT2, "MPI_INT32_T": INT4, "MPI_INT64_T": INT8,
         "MPI_UINT8_T": UINT1, "MPI_UINT16_T": UINT2, "MPI_UINT32_T": UINT4, "MPI_UINT64_T": UINT8,
-        "MPI_FLOAT": FLOAT4, "MPI_DOUBLE": FLOAT8, "MPI_LONG_DOUBLE": FLOAT16,
+        # x86-64: long double has 64 mantissa digits in 16 bytes -> FLOAT12
+        # (ompi_datatype_internal.h:637-638, opal_datatype_constructors.h:267-270)
+        "MPI_FLOAT": FLOAT4, "MPI_DOUBLE": FLOAT8, "MPI_LONG_DOUBLE": FLOAT12,
         "MPI_C_FLOAT_COMPLEX": FLOAT_COMPLEX, "MPI_C_DOUBLE_COMPLEX": DOUBLE_COMPLEX,
+        "MPI_C_LONG_DOUBLE_COMPLEX": LONG_DOUBLE_COMPLEX,
         "MPI_C_BOOL": BOOL, "MPI_WCHAR": WCHAR,
     }
 

@@ -841,11 +841,51 @@ int64_t ort_raw(ort_type *t, int64_t count, int64_t base, int64_t position, int6
  *     zero- (UNSIGNED_LONG) extends;
  *   - complex types: each component byte-swapped (COPY_2SAMETYPE_HETEROGENEOUS :776-842);
  *   - every other type: byte-swapped whole (opal_dt_swap_bytes :49-70).
- * Long double types (FLOAT12, FLOAT16, LONG_DOUBLE_COMPLEX, FLOAT128_COMPLEX) depend on the
- * reference's build (HAVE_IEEE754_H, :121-230): refused (-1).
+ * Long double types follow the reference as built by gcc on x86-64 Linux (long double = x87
+ * 80-bit in 16 bytes, LDBL_MANT_DIG 64, _Float128 available), the build this engine's
+ * native layout matches:
+ *   - FLOAT12 is `long double` (opal_datatype_constructors.h:267-270; MPI_LONG_DOUBLE,
+ *     ompi_datatype_internal.h:637-638) and FLOAT16 is `_Float128` (:281-284); their
+ *     heterogeneous copies are COPY_TYPE_HETEROGENEOUS without the long-double flag
+ *     (opal_copy_functions_heterogeneous.c:1033-1034, :1058-1059): 16 bytes swapped whole,
+ *     no format change;
+ *   - LONG_DOUBLE_COMPLEX converts each component between the local x87 format and
+ *     external32's IEEE quad (COPY_2SAMETYPE_HETEROGENEOUS_INTERNAL(..., 1) :779-842, arch
+ *     ompi_datatype_external32.c:106): pack = ldbl_to_f128 (:488-519, `(_Float128)` of the
+ *     long double) then the in-place swap; unpack = swap into the destination, then
+ *     f128_to_ldbl (:558-590) in place: the long double store writes the 10 value bytes and
+ *     the 6 padding bytes keep the swapped quad's bytes 10..15 (aligned destination);
+ *   - FLOAT128_COMPLEX is refused (-1): its reference copy passes `_Float128` components
+ *     through ldbl_to_f128 as if they were long doubles (:1082-1083), which is not a format
+ *     conversion this engine reproduces.
+ * This restatement runs the host's own long double <-> _Float128 conversions (libgcc).
  */
 static const int64_t ort_ext_size[29] = {
-    0, 0, 0, 0, 1, 2, 4, 8, 16, 1, 2, 4, 8, 16, 2, 4, 8, -1, -1, 4, 8, 16, -1, 1, 4, 4, 4, -1, 0};
+    0, 0, 0, 0, 1, 2, 4, 8, 16, 1, 2, 4, 8, 16, 2, 4, 8, 16, 16, 4, 8, 16, 32, 1, 4, 4, 4, -1, 0};
+
+/* one long double component: local x87 (16 bytes) <-> external32 big-endian IEEE quad */
+static void ort_ext_ldbl(const unsigned char *from, unsigned char *to, int pack)
+{
+    unsigned char q[16];
+    if (pack) {
+        long double l;
+        _Float128 f;
+        memcpy(&l, from, sizeof(l));
+        f = (_Float128) l;
+        memcpy(q, &f, 16);
+        for (int k = 0; k < 16; k++)
+            to[k] = q[15 - k];
+    } else {
+        _Float128 f;
+        long double l;
+        for (int k = 0; k < 16; k++)
+            q[k] = from[15 - k];
+        memcpy(&f, q, 16);
+        l = (long double) f;
+        memcpy(to, q, 16);
+        memcpy(to, &l, 10);   /* the x87 store: 10 value bytes, the rest keep q's */
+    }
+}
 
 static int64_t ort_ext_comp(int64_t tid)
 {
@@ -883,6 +923,11 @@ static void ort_ext_elem(int64_t tid, const unsigned char *from, unsigned char *
             for (int k = 4; k < 8; k++)
                 to[k] = fill;
         }
+        return;
+    }
+    if (tid == 22) {   /* long double complex: two converted components */
+        ort_ext_ldbl(from, to, pack);
+        ort_ext_ldbl(from + 16, to + 16, pack);
         return;
     }
     const int64_t c = ort_ext_comp(tid);

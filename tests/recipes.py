@@ -26,9 +26,10 @@ from . import oracle as O
 # (opal id, size) of the basic types the fuzzer draws from
 BASICS = [(4, 1), (5, 2), (6, 4), (15, 4), (16, 8), (7, 8), (21, 16), (11, 4), (9, 1)]
 # every type with an external32 form: adds INT16, FLOAT2, the complex types, BOOL, WCHAR,
-# LONG and UNSIGNED_LONG (size-changing)
+# LONG and UNSIGNED_LONG (size-changing), the long doubles (FLOAT12 = MPI_LONG_DOUBLE, FLOAT16 =
+# _Float128, LONG_DOUBLE_COMPLEX converted x87 <-> IEEE quad)
 EXT_BASICS = BASICS + [(8, 16), (14, 2), (19, 4), (20, 8), (23, 1), (24, 4), (25, 8), (26, 8),
-                       (12, 8), (10, 2)]
+                       (12, 8), (10, 2), (17, 16), (18, 16), (22, 32)]
 
 
 def build_oracle(recipe, memo=None):

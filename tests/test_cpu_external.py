@@ -90,11 +90,73 @@ def test_unsigned_long_zero_extends():
     assert struct.unpack("<Q", back.tobytes())[0] == 0x80000001
 
 
-def test_long_double_has_no_external_form():
-    assert O.basic(18).external_size() == -1
+def _quad_be(sign: int, exp: int, frac112: int) -> bytes:
+    """IEEE binary128, big-endian (the external32 long double, ompi_datatype_external32.c:95-99)."""
+    return ((sign << 127) | (exp << 112) | frac112).to_bytes(16, "big")
+
+
+def test_long_double_complex_converts_x87_to_ieee_quad():
+    """LONG_DOUBLE_COMPLEX (COPY_2SAMETYPE_HETEROGENEOUS_INTERNAL(..., 1),
+    opal_copy_functions_heterogeneous.c:779-842): each x87 component becomes a big-endian
+    IEEE quad on pack (exact); unpack converts back, and the component's 6 padding bytes
+    keep the swapped quad's bytes 10..15 (the in-place f128_to_ldbl store, :558-590)."""
+    vals = np.array([1.0, -2.5, 0.1, np.finfo(np.longdouble).tiny / 4, np.inf, -0.0],
+                    dtype=np.longdouble)
+    assert vals.dtype.itemsize == 16   # x86-64 long double: 80 bits in 16 bytes
+    user = vals.view(np.uint8).copy()
+    t = O.basic(22)
+    ext = t.pack_external(3, user, 0)
+    assert t.external_size() == 32 and len(ext) == 96
+    assert ext[0:16] == _quad_be(0, 16383, 0)                     # 1.0
+    assert ext[16:32] == _quad_be(1, 16384, 1 << 110)             # -2.5 = -1.25 x 2^1
+    # 0.1 as x87: mantissa 0xCCCCCCCCCCCCCCCD x 2^-67 -> quad fraction = (m - 2^63) << 49
+    m = int.from_bytes(vals[2:3].view(np.uint8)[:8].tobytes(), "little")
+    assert ext[32:48] == _quad_be(0, 16383 - 4, (m - (1 << 63)) << 49)
+    assert ext[48:64] == _quad_be(0, 0, (1 << 61) << 49)         # x87 denormal 2^-16384
+    assert ext[64:80] == _quad_be(0, 0x7FFF, 0)                   # inf
+    assert ext[80:96] == _quad_be(1, 0, 0)                        # -0.0
+    back = np.zeros(96, dtype=np.uint8)
+    t.unpack_external(3, back, 0, ext)
+    for i in range(6):
+        comp, q = back[16 * i:16 * i + 16].tobytes(), ext[16 * i:16 * i + 16][::-1]
+        assert comp[:10] == user[16 * i:16 * i + 10].tobytes()
+        assert comp[10:] == q[10:]
+
+
+def test_long_double_unpack_rounds_to_nearest_even():
+    """A quad with more precision than x87 holds (f128_to_ldbl, libgcc __trunctfxf2): the 49
+    dropped fraction bits round to nearest, ties to even, carrying into the exponent."""
+    t = O.basic(22)
+    cases = [((1 << 112) - 1, 1 << 63, 16384),     # all ones: rounds up into the next binade
+             (1 << 48, 1 << 63, 16383),             # tie, even mantissa: stays
+             ((1 << 49) | (1 << 48), (1 << 63) | 2, 16383)]   # tie, odd mantissa: rounds up
+    for frac, want_m, want_e in cases:
+        q = _quad_be(0, 16383, frac)
+        back = np.zeros(32, dtype=np.uint8)
+        t.unpack_external(1, back, 0, q + q)
+        assert int.from_bytes(back[:8].tobytes(), "little") == want_m
+        assert int.from_bytes(back[8:10].tobytes(), "little") == want_e
+
+
+def test_long_double_and_float128_swap_whole():
+    """FLOAT12 (MPI_LONG_DOUBLE) and FLOAT16 (_Float128) use the copy functions without the
+    long-double flag (opal_copy_functions_heterogeneous.c:1033-1034, :1058-1059): 16 bytes
+    reversed, no format change."""
+    raw = np.arange(32, dtype=np.uint8)
+    for tid in (17, 18):
+        t = O.basic(tid)
+        ext = t.pack_external(2, raw, 0)
+        assert ext == raw[:16].tobytes()[::-1] + raw[16:].tobytes()[::-1]
+        assert ompi_amd.pack_external_size(2, __import__("ompi_amd").datatype.predefined(tid)) == 32
+
+
+def test_float128_complex_has_no_external_form():
+    """FLOAT128_COMPLEX: the reference routes its quad components through ldbl_to_f128 as if
+    they were long doubles (:1082-1083); the engine refuses it rather than guess."""
+    assert O.basic(27).external_size() == -1
     from ompi_amd import datatype as D
     with pytest.raises(ompi_amd.DDTError) as ei:
-        ompi_amd.pack_external_size(1, D.predefined(D.FLOAT16))
+        ompi_amd.pack_external_size(1, D.predefined(D.FLOAT128_COMPLEX))
     assert ei.value.code == -10
 
 
@@ -121,7 +183,7 @@ def test_oracle_external_roundtrip_fuzz():
         ext = b.o.pack_external(count, user, origin)
         assert len(ext) == b.o.external_size() * count
         # the native stream and the external stream hold the same elements: for types
-        # without LONG the byte multisets of each element agree, so lengths match
-        if b.o.external_size() == info["size"]:
+        # without LONG or converted long doubles the byte multisets agree
+        if b.o.external_size() == info["size"] and 22 not in {r[3] for r in b.o.typed_runs()}:
             native = b.o.pack(count, user, origin, 0, info["size"] * count, element_granular=False)
             assert sorted(native) == sorted(ext)

@@ -400,6 +400,21 @@ def test_raw_export_regions_rebuild_packed_stream(device):
         assert torch.equal(rebuilt, packed), b.recipe
 
 
+def _no_pseudo_denormals(host, otype, count, origin):
+    """Clear the explicit bit of x87 components with a zero exponent in LONG_DOUBLE_COMPLEX
+    elements: such pseudo-denormals convert differently on different host CPUs (see
+    convert_ldbl in ddt_kernels.hip), so the oracle has no single answer for them."""
+    ext = otype.extent
+    for i in range(count):
+        for disp, ln, esz, tid in otype.typed_runs():
+            if tid != 22:
+                continue
+            for off in range(0, ln, 16):
+                c = origin + i * ext + disp + off
+                if host[c + 8] == 0 and (host[c + 9] & 0x7F) == 0:
+                    host[c + 7] &= 0x7F
+
+
 @pytest.mark.parametrize("host_ext", [False, True])
 def test_external32_matches_oracle(device, host_ext):
     """MPI_Pack_external / MPI_Unpack_external on the GPU: bit-exact with the oracle's
@@ -418,6 +433,7 @@ def test_external32_matches_oracle(device, host_ext):
             continue
         span, origin = R.layout(info, count)
         host = R.fill(span, n)
+        _no_pseudo_denormals(host, b.o, count, origin)
         user = _dev(host, device)
         e = b.engine()
         ref = b.o.pack_external(count, host, origin)
@@ -455,10 +471,49 @@ def test_external32_errors(device):
     with pytest.raises(ompi_amd.DDTError) as ei:
         ompi_amd.pack_external(user, 1, t, out, 15, 0)
     assert ei.value.code == -9   # truncate
-    ld = D.predefined(D.FLOAT16)
+    q = D.predefined(D.FLOAT128_COMPLEX)   # no external form (ddt_external.cpp)
+    user32 = torch.zeros(32, dtype=torch.uint8, device=device)
+    out32 = torch.zeros(32, dtype=torch.uint8, device=device)
     with pytest.raises(ompi_amd.DDTError) as ei:
-        ompi_amd.pack_external(user, 1, ld, out, 16, 0)
+        ompi_amd.pack_external(user32, 1, q, out32, 32, 0)
     assert ei.value.code == -10
+
+
+@pytest.mark.parametrize("tid", [22, 17, 18])
+def test_external32_long_doubles_every_bit_pattern(device, tid):
+    """Long doubles through the GPU conversion (ddt_kernels.hip convert_ldbl) against the
+    oracle, which runs the host's own libgcc long double <-> _Float128 conversions as the
+    reference's gcc/x86-64 build does: 64 Ki random 16-byte patterns per component (normals,
+    denormals, NaN payloads, unnormals), packed from a vector with gaps and unpacked back
+    with the gaps kept."""
+    import torch
+    import ompi_amd
+    from ompi_amd import datatype as D
+    n = 1 << 15
+    esz = 32 if tid == 22 else 16
+    rng = np.random.default_rng(tid)
+    host = rng.integers(0, 256, size=2 * n * esz, dtype=np.uint8)   # stride 2: a gap after each
+    # x87 pseudo-denormals (exponent 0, explicit bit set) convert differently on different host
+    # CPUs (ddt_kernels.hip convert_ldbl): clear the explicit bit of zero-exponent components
+    comp = host.reshape(-1, 16)
+    zero_exp = (comp[:, 8] == 0) & ((comp[:, 9] & 0x7F) == 0)
+    comp[zero_exp, 7] &= 0x7F
+    t_o = O.vector(n, 1, 2, O.basic(tid))
+    t_e = D.create_vector(n, 1, 2, D.predefined(tid)).commit()
+    ref = t_o.pack_external(1, host, 0)
+    assert len(ref) == n * esz
+    user = _dev(host, device)
+    out = torch.zeros(len(ref), dtype=torch.uint8, device=device)
+    assert ompi_amd.pack_external(user.data_ptr(), 1, t_e, out.data_ptr(), len(ref), 0) == len(ref)
+    np.testing.assert_array_equal(_host(out), np.frombuffer(ref, dtype=np.uint8))
+    # unpack random external bytes (arbitrary quads, not only images of x87 values)
+    ext = rng.integers(0, 256, size=len(ref), dtype=np.uint8)
+    exp = np.full(host.size, 0xA5, dtype=np.uint8)
+    t_o.unpack_external(1, exp, 0, ext.tobytes())
+    dst = torch.full((host.size,), 0xA5, dtype=torch.uint8, device=device)
+    src = _dev(ext, device)
+    assert ompi_amd.unpack_external(src.data_ptr(), len(ref), 0, dst.data_ptr(), 1, t_e) == len(ref)
+    np.testing.assert_array_equal(_host(dst), exp)
 
 
 def test_darray_roundtrip(device):
