@@ -310,7 +310,8 @@ int64_t ddt_type_plan_list(const ddt_datatype_t *type, size_t leaf, int64_t *dis
  * 0 none); "stage_mb" =
  * staging slot MiB for pageable host iovecs (read when a convertor first stages); "sseg" =
  * address-ordered engine segment bytes (64 or 128); "sunroll" = its pack-1 elements per
- * thread in flight (4, 8, 16 default);
+ * thread in flight (4, 8, 16 default); "s2unroll" = the same for its unpack pass 2' (4, 8
+ * default, 16);
  * "reset" = restore the defaults.
  * Environment: DDT_NT, DDT_TASK_KB, DDT_WT, DDT_XCD. */
 int ddt_tune(const char *key, long value);

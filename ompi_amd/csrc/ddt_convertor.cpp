@@ -217,7 +217,8 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                 uint8_t *u = reinterpret_cast<uint8_t *>(user + uint64_t(L.list_shift) + uint64_t(P.dev[0].disp_base)
                                                          + i * uint64_t(t->extent()));
                 uint8_t *pk = reinterpret_cast<uint8_t *>(wins[0].ptr + i * uint64_t(t->size));
-                HIPCHK(SL->run(u, pk, dir, uint32_t(tuning().spol), stream, uint32_t(tuning().sunroll)));
+                HIPCHK(SL->run(u, pk, dir, uint32_t(tuning().spol), stream, uint32_t(tuning().sunroll),
+                               uint32_t(tuning().s2unroll)));
             }
             return DDT_SUCCESS;
         }
@@ -1347,6 +1348,8 @@ int ddt_tune(const char *key, long value)
         tuning().hd_grid = value < 0 ? 0 : value;
     else if (k == "hd_grid_pack")
         tuning().hd_grid_pack = value < 0 ? 0 : value;
+    else if (k == "s2unroll")
+        tuning().s2unroll = value >= 16 ? 16 : (value >= 8 ? 8 : 4);
     else if (k == "sunroll")
         tuning().sunroll = value >= 16 ? 16 : (value >= 8 ? 8 : 4);
     else if (k == "sseg")

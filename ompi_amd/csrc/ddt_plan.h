@@ -35,6 +35,7 @@ struct Tuning {
                           // (scripts/ubench_pcie.hip, profiles/r2_ubench_pcie.log)
     long hd_grid_pack = 0;   // the same cap for a pack writing pinned host memory
     long sunroll = 16;    // address-ordered engine: pack 1 elements per thread in flight (4, 8, 16)
+    long s2unroll = 8;    // the same for its unpack pass 2' 
     long sseg = 64;       // address-ordered engine: U segment bytes (64 or 128), read at plan build
 };
 Tuning &tuning();

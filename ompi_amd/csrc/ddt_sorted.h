@@ -38,8 +38,9 @@ struct SortedList {
                hipStream_t stream);
     // pol: access policy bits (POL_* in ddt_sorted.hip; ddt_tune "spol")
     // unroll: elements per thread in flight in pack 1's address-ordered gather (4, 8 or 16)
+    // k2: the same for unpack pass 2' (4, 8 or 16)
     hipError_t run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol, hipStream_t stream,
-                   uint32_t unroll = 16);
+                   uint32_t unroll = 16, uint32_t k2 = 8);
 };
 
 }  // namespace ddt

@@ -308,7 +308,7 @@ __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, 
 }
 
 // pack pass 2: the bucket's runs scatter into LDS by destination, then stream out
-template <int E>
+template <int E, int K>
 __global__ __launch_bounds__(PT) void k_pack2(const uint8_t *__restrict__ U, const uint16_t *__restrict__ upos,
                                               const uint32_t *__restrict__ bstart, uint8_t *__restrict__ packed,
                                               uint32_t n, uint32_t pol)
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(PT) void k_pack2(const uint8_t *__restrict__ U, con
     const uint32_t k = blockIdx.x;
     const uint32_t s0 = bstart[k], s1 = bstart[k + 1];
     const T *src = reinterpret_cast<const T *>(U);
-    constexpr int K = 4;
+    
     for (uint32_t x0 = s0 + threadIdx.x; x0 < s1; x0 += PT * K) {
         T v[K];
         uint32_t p[K];
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(PT) void k_pack2(const uint8_t *__restrict__ U, con
 }
 
 // unpack pass 2': the bucket's packed elements into LDS, then out to U in run order
-template <int E>
+template <int E, int K>
 __global__ __launch_bounds__(PT) void k_unpack2(const uint8_t *__restrict__ packed, const uint16_t *__restrict__ upos,
                                                 const uint32_t *__restrict__ bstart, uint8_t *__restrict__ U,
                                                 uint32_t n, uint32_t pol)
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(PT) void k_unpack2(const uint8_t *__restrict__ pack
     const uint32_t k = blockIdx.x;
     const uint32_t m = min(RG, n - k * RG);
     const T *src = reinterpret_cast<const T *>(packed) + size_t(k) * RG;
-    constexpr int K = 4;
+    
     for (uint32_t t0 = threadIdx.x; t0 < m; t0 += PT * K) {
         T v[K];
 #pragma unroll
@@ -474,6 +474,23 @@ __global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, cons
                 else
                     dst[a[q]] = v[q];
             }
+    }
+}
+
+// pass 2 with 4 elements per thread in flight; pass 2' with k2 (4, 8 or 16; E * k2 <= 64
+// bytes).  cfg4 A/B (profiles/r2_ab_sorted_pass2_unroll.log): unpack 780 -> 751 us at 8 or 16,
+// pack 575 -> 587 us, so only the unpack side takes the knob.
+template <int E, int DIR>
+void launch_pass2(dim3 gb, dim3 blk, hipStream_t stream, const uint8_t *src, const uint16_t *upos,
+                  const uint32_t *bstart, uint8_t *dst, uint32_t n, uint32_t pol, uint32_t k2)
+{
+    constexpr int K16 = E == 4 ? 16 : 4, K8 = E <= 8 ? 8 : 4;
+    if (DIR == 0) {
+        hipLaunchKernelGGL((k_pack2<E, 4>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
+    } else {
+        if (k2 >= 16) hipLaunchKernelGGL((k_unpack2<E, K16>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
+        else if (k2 >= 8) hipLaunchKernelGGL((k_unpack2<E, K8>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
+        else hipLaunchKernelGGL((k_unpack2<E, 4>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
     }
 }
 
@@ -619,7 +636,7 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
 // A/B (profiles/r2_ab_sorted_unroll.log): pack 656 / 617 / 612 us; unpack 1' keeps 4 (its
 // scatter has one dependent load per element; 8 and 16 measured slower, 804 -> 818 / 842 us).
 hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol, hipStream_t stream,
-                           uint32_t unroll)
+                           uint32_t unroll, uint32_t k2)
 {
     // U is one scratch per plan: a launch on another stream waits for the last one
     std::lock_guard<std::mutex> g(mu);
@@ -634,9 +651,9 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol
 #define DDT_SORTED_LAUNCH_K(E, SB, K)                                                                           \
     if (dir == 0) {                                                                                             \
         hipLaunchKernelGGL((k_pack1<E, SB, K>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);  \
-        hipLaunchKernelGGL((k_pack2<E>), gb, blk, 0, stream, u8, upos, bstart, packed, n, pol);                 \
+        launch_pass2<E, 0>(gb, blk, stream, u8, upos, bstart, packed, n, pol, k2);                             \
     } else {                                                                                                    \
-        hipLaunchKernelGGL((k_unpack2<E>), gb, blk, 0, stream, packed, upos, bstart, u8, n, pol);               \
+        launch_pass2<E, 1>(gb, blk, stream, packed, upos, bstart, u8, n, pol, k2);                             \
         hipLaunchKernelGGL((k_unpack1<E, SB, 4>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);\
     }
 // K * E <= 64 bytes of elements per thread in flight: wider elements at K = 16 (or 16-byte
