@@ -506,7 +506,10 @@ def main():
                                         f"({split['total_count']} instances in total, no collective)"
                                         if split else
                                         f"replicas x{world} (fields sharded by count, no collective)")),
-            "per_gpu_GiBs": round(2.0 * S / (tp + tu) / GiB, 3),
+            # rank 0's pack + unpack kernel time from HIP events on every 10th timed step (the
+            # events add a few us of stream time to those steps, so this sits slightly below
+            # a per-GPU share of `value`, which is wall clock over all K steps)
+            "per_gpu_GiBs_from_events": round(2.0 * S / (tp + tu) / GiB, 3),
             "all_gather_check": rccl,
             "kernel_ms": {"pack": round(tp * 1e3, 4), "unpack": round(tu * 1e3, 4)},
             "graph_replay_GiBs_per_gpu": (round(2.0 * S / graph_step / GiB, 3) if graph_step else None),
