@@ -213,9 +213,12 @@ def cpu_baseline(name, srec, scount, what, host_user, origin, gpu_prefix, budget
             "host": {"cpus_available": logical, "physical_cores_available": physical,
                      "machine_cpus": os.cpu_count()},
             "sample": f"{what} of config {name}: pack+unpack of {S} packed bytes per trial, "
-                      f"oracle/ddt_oracle.c position-sharded over {threads_all} threads (every physical "
-                      f"core of this process's CPU set) and over 1 thread; value = median of the "
-                      f"Tukey-retained trials at {threads_all} threads"}
+                      f"oracle/ddt_oracle.c position-sharded over {threads_all} threads ("
+                      + ("every physical core of this process's CPU set" if threads_all == physical else
+                         f"the CPU share OMP_NUM_THREADS grants this one-GPU process, of {physical} "
+                         f"physical cores visible")
+                      + f") and over 1 thread; value = median of the Tukey-retained trials at "
+                      f"{threads_all} threads"}
 
 
 # ------------------------------------------------------------------ latency
