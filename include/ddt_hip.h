@@ -308,7 +308,7 @@ int64_t ddt_type_plan_list(const ddt_datatype_t *type, size_t leaf, int64_t *dis
  * pinned host iovecs moved by the kernel over PCIe (bit 0 unpack, bit 1 pack; 3 default, 0 =
  * HBM staging); "hd_grid" / "hd_grid_pack" = workgroup cap of such an unpack / pack launch (256 / 0 default,
  * 0 none); "stage_mb" =
- * staging slot MiB for pageable host iovecs (read when a convertor first stages); "sseg" =
+ * staging buffer MiB for pageable host iovecs (256 default; read when a convertor first stages); "sseg" =
  * address-ordered engine segment bytes (64 or 128); "sunroll" = its pack-1 elements per
  * thread in flight (4, 8, 16 default); "s2unroll" = the same for its unpack pass 2' (4, 8
  * default, 16);

@@ -323,17 +323,17 @@ struct ddt_convertor {
     uint64_t bConverted = 0;
     hipStream_t stream = nullptr;
     bool async = false;
-    // host-iovec staging pipeline (two HBM slots, one copy stream).  The slot state lives
-    // with the convertor, not with one call: a slot is written only after the last reader
-    // of its previous contents -- the D2H copy of a pack (ev_c) or the kernel of an unpack
-    // (ev_k), possibly queued by an earlier asynchronous call on another stream -- has
-    // passed (pml_ob1_recvreq.c:627-663 issues such back-to-back async unpacks).
-    void *stage[2] = {nullptr, nullptr};
+    // host-iovec staging (one HBM buffer of up to stage_mb MiB, one copy stream).  The
+    // buffer state lives with the convertor, not with one call: the buffer is rewritten
+    // only after the last reader of its previous contents -- the D2H copies of a pack or
+    // the kernels of an unpack (ev_free), possibly queued by an earlier asynchronous call
+    // -- has passed (pml_ob1_recvreq.c:627-663 issues such back-to-back async unpacks).
+    void *stage = nullptr;
     uint64_t stage_size = 0;
     hipStream_t copy_stream = nullptr;
-    hipEvent_t ev_k[2] = {nullptr, nullptr}, ev_c[2] = {nullptr, nullptr};
-    bool rec_k[2] = {false, false}, rec_c[2] = {false, false};
-    uint32_t next_slot = 0;
+    hipEvent_t ev_chunk[2] = {nullptr, nullptr};
+    hipEvent_t ev_free = nullptr;
+    bool rec_free = false;
     ~ddt_convertor()
     {
         if (stream)
@@ -342,12 +342,13 @@ struct ddt_convertor {
             (void) hipStreamSynchronize(copy_stream);
             (void) hipStreamDestroy(copy_stream);
         }
-        for (int i = 0; i < 2; ++i) {
-            if (ev_k[i] && rec_k[i]) (void) hipEventSynchronize(ev_k[i]);
-            if (stage[i]) (void) hipFree(stage[i]);
-            if (ev_k[i]) (void) hipEventDestroy(ev_k[i]);
-            if (ev_c[i]) (void) hipEventDestroy(ev_c[i]);
-        }
+        if (ev_free && rec_free)
+            (void) hipEventSynchronize(ev_free);
+        if (stage)
+            (void) hipFree(stage);
+        for (hipEvent_t e : {ev_chunk[0], ev_chunk[1], ev_free})
+            if (e)
+                (void) hipEventDestroy(e);
     }
     int ensure_staging()
     {
@@ -355,36 +356,27 @@ struct ddt_convertor {
             return DDT_SUCCESS;
         HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
         stage_size = stage_bytes();
-        for (int i = 0; i < 2; ++i) {
-            HIPCHK(hipMalloc(&stage[i], stage_size));
-            HIPCHK(hipEventCreateWithFlags(&ev_k[i], hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&ev_c[i], hipEventDisableTiming));
-        }
-        return DDT_SUCCESS;
-    }
-    // make `writer` wait until slot s may be overwritten
-    int slot_free_on(int s, hipStream_t writer)
-    {
-        if (rec_k[s])
-            HIPCHK(hipStreamWaitEvent(writer, ev_k[s], 0));
-        if (rec_c[s])
-            HIPCHK(hipStreamWaitEvent(writer, ev_c[s], 0));
+        HIPCHK(hipMalloc(&stage, stage_size));
+        for (hipEvent_t *e : {&ev_chunk[0], &ev_chunk[1], &ev_free})
+            HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         return DDT_SUCCESS;
     }
 };
 
 namespace {
 
-// Chunk schedule of a staged window: a short first chunk (the copy engine starts while
-// the first kernel is still short), then full slots.
-uint64_t stage_chunk(uint64_t slot, uint64_t done, uint64_t left)
-{
-    const uint64_t want = done == 0 ? std::max<uint64_t>(slot >> 4, 1u << 20) : slot;
-    return std::min<uint64_t>(std::min<uint64_t>(want, slot), left);
-}
+constexpr uint64_t kSplitMin = 24ull << 20;   // host pieces split into two overlapped chunks
 
-// Move the packed windows of a convertor call: device iovecs in one launch, host iovecs
-// through the HBM staging pipeline (kernel on the user stream, copies on copy_stream).
+// Move the packed windows of a convertor call: device iovecs (and pinned host iovecs the
+// kernel reaches over PCIe) in one launch; other host iovecs through the HBM staging buffer,
+// kernels on the user stream, copies on copy_stream, in pieces of at most stage_size.
+//
+// A piece of >= 24 MiB is split in two chunks so that kernels and copies overlap, with the short chunk
+// where it is exposed (round 2; profiles/r2_e2e_pageable.jsonl): a pack queues BOTH chunk
+// kernels first (short chunk first) and only then the copies -- a copy from or to pageable
+// memory blocks the calling thread, so a kernel queued after it would start only when it
+// ends; an unpack copies the long chunk first and ends on the short one, so only the short
+// chunk's copy and kernel are not hidden.
 int execute(ddt_convertor *c, const std::vector<Window> &dev_wins,
             const std::vector<std::pair<Window, void *>> &host_wins, int dir, bool pcie = false)
 {
@@ -399,45 +391,75 @@ int execute(ddt_convertor *c, const std::vector<Window> &dev_wins,
     if (!host_wins.empty()) {
         if ((rc = c->ensure_staging()) != DDT_SUCCESS)
             return rc;
-        bool last[2] = {false, false};
+        char *st = static_cast<char *>(c->stage);
         for (const auto &hw : host_wins) {
             for (uint64_t off = hw.first.w0; off < hw.first.w1;) {
-                const int s = int(c->next_slot++ & 1u);
-                const uint64_t n = stage_chunk(c->stage_size, off - hw.first.w0, hw.first.w1 - off);
+                const uint64_t piece = std::min<uint64_t>(c->stage_size, hw.first.w1 - off);
+                const uint64_t small = std::min<uint64_t>(piece, std::max<uint64_t>(piece / 16, 1u << 20));
+                const uint64_t len[2] = {dir == 0 ? small : piece - small, dir == 0 ? piece - small : small};
                 char *hp = static_cast<char *>(hw.second) + (off - hw.first.w0);
-                std::vector<Window> w{{off, off + n, uint64_t(uintptr_t(c->stage[s]))}};
-                if (dir == 0) {   // pack: kernel -> D2H
-                    if ((rc = c->slot_free_on(s, c->stream)))
-                        return rc;
-                    if ((rc = run_windows(c->dt, *c->plan, c->count, c->base, w, false, 0, c->stream)))
-                        return rc;
-                    HIPCHK(hipEventRecord(c->ev_k[s], c->stream));
-                    c->rec_k[s] = true;
-                    HIPCHK(hipStreamWaitEvent(c->copy_stream, c->ev_k[s], 0));
-                    HIPCHK(hipMemcpyAsync(hp, c->stage[s], n, hipMemcpyDeviceToHost, c->copy_stream));
-                    HIPCHK(hipEventRecord(c->ev_c[s], c->copy_stream));
-                    c->rec_c[s] = true;
-                } else {          // unpack: H2D -> kernel
-                    if ((rc = c->slot_free_on(s, c->copy_stream)))
-                        return rc;
-                    HIPCHK(hipMemcpyAsync(c->stage[s], hp, n, hipMemcpyHostToDevice, c->copy_stream));
-                    HIPCHK(hipEventRecord(c->ev_c[s], c->copy_stream));
-                    c->rec_c[s] = true;
-                    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_c[s], 0));
-                    if ((rc = run_windows(c->dt, *c->plan, c->count, c->base, w, false, 1, c->stream)))
-                        return rc;
-                    HIPCHK(hipEventRecord(c->ev_k[s], c->stream));
-                    c->rec_k[s] = true;
+                if (piece < kSplitMin) {
+                    // one kernel and one copy, both on the user stream: below ~24 MiB a second
+                    // chunk hides less kernel time than its extra copy costs (16 MiB pageable:
+                    // 35.7 GiB/s split against 44.9 in one; 24 and 48 MiB gain 2 % from the split,
+                    // profiles/r2_e2e_pageable.jsonl)
+                    if (c->rec_free)
+                        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_free, 0));
+                    std::vector<Window> w{{off, off + piece, uint64_t(uintptr_t(st))}};
+                    if (dir == 0) {
+                        if ((rc = run_windows(c->dt, *c->plan, c->count, c->base, w, false, 0, c->stream)))
+                            return rc;
+                        HIPCHK(hipMemcpyAsync(hp, st, piece, hipMemcpyDeviceToHost, c->stream));
+                    } else {
+                        HIPCHK(hipMemcpyAsync(st, hp, piece, hipMemcpyHostToDevice, c->stream));
+                        if ((rc = run_windows(c->dt, *c->plan, c->count, c->base, w, false, 1, c->stream)))
+                            return rc;
+                    }
+                    HIPCHK(hipEventRecord(c->ev_free, c->stream));
+                } else if (dir == 0) {   // pack: both kernels, then both D2H copies
+                    if (c->rec_free)
+                        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_free, 0));   // last call's copies
+                    for (int j = 0; j < 2; ++j) {
+                        const uint64_t b0 = j ? len[0] : 0;
+                        if (!len[j])
+                            continue;
+                        std::vector<Window> w{{off + b0, off + b0 + len[j], uint64_t(uintptr_t(st + b0))}};
+                        if ((rc = run_windows(c->dt, *c->plan, c->count, c->base, w, false, 0, c->stream)))
+                            return rc;
+                        HIPCHK(hipEventRecord(c->ev_chunk[j], c->stream));
+                    }
+                    for (int j = 0; j < 2; ++j) {
+                        const uint64_t b0 = j ? len[0] : 0;
+                        if (!len[j])
+                            continue;
+                        HIPCHK(hipStreamWaitEvent(c->copy_stream, c->ev_chunk[j], 0));
+                        HIPCHK(hipMemcpyAsync(hp + b0, st + b0, len[j], hipMemcpyDeviceToHost, c->copy_stream));
+                    }
+                    HIPCHK(hipEventRecord(c->ev_free, c->copy_stream));
+                } else {          // unpack: per chunk H2D copy, then its kernel
+                    if (c->rec_free)
+                        HIPCHK(hipStreamWaitEvent(c->copy_stream, c->ev_free, 0));   // last kernels
+                    for (int j = 0; j < 2; ++j) {
+                        const uint64_t b0 = j ? len[0] : 0;
+                        if (!len[j])
+                            continue;
+                        HIPCHK(hipMemcpyAsync(st + b0, hp + b0, len[j], hipMemcpyHostToDevice, c->copy_stream));
+                        HIPCHK(hipEventRecord(c->ev_chunk[j], c->copy_stream));
+                        HIPCHK(hipStreamWaitEvent(c->stream, c->ev_chunk[j], 0));
+                        std::vector<Window> w{{off + b0, off + b0 + len[j], uint64_t(uintptr_t(st + b0))}};
+                        if ((rc = run_windows(c->dt, *c->plan, c->count, c->base, w, false, 1, c->stream)))
+                            return rc;
+                    }
+                    HIPCHK(hipEventRecord(c->ev_free, c->stream));
                 }
-                last[s] = true;
-                off += n;
+                c->rec_free = true;
+                off += piece;
             }
         }
         // the user stream observes completion of this call's copies (an event the caller
         // records on it after the call covers the whole message)
-        for (int s = 0; s < 2; ++s)
-            if (last[s] && dir == 0)
-                HIPCHK(hipStreamWaitEvent(c->stream, c->ev_c[s], 0));
+        if (dir == 0)
+            HIPCHK(hipStreamWaitEvent(c->stream, c->ev_free, 0));
     }
     if (!c->async)
         HIPCHK(hipStreamSynchronize(c->stream));

@@ -29,7 +29,8 @@ struct Tuning {
     long spass = 1;       // task of a streaming leaf: this many unrolled workgroup passes
     int hostdirect = 3;   // pinned host iovecs moved by the kernel itself over PCIe (no HBM
                           // staging): bit 0 unpack, bit 1 pack (end to end)
-    long stage_mb = 64;   // HBM staging slot (two per convertor) for pageable host iovecs
+    long stage_mb = 256;  // HBM staging buffer (one per convertor) for pageable host iovecs: the
+                          // largest piece of a host window moved in one kernel/copy overlap
     long hd_grid = 256;   // workgroup cap of an unpack launch reading pinned host memory (0 = none):
                           // PCIe reads lose rate to thousands of workgroups, writes do not
                           // (scripts/ubench_pcie.hip, profiles/r2_ubench_pcie.log)

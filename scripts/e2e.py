@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--tune", default="", help="extra ddt_tune settings, k=v;k=v")
     ap.add_argument("--hostdirect", type=int, default=-1,
                     help="ddt_tune('hostdirect'): 1 = kernel moves pinned host bytes itself, 0 = HBM staging")
+    ap.add_argument("--pageable", action="store_true",
+                    help="host packed stream in pageable memory (staged through HBM slots)")
     ap.add_argument("--variants", default="",
                     help="several runs in one process, '|'-separated tune strings (k=v;k=v), each "
                          "with fresh convertors (the staging slot size is read when a slot is made)")
@@ -76,7 +78,7 @@ def run(args, tune):
     user = torch.randint(1, 255, (span,), dtype=torch.uint8, device=dev)
     uptr = user.data_ptr() + origin
     dpk = torch.empty(S, dtype=torch.uint8, device=dev)
-    hpk = torch.empty(S, dtype=torch.uint8, pin_memory=True)
+    hpk = torch.empty(S, dtype=torch.uint8, pin_memory=not args.pageable)
     st = torch.cuda.current_stream(dev)
     cp, cu = ompi_amd.Convertor(), ompi_amd.Convertor()
     for c in (cp, cu):
@@ -166,6 +168,7 @@ def run(args, tune):
     same_u = bool(torch.equal(got_o, user))
     user.copy_(keep)
     out = {"config": args.config, "workload": desc["workload"], "packed_bytes": S,
+           "host_memory": "pageable" if args.pageable else "pinned",
            "hostdirect": int(args.hostdirect), "stage_mb": args.stage_mb, "tune": tune,
            "overlapped_matches_device_path": same, "overlapped_unpack_matches": same_u,
            "GiBs": {k: round(S / v / GiB, 2) for k, v in t.items()},
