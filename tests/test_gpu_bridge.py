@@ -441,7 +441,8 @@ def test_engine_async_unpack_slot_reuse_across_calls(device, mode):
     c.set_stream(s, True)
     for k, out in enumerate(outs):
         c.prepare_for_recv(e, 1, out.data_ptr() + origin)
-        for a, n in ((0, 17 << 20), (17 << 20, 3), ((17 << 20) + 3, size - (17 << 20) - 3)):
+        # a 25 MiB window (staged in two overlapped chunks), 3 bytes, the rest (one chunk)
+        for a, n in ((0, 25 << 20), (25 << 20, 3), ((25 << 20) + 3, size - (25 << 20) - 3)):
             c.set_position(a)
             rc, _, md = c.unpack([(src[k % 2].data_ptr() + a, n)])
             assert md == n
@@ -451,6 +452,41 @@ def test_engine_async_unpack_slot_reuse_across_calls(device, mode):
     ompi_amd.lib().ddt_tune(b"hostdirect", 3)
     for out in outs:
         np.testing.assert_array_equal(_host(out), want)
+
+
+@pytest.mark.parametrize("mode", ["pinned-staged", "pageable-staged"])
+def test_engine_async_pack_staging_across_calls(device, mode):
+    """Back-to-back asynchronous packs into host buffers through ONE engine convertor: each
+    call's kernels rewrite the staging buffer only after the previous call's D2H copies have
+    read it; windows of 30 MiB (two overlapped chunks, kernels queued before the copies) and
+    10 MiB (one chunk)."""
+    import torch
+    import ompi_amd
+    ompi_amd.lib().ddt_tune(b"hostdirect", 0 if mode == "pinned-staged" else 3)
+    rec = ("vector", 5 << 20, 2, 3, ("basic", FLOAT4))   # 40 MiB packed
+    b = R.Built(rec)
+    e = b.engine()
+    info = b.o.info()
+    size = info["size"]
+    span, origin = R.layout(info, 1)
+    srcs = [R.fill(span, 40 + k) for k in range(3)]
+    users = [_dev(h, device) for h in srcs]
+    refs = [np.frombuffer(b.o.pack(1, h, origin, 0, size, element_granular=False), dtype=np.uint8)
+            for h in srcs]
+    pin = mode.startswith("pinned")
+    dsts = [torch.zeros(size, dtype=torch.uint8, pin_memory=pin) for _ in range(3)]
+    s = torch.cuda.Stream(device)
+    c = ompi_amd.Convertor()
+    c.set_stream(s, True)
+    for k in range(3):
+        c.prepare_for_send(e, 1, users[k].data_ptr() + origin)
+        for a, n in ((0, 30 << 20), (30 << 20, size - (30 << 20))):
+            rc, _, md = c.pack([(dsts[k].data_ptr() + a, n)])
+            assert md == n
+    s.synchronize()
+    ompi_amd.lib().ddt_tune(b"hostdirect", 3)
+    for k in range(3):
+        np.testing.assert_array_equal(dsts[k].numpy(), refs[k])
 
 
 # ------------------------------------------------------------------ unpack_ooo.c
