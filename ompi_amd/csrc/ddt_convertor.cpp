@@ -328,8 +328,11 @@ struct ddt_convertor {
     // only after the last reader of its previous contents -- the D2H copies of a pack or
     // the kernels of an unpack (ev_free), possibly queued by an earlier asynchronous call
     // -- has passed (pml_ob1_recvreq.c:627-663 issues such back-to-back async unpacks).
+    // The buffer grows with the largest piece a call stages (1 MiB steps, doubling, up to
+    // stage_mb): a convertor that stages kilobyte fragments holds a megabyte, not 256.
     void *stage = nullptr;
     uint64_t stage_size = 0;
+    std::vector<void *> outgrown;   // earlier, smaller buffers: freed with the convertor
     hipStream_t copy_stream = nullptr;
     hipEvent_t ev_chunk[2] = {nullptr, nullptr};
     hipEvent_t ev_free = nullptr;
@@ -346,19 +349,31 @@ struct ddt_convertor {
             (void) hipEventSynchronize(ev_free);
         if (stage)
             (void) hipFree(stage);
+        for (void *p : outgrown)
+            (void) hipFree(p);
         for (hipEvent_t e : {ev_chunk[0], ev_chunk[1], ev_free})
             if (e)
                 (void) hipEventDestroy(e);
     }
-    int ensure_staging()
+    // a staging buffer of at least min(need, stage_mb) bytes
+    int ensure_staging(uint64_t need)
     {
-        if (copy_stream)
+        if (!copy_stream) {
+            HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+            for (hipEvent_t *e : {&ev_chunk[0], &ev_chunk[1], &ev_free})
+                HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        }
+        const uint64_t cap = std::max<uint64_t>(stage_bytes(), 1u << 20), mib = 1u << 20;
+        uint64_t want = (std::min(need, cap) + mib - 1) / mib * mib;
+        if (stage_size >= want)
             return DDT_SUCCESS;
-        HIPCHK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
-        stage_size = stage_bytes();
-        HIPCHK(hipMalloc(&stage, stage_size));
-        for (hipEvent_t *e : {&ev_chunk[0], &ev_chunk[1], &ev_free})
-            HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        want = std::max(want, std::min(cap, stage_size * 2));
+        void *p = nullptr;
+        HIPCHK(hipMalloc(&p, want));
+        if (stage)
+            outgrown.push_back(stage);   // may still be read by queued work: kept until destruction
+        stage = p;
+        stage_size = want;
         return DDT_SUCCESS;
     }
 };
@@ -389,7 +404,10 @@ int execute(ddt_convertor *c, const std::vector<Window> &dev_wins,
     if (rc != DDT_SUCCESS)
         return rc;
     if (!host_wins.empty()) {
-        if ((rc = c->ensure_staging()) != DDT_SUCCESS)
+        uint64_t need = 0;
+        for (const auto &hw : host_wins)
+            need = std::max(need, hw.first.w1 - hw.first.w0);
+        if ((rc = c->ensure_staging(need)) != DDT_SUCCESS)
             return rc;
         char *st = static_cast<char *>(c->stage);
         for (const auto &hw : host_wins) {
