@@ -150,3 +150,39 @@ def test_exported_descriptions_round_trip():
         t = D.from_opal_desc(desc, info["size"], info["lb"], info["ub"], info["true_lb"], info["true_ub"])
         np.testing.assert_array_equal(E.engine_blocks(t), E.oracle_blocks(b.o))
     assert loops > 50
+
+
+def test_import_cache_under_concurrent_threads():
+    """One thread per convertor is the reference's contract, but many threads share the
+    datatypes: eight threads attach convertors to the same six descriptions at once (ctypes
+    releases the GIL inside the calls).  Each description is imported exactly once and
+    every later attach hits the cache."""
+    import threading
+    L = S.bridge_lib()
+    L.opal_hip_bridge_finalize()
+    base = S.stats()
+    types = [_xface(n) for n in (8, 12, 16, 20, 24, 28)]
+    errors = []
+
+    def worker(k):
+        try:
+            for i in range(60):
+                t = types[(k + i) % len(types)]
+                rc = S.Convertor().prepare(t, 1 + i % 3, 0x7000_0000_0000, send=bool(i % 2))
+                assert rc == S.OPAL_SUCCESS
+        except Exception as ex:   # noqa: BLE001 - reported below
+            errors.append(repr(ex))
+
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors
+    st = S.stats()
+    assert st["imports"] - base["imports"] == len(types)
+    assert st["hits"] - base["hits"] == 8 * 60 - len(types)
+    assert st["entries"] == len(types)
+    for t in types:
+        t.destruct()
+    assert S.stats()["entries"] == 0
