@@ -1126,13 +1126,19 @@ static int window_common(const ddt_datatype_t *t, size_t count, const void *buf,
     uint64_t w1 = std::min<uint64_t>(w0 + len, c.local_size);
     std::vector<Window> dev;
     std::vector<std::pair<Window, void *>> host;
+    bool pcie = false;
     if (w1 > w0) {
+        uint64_t hd = 0;
         if (classify(packed) == MEM_DEVICE)
             dev.push_back({w0, w1, uint64_t(uintptr_t(packed))});
-        else
+        else if ((tuning().hostdirect & (dir == 0 ? 2 : 1)) && (hd = pinned_device_range(packed, w1 - w0)) != 0) {
+            dev.push_back({w0, w1, hd});   // pinned host window: the kernel moves it over PCIe
+            pcie = true;
+        } else {
             host.push_back({{w0, w1, 0}, packed});
+        }
     }
-    rc = execute(&c, dev, host, dir);
+    rc = execute(&c, dev, host, dir, pcie);
     if (rc == DDT_SUCCESS && !host.empty())
         HIPCHK(hipStreamSynchronize(c.stream));   // staging slots die with `c`
     c.stream = nullptr;

@@ -675,6 +675,62 @@ def sorted_from(request):
     L.ddt_tune(b"sorted", -1)
 
 
+@pytest.mark.parametrize("seed", range(int(__import__("os").environ.get("DDT_FUZZ_PINNED_SEEDS", "2"))))
+def test_fuzz_pinned_host_iovecs_capped_grid(device, seed):
+    """Random types packed into and unpacked from PINNED host memory, which the kernel moves
+    over PCIe itself: with the workgroup cap of such launches forced down to 8 (ddt_tune
+    hd_grid / hd_grid_pack) every item kind -- affine, fragments, index lists with their LDS
+    scans -- runs inside the grid-stride loop.  MPI_Pack / MPI_Unpack and the UCX window
+    API (pack_window / unpack_window at a random offset) against the oracle."""
+    import torch
+    import ompi_amd
+    from ompi_amd import convertor as CV
+    L = ompi_amd.lib()
+    L.ddt_tune(b"hd_grid", 8)
+    L.ddt_tune(b"hd_grid_pack", 8)
+    try:
+        rng = random.Random(9100 + seed)
+        tested = 0
+        for n in range(50):
+            b = R.Built(R.random_recipe(rng))
+            info = b.o.info()
+            count = rng.choice([1, 2, 5])
+            size = info["size"] * count
+            if size == 0 or _overlapping(b.o, count):
+                continue
+            span, origin = R.layout(info, count)
+            host = R.fill(span, 300 + n)
+            user = _dev(host, device)
+            e = b.engine()
+            ref = np.frombuffer(b.o.pack(count, host, origin, 0, size, element_granular=False), dtype=np.uint8)
+            pk = torch.zeros(size, dtype=torch.uint8).pin_memory()
+            assert ompi_amd.pack(user.data_ptr() + origin, count, e, pk.data_ptr(), size, 0) == size
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(pk.numpy(), ref, err_msg=str(b.recipe))
+            out = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
+            exp = np.full(span, 0xA5, dtype=np.uint8)
+            b.o.unpack(count, exp, origin, 0, ref.tobytes())
+            assert ompi_amd.unpack(pk.data_ptr(), size, 0, out.data_ptr() + origin, count, e) == size
+            np.testing.assert_array_equal(_host(out), exp, err_msg=str(b.recipe))
+            # a window of the stream through the UCX-style API, pinned on both directions
+            off = rng.randrange(size)
+            ln = rng.randrange(1, size - off + 1)
+            win = torch.zeros(ln, dtype=torch.uint8).pin_memory()
+            assert CV.pack_window(e, count, user.data_ptr() + origin, off, win.data_ptr(), ln) == ln
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(win.numpy(), ref[off:off + ln], err_msg=str(b.recipe))
+            out2 = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
+            exp2 = np.full(span, 0xA5, dtype=np.uint8)
+            b.o.unpack(count, exp2, origin, off, ref[off:off + ln].tobytes())
+            CV.unpack_window(e, count, out2.data_ptr() + origin, off, win.data_ptr(), ln)
+            np.testing.assert_array_equal(_host(out2), exp2, err_msg=str(b.recipe))
+            tested += 1
+        assert tested > 20
+    finally:
+        L.ddt_tune(b"hd_grid", 256)
+        L.ddt_tune(b"hd_grid_pack", 0)
+
+
 @pytest.mark.parametrize("esz,count,density", [(4, 1, 4), (4, 2, 3), (8, 1, 5), (16, 2, 4), (4, 1, 64)])
 def test_sorted_list_engine(device, sorted_from, esz, count, density):
     """Single-element index lists through ddt_sorted.hip (forced from 1 block): several
