@@ -1,5 +1,5 @@
 // ddt_device.h -- launch descriptors shared by the host plan compiler and the
-// gfx950 kernels (ddt_kernels.hip).  Plain-old-data only.
+// gfx950 kernels (ddt_move.hip.h, ddt_kernels.hip).  Plain-old-data only.
 #pragma once
 
 #include <cstdint>

@@ -20,544 +20,22 @@
 #include "ddt_device.h"
 #include "ddt_plan.h"
 
+// The move kernel itself lives in ddt_move.hip.h and is instantiated in four translation
+// units (ddt_move_{p,u}{0,1}.hip: pack / unpack x without / with index lists) that the build
+// compiles in parallel; this file dispatches to them and holds the external32 kernel.
+
 namespace ddt {
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-template <int U> struct Vec;
-template <> struct Vec<16> { using T = u32x4; };
-template <> struct Vec<8> { using T = u32x2; };
-template <> struct Vec<4> { using T = uint32_t; };
-template <> struct Vec<2> { using T = uint16_t; };
-template <> struct Vec<1> { using T = uint8_t; };
-
-// Nest of an item, ND dims kept in registers (ND = 0: generic MAXD path).
-template <int ND> struct Nest {
-    static constexpr int N = ND > 0 ? ND : MAXD;
-    uint32_t ndim;
-    uint32_t cnt[N];
-    FastDiv fd[N];
-    int64_t us[N];
-    int64_t ps[N];
-};
-
-template <int ND>
-__device__ __forceinline__ void load_nest(const Item *it, Nest<ND> &n)
-{
-    n.ndim = ND > 0 ? uint32_t(ND) : it->ndim;
-#pragma unroll
-    for (int j = 0; j < Nest<ND>::N; ++j) {
-        n.cnt[j] = uint32_t(it->cnt[j]);
-        n.fd[j] = it->fd[j];
-        n.us[j] = it->ustr[j];
-        n.ps[j] = it->pstr[j];
-    }
-}
-
-// block index -> (user, packed) byte offsets over the nest (32-bit index path)
-template <int ND>
-__device__ __forceinline__ void nest_offsets32(const Nest<ND> &n, uint32_t blk, int64_t &uo, int64_t &po)
-{
-#pragma unroll
-    for (int j = Nest<ND>::N - 1; j > 0; --j) {
-        if (ND > 0 || j < int(n.ndim)) {
-            uint32_t q = fastdiv(blk, n.fd[j]);
-            uint32_t idx = blk - q * n.cnt[j];
-            blk = q;
-            uo += int64_t(idx) * n.us[j];
-            po += int64_t(idx) * n.ps[j];
-        }
-    }
-    if (ND > 0 || n.ndim > 0) {
-        uo += int64_t(blk) * n.us[0];
-        po += int64_t(blk) * n.ps[0];
-    }
-}
-
-__device__ __forceinline__ void nest_offsets64(const Item *it, uint64_t blk, int64_t &uo, int64_t &po)
-{
-    for (int j = int(it->ndim) - 1; j > 0; --j) {
-        uint64_t c = it->cnt[j];
-        uint64_t idx = blk % c;
-        blk /= c;
-        uo += int64_t(idx) * it->ustr[j];
-        po += int64_t(idx) * it->pstr[j];
-    }
-    if (it->ndim > 0) {
-        uo += int64_t(blk) * it->ustr[0];
-        po += int64_t(blk) * it->pstr[0];
-    }
-}
-
-template <int U> constexpr int unroll() { return unroll_of(U); }
-
-// Item::user / Item::packed are offsets from the launch's two base pointers (Bases), so one
-// descriptor set serves every buffer pair with the same 16-byte alignment (ddt_convertor.cpp).
-struct Bases {
-    uint64_t u, p;
-};
-
-template <int U, int DIR>
-__device__ __noinline__ void run_affine64(const Item *it, Bases bs, uint64_t ub, uint64_t ue)
-{
-    using T = typename Vec<U>::T;
-    const uint64_t user = bs.u + it->user, packed = bs.p + it->packed, upb = it->upb;
-    for (uint64_t u = ub + threadIdx.x; u < ue; u += THREADS) {
-        uint64_t blk = u / upb, within = u - blk * upb;
-        int64_t uo = int64_t(within) * U, po = uo;
-        nest_offsets64(it, blk, uo, po);
-        const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
-        T *dst = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
-        *dst = *src;
-    }
-}
-
-template <typename T, bool NT> __device__ __forceinline__ T ld(const T *p)
-{
-    if constexpr (NT) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-// Write-through store (sc1): the line is not allocated dirty in L2; the bytes go on to
-// the memory side with their byte mask (Item::wt, use_wt in ddt_plan.cpp).
-__device__ __forceinline__ void st_wt(uint8_t *p, uint8_t v)
-{
-    asm volatile("global_store_byte %0, %1, off sc1" ::"v"(p), "v"(uint32_t(v)) : "memory");
-}
-__device__ __forceinline__ void st_wt(uint16_t *p, uint16_t v)
-{
-    asm volatile("global_store_short %0, %1, off sc1" ::"v"(p), "v"(uint32_t(v)) : "memory");
-}
-__device__ __forceinline__ void st_wt(uint32_t *p, uint32_t v)
-{
-    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void st_wt(u32x2 *p, u32x2 v)
-{
-    asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void st_wt(u32x4 *p, u32x4 v)
-{
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-
-template <typename T, bool WT> __device__ __forceinline__ void st(T *p, T v)
-{
-    if constexpr (WT) st_wt(p, v);
-    else *p = v;
-}
-
-// NT: 0 plain; 1 non-temporal user-side loads (pack of sparse gathers, Item::nt == 1);
-// streaming leaves (Item::nt >= 2): 2 every load and store non-temporal, 3 loads only,
-// 4 stores only, 5 loads only and only when packing (the user-side rows).
-template <int U, int DIR, int ND, int NT, bool WT>
-__device__ __forceinline__ void run_affine(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
-{
-    using T = typename Vec<U>::T;
-    constexpr int K = unroll<U>();
-    const uint64_t user = bs.u + it->user, packed = bs.p + it->packed;
-    Nest<ND> n;
-    load_nest(it, n);
-    const FastDiv fdu = it->fd_upb;
-    const uint32_t upb = uint32_t(it->upb);
-    for (uint32_t base = ub + threadIdx.x; base < ue; base += THREADS * K) {
-        T v[K];
-        T *dst[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t u = base + uint32_t(k) * THREADS;
-            dst[k] = nullptr;
-            if (u < ue) {
-                const uint32_t blk = fastdiv(u, fdu);
-                const uint32_t within = u - blk * upb;
-                int64_t uo = int64_t(within) * U, po = uo;
-                nest_offsets32(n, blk, uo, po);
-                const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
-                dst[k] = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
-                v[k] = ld<T, ((NT == 1 || NT == 5) && DIR == 0) || NT == 2 || NT == 3>(src);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            if (dst[k]) {
-                if constexpr (NT == 2 || NT == 4)
-                    __builtin_nontemporal_store(v[k], dst[k]);
-                else
-                    st<T, WT>(dst[k], v[k]);   // (nt scattered stores measured slower: 51 vs 18 us)
-            }
-    }
-}
-
-template <int U, int DIR>
-__device__ __noinline__ void run_list_uni64(const Item *it, Bases bs, uint64_t ub, uint64_t ue)
-{
-    using T = typename Vec<U>::T;
-    const uint64_t user = bs.u + it->user, packed = bs.p + it->packed, ulen = it->ulen;
-    const bool d32 = it->ldisp32 != 0;
-    const int32_t *disp32 = reinterpret_cast<const int32_t *>(it->ldisp);
-    const int64_t *disp64 = reinterpret_cast<const int64_t *>(it->ldisp);
-    const uint64_t upb = it->upb, nb = it->nblk;
-    for (uint64_t u = ub + threadIdx.x; u < ue; u += THREADS) {
-        uint64_t blk = u / upb, within = u - blk * upb;
-        uint64_t i = blk % nb, outer = blk / nb;
-        int64_t uo = 0, po = 0;
-        nest_offsets64(it, outer, uo, po);
-        int64_t d = d32 ? int64_t(disp32[i]) : disp64[i];
-        uo += d + int64_t(within) * U;
-        po += (it->same ? d : int64_t(i * ulen)) + int64_t(within) * U;
-        const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
-        T *dst = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
-        *dst = *src;
-    }
-}
-
-// Index list with one block length: all K displacement loads of a round are issued
-// (coalesced) before the K dependent gathers, so each round pays two memory latencies
-// instead of 2K.
-template <int U, int DIR, bool WT>
-__device__ __forceinline__ void run_list_uni(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
-{
-    using T = typename Vec<U>::T;
-    constexpr int K = unroll<U>();
-    const uint64_t user = bs.u + it->user, packed = bs.p + it->packed;
-    const uint64_t ulen = it->ulen;
-    const bool d32 = it->ldisp32 != 0;
-    const bool same = it->same != 0;
-    const int32_t *disp32 = reinterpret_cast<const int32_t *>(it->ldisp);
-    const int64_t *disp64 = reinterpret_cast<const int64_t *>(it->ldisp);
-    Nest<0> n;
-    load_nest(it, n);
-    const FastDiv fdu = it->fd_upb, fdn = it->fd_nblk;
-    const uint32_t upb = uint32_t(it->upb), nb = uint32_t(it->nblk);
-    for (uint32_t base = ub + threadIdx.x; base < ue; base += THREADS * K) {
-        int64_t uo[K], po[K];
-        uint32_t ii[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t u = base + uint32_t(k) * THREADS;
-            const uint32_t uu = u < ue ? u : ub;   // clamp: keeps the loads in bounds
-            const uint32_t blk = fastdiv(uu, fdu);
-            const uint32_t within = uu - blk * upb;
-            const uint32_t outer = fastdiv(blk, fdn);
-            ii[k] = blk - outer * nb;
-            uo[k] = int64_t(within) * U;
-            po[k] = int64_t(uint64_t(ii[k]) * ulen) + int64_t(within) * U;
-            nest_offsets32(n, outer, uo[k], po[k]);
-        }
-        int64_t d[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            d[k] = d32 ? int64_t(disp32[ii[k]]) : disp64[ii[k]];
-        if (same) {
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                po[k] += d[k] - int64_t(uint64_t(ii[k]) * ulen);
-        }
-        T v[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo[k] + d[k] : packed + po[k]);
-            v[k] = *src;
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if (base + uint32_t(k) * THREADS < ue) {
-                T *dst = reinterpret_cast<T *>(DIR == 0 ? packed + po[k] : user + uo[k] + d[k]);
-                st<T, WT>(dst, v[k]);
-            }
-        }
-    }
-}
-
-template <int U>
-__device__ __forceinline__ void copy_run(uint8_t *dst, const uint8_t *src, uint64_t n)
-{
-    using T = typename Vec<U>::T;
-    for (uint64_t o = 0; o < n; o += U)
-        *reinterpret_cast<T *>(dst + o) = *reinterpret_cast<const T *>(src + o);
-}
-
-__device__ __forceinline__ void copy_bytes_aligned(uint8_t *dst, const uint8_t *src, uint64_t n, uint32_t U)
-{
-    const uint64_t a = uint64_t(uintptr_t(dst)) | uint64_t(uintptr_t(src)) | n;
-    if (U >= 16 && (a & 15) == 0) copy_run<16>(dst, src, n);
-    else if (U >= 8 && (a & 7) == 0) copy_run<8>(dst, src, n);
-    else if (U >= 4 && (a & 3) == 0) copy_run<4>(dst, src, n);
-    else if (U >= 2 && (a & 1) == 0) copy_run<2>(dst, src, n);
-    else copy_run<1>(dst, src, n);
-}
-
-// Variable-length index list: one wave per group of 64 blocks.  Block packed offsets
-// come from the per-group base (plan time) plus a wave-level exclusive prefix scan of
-// the 64 block lengths, so no per-block packed offset is stored in HBM.
-template <int DIR>
-__device__ __forceinline__ void run_list_var(const Item *it, Bases bs, uint64_t ub, uint64_t ue)
-{
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t user = bs.u + it->user, packed = bs.p + it->packed;
-    const uint32_t *len = reinterpret_cast<const uint32_t *>(it->llen);
-    const uint64_t *goff = reinterpret_cast<const uint64_t *>(it->lgoff);
-    const bool d32 = it->ldisp32 != 0;
-    const int32_t *disp32 = reinterpret_cast<const int32_t *>(it->ldisp);
-    const int64_t *disp64 = reinterpret_cast<const int64_t *>(it->ldisp);
-    const uint64_t ng = it->upb, nb = it->nblk, total = it->ulen;
-    const int64_t w0 = it->w0, w1 = it->w1;
-    for (uint64_t gu = ub + uint64_t(wave); gu < ue; gu += THREADS / 64) {
-        const uint64_t outer = gu / ng, g = gu - outer * ng;
-        int64_t uo = 0, po = 0;
-        nest_offsets64(it, outer, uo, po);
-        const uint64_t i = g * 64 + uint64_t(lane);
-        const bool valid = i < nb;
-        const uint64_t l = valid ? len[i] : 0;
-        uint64_t incl = l;
-#pragma unroll
-        for (int s = 1; s < 64; s <<= 1) {
-            uint64_t y = __shfl_up(incl, s, 64);
-            if (lane >= s) incl += y;
-        }
-        const uint64_t excl = incl - l;
-        const int64_t lx = int64_t(outer * total + goff[g] + excl);   // leaf-local offset
-        const int64_t s0 = lx > w0 ? lx : w0;
-        const int64_t s1 = (lx + int64_t(l)) < w1 ? lx + int64_t(l) : w1;
-        if (valid && s1 > s0) {
-            const int64_t d = d32 ? int64_t(disp32[i]) : disp64[i];
-            const int64_t off = s0 - lx;
-            uint8_t *up = reinterpret_cast<uint8_t *>(user + uo + d + off);
-            uint8_t *pp = reinterpret_cast<uint8_t *>(packed + po + (it->same ? d : int64_t(goff[g] + excl)) + off);
-            if (DIR == 0) copy_bytes_aligned(pp, up, uint64_t(s1 - s0), it->U);
-            else copy_bytes_aligned(up, pp, uint64_t(s1 - s0), it->U);
-        }
-    }
-}
-
-// Deep nests (> 4 dims) are rare: their dims are re-read from the (cached) item on every
-// unit instead of being held in registers, which keeps the kernel's SGPR budget small.
-template <int U, int DIR, int NT, bool WT>
-__device__ __forceinline__ void run_affine_deep(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
-{
-    using T = typename Vec<U>::T;
-    const uint64_t user = bs.u + it->user, packed = bs.p + it->packed;
-    const FastDiv fdu = it->fd_upb;
-    const uint32_t upb = uint32_t(it->upb);
-    const int nd = int(it->ndim);
-    for (uint32_t u = ub + threadIdx.x; u < ue; u += THREADS) {
-        uint32_t blk = fastdiv(u, fdu);
-        const uint32_t within = u - blk * upb;
-        int64_t uo = int64_t(within) * U, po = uo;
-        for (int j = nd - 1; j > 0; --j) {
-            const uint32_t q = fastdiv(blk, it->fd[j]);
-            const uint32_t idx = blk - q * uint32_t(it->cnt[j]);
-            blk = q;
-            uo += int64_t(idx) * it->ustr[j];
-            po += int64_t(idx) * it->pstr[j];
-        }
-        uo += int64_t(blk) * it->ustr[0];
-        po += int64_t(blk) * it->pstr[0];
-        const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
-        T *dst = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
-        st<T, WT>(dst, ld<T, NT == 1 && DIR == 0>(src));
-    }
-}
-
-template <int U, int DIR, int NT, bool WT>
-__device__ __forceinline__ void dispatch_affine_u(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
-{
-    switch (it->ndim) {
-    case 1: run_affine<U, DIR, 1, NT, WT>(it, bs, ub, ue); break;
-    case 2: run_affine<U, DIR, 2, NT, WT>(it, bs, ub, ue); break;
-    case 3: run_affine<U, DIR, 3, NT, WT>(it, bs, ub, ue); break;
-    case 4: run_affine<U, DIR, 4, NT, WT>(it, bs, ub, ue); break;
-    default: run_affine_deep<U, DIR, NT, WT>(it, bs, ub, ue); break;
-    }
-}
-
-template <int DIR, int NT, bool WT>
-__device__ __forceinline__ void dispatch_affine(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
-{
-    switch (it->U) {
-    case 16: dispatch_affine_u<16, DIR, NT, WT>(it, bs, ub, ue); break;
-    case 8: dispatch_affine_u<8, DIR, NT, WT>(it, bs, ub, ue); break;
-    case 4: dispatch_affine_u<4, DIR, NT, WT>(it, bs, ub, ue); break;
-    case 2: dispatch_affine_u<2, DIR, NT, WT>(it, bs, ub, ue); break;
-    default: dispatch_affine_u<1, DIR, NT, WT>(it, bs, ub, ue); break;
-    }
-}
-
-// wt = 1 asks for write-through user-side stores (unpack); wt = 2 for every store.
-template <int DIR>
-__device__ __forceinline__ bool wt_stores(const Item *it)
-{
-    return it->wt == 2 || (DIR == 1 && it->wt == 1);
-}
-
-template <int DIR, bool WT>
-__device__ __forceinline__ void dispatch_list_uni(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
-{
-    switch (it->U) {
-    case 16: run_list_uni<16, DIR, WT>(it, bs, ub, ue); break;
-    case 8: run_list_uni<8, DIR, WT>(it, bs, ub, ue); break;
-    case 4: run_list_uni<4, DIR, WT>(it, bs, ub, ue); break;
-    case 2: run_list_uni<2, DIR, WT>(it, bs, ub, ue); break;
-    default: run_list_uni<1, DIR, WT>(it, bs, ub, ue); break;
-    }
-}
-
-// LISTS = false: affine + fragment items only (vector/hvector/subarray/struct nests), a
-// lean register budget; LISTS = true adds the index-list paths.
-template <int DIR, bool LISTS>
-__device__ __forceinline__ void move_task(const Item *__restrict__ items, uint32_t nitems, Bases bs, uint32_t b)
-{
-    uint32_t lo = 0, hi = nitems - 1;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (items[mid].task_begin <= b) lo = mid;
-        else hi = mid - 1;
-    }
-    const Item *it = items + lo;
-    uint32_t t = b - it->task_begin;
-    if (it->slab) {
-        // Workgroups are dispatched round-robin over the 8 XCDs, so the item's local task t
-        // runs on XCD (task_begin + t) % 8.  Give each XCD one contiguous slab of the item's
-        // tasks instead of every 8th one (a bijection on [0, ntasks)).
-        const uint32_t T = it->ntasks;
-        if (it->slab == SLAB_FULL) {
-            const uint32_t x = t & 7u, i = t >> 3, per = T >> 3, rem = T & 7u;
-            t = x * per + (x < rem ? x : rem) + i;
-        } else {
-            // runs of C tasks per XCD inside groups of 8C (the tail stays round-robin)
-            const uint32_t C = it->slab, G = C * 8u;
-            if (t < T - T % G) {
-                const uint32_t r = t % G;
-                t = t - r + (r & 7u) * C + (r >> 3);
-            }
-        }
-    }
-    const uint64_t ub = it->u0 + t * it->units_per_task;
-    uint64_t ue = ub + it->units_per_task;
-    if (ue > it->u1) ue = it->u1;
-    switch (it->kind) {
-    case ITEM_AFFINE:
-        if (it->idx64) {
-            switch (it->U) {
-            case 16: run_affine64<16, DIR>(it, bs, ub, ue); break;
-            case 8: run_affine64<8, DIR>(it, bs, ub, ue); break;
-            case 4: run_affine64<4, DIR>(it, bs, ub, ue); break;
-            case 2: run_affine64<2, DIR>(it, bs, ub, ue); break;
-            default: run_affine64<1, DIR>(it, bs, ub, ue); break;
-            }
-        } else {
-            if (it->nt >= 2 && it->U == 16) {
-                if (it->nt == 3) dispatch_affine_u<16, DIR, 3, false>(it, bs, uint32_t(ub), uint32_t(ue));
-                else if (it->nt == 4) dispatch_affine_u<16, DIR, 4, false>(it, bs, uint32_t(ub), uint32_t(ue));
-                else if (it->nt == 5) dispatch_affine_u<16, DIR, 5, false>(it, bs, uint32_t(ub), uint32_t(ue));
-                else dispatch_affine_u<16, DIR, 2, false>(it, bs, uint32_t(ub), uint32_t(ue));
-            } else if (wt_stores<DIR>(it)) {
-                if (DIR == 0 && it->nt == 1) dispatch_affine<DIR, 1, true>(it, bs, uint32_t(ub), uint32_t(ue));
-                else dispatch_affine<DIR, 0, true>(it, bs, uint32_t(ub), uint32_t(ue));
-            } else {
-                if (DIR == 0 && it->nt == 1) dispatch_affine<DIR, 1, false>(it, bs, uint32_t(ub), uint32_t(ue));
-                else dispatch_affine<DIR, 0, false>(it, bs, uint32_t(ub), uint32_t(ue));
-            }
-        }
-        break;
-    case ITEM_LIST_UNI:
-        if (!LISTS) break;
-        if (it->idx64) {
-            switch (it->U) {
-            case 16: run_list_uni64<16, DIR>(it, bs, ub, ue); break;
-            case 8: run_list_uni64<8, DIR>(it, bs, ub, ue); break;
-            case 4: run_list_uni64<4, DIR>(it, bs, ub, ue); break;
-            case 2: run_list_uni64<2, DIR>(it, bs, ub, ue); break;
-            default: run_list_uni64<1, DIR>(it, bs, ub, ue); break;
-            }
-        } else {
-            if (wt_stores<DIR>(it)) dispatch_list_uni<DIR, true>(it, bs, uint32_t(ub), uint32_t(ue));
-            else dispatch_list_uni<DIR, false>(it, bs, uint32_t(ub), uint32_t(ue));
-        }
-        break;
-    case ITEM_LIST_VAR:
-        if (LISTS) run_list_var<DIR>(it, bs, ub, ue);
-        break;
-    default:   // ITEM_FRAG
-        if (threadIdx.x == 0) {
-            const uint8_t *src = reinterpret_cast<const uint8_t *>(DIR == 0 ? bs.u + it->user : bs.p + it->packed);
-            uint8_t *dst = reinterpret_cast<uint8_t *>(DIR == 0 ? bs.p + it->packed : bs.u + it->user);
-            for (uint64_t k = 0; k < it->nbytes; ++k)
-                dst[k] = src[k];
-        }
-        break;
-    }
-}
-
-// One workgroup per task, or -- when the launch is capped below the task count (a window
-// in pinned host memory, where PCIe and not the CU count is the limit: a few hundred
-// workgroups keep it full, thousands of them contend for it, scripts/ubench_pcie.hip) --
-// a grid-stride loop over the tasks.  A cap that is a multiple of 8 keeps every task on
-// the XCD the slab mapping chose for it.
-template <int DIR, bool LISTS>
-__device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32_t nitems, Bases bs, uint32_t ntasks)
-{
-    for (uint32_t b = blockIdx.x; b < ntasks; b += gridDim.x) {
-        if (b != blockIdx.x)
-            __syncthreads();   // LDS of the previous task (list scans) is free again
-        move_task<DIR, LISTS>(items, nitems, bs, b);
-    }
-}
-
-template <int DIR, bool LISTS>
-__global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restrict__ items, uint32_t nitems,
-                                                           uint64_t ubase, uint64_t pbase, uint32_t ntasks)
-{
-    move_body<DIR, LISTS>(items, nitems, Bases{ubase, pbase}, ntasks);
-}
-
-// Small launches carry their descriptors in the kernel-argument segment: no device
-// buffer, no upload, no cache entry (fragment pipelines, windows, one-off messages).
-template <int DIR, bool LISTS, uint32_t NI>
-__global__ __launch_bounds__(THREADS) void ddt_move_inline_kernel(ItemBlockN<NI> blk)
-{
-    // read the block in place from the kernarg segment (taking the address of `blk`
-    // would copy it to scratch)
-    const ItemBlockN<NI> *kb = reinterpret_cast<const ItemBlockN<NI> *>(
-        (const void *) __builtin_amdgcn_kernarg_segment_ptr());
-    move_body<DIR, LISTS>(kb->items, kb->n, Bases{kb->ubase, kb->pbase}, kb->ntasks);
-}
-
-template <int DIR, bool LISTS, uint32_t NI>
-static void launch_inline_n(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, uint64_t ubase,
-                            uint64_t pbase, hipStream_t stream)
-{
-    ItemBlockN<NI> b;
-    b.n = blk.n;
-    b.ntasks = ntasks;
-    b.ubase = ubase;
-    b.pbase = pbase;
-    for (uint32_t i = 0; i < blk.n; ++i)
-        b.items[i] = blk.items[i];
-    hipLaunchKernelGGL((ddt_move_inline_kernel<DIR, LISTS, NI>), dim3(grid), dim3(THREADS), 0,
-                       stream, b);
-}
-
-template <int DIR, bool LISTS>
-static void launch_inline(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, uint64_t ubase, uint64_t pbase,
-                          hipStream_t stream)
-{
-    if (blk.n == 1) launch_inline_n<DIR, LISTS, 1>(blk, ntasks, grid, ubase, pbase, stream);
-    else if (blk.n == 2) launch_inline_n<DIR, LISTS, 2>(blk, ntasks, grid, ubase, pbase, stream);
-    else if (blk.n <= 4) launch_inline_n<DIR, LISTS, 4>(blk, ntasks, grid, ubase, pbase, stream);
-    else launch_inline_n<DIR, LISTS, INLINE_ITEMS>(blk, ntasks, grid, ubase, pbase, stream);
-}
-
-template <int DIR>
-static void launch_dir(const Item *d_items, uint32_t nitems, uint32_t ntasks, uint32_t grid, bool lists,
-                       uint64_t ubase, uint64_t pbase, hipStream_t stream)
-{
-    if (lists)
-        hipLaunchKernelGGL((ddt_move_kernel<DIR, true>), dim3(grid), dim3(THREADS), 0, stream,
-                           d_items, nitems, ubase, pbase, ntasks);
-    else
-        hipLaunchKernelGGL((ddt_move_kernel<DIR, false>), dim3(grid), dim3(THREADS), 0, stream,
-                           d_items, nitems, ubase, pbase, ntasks);
-}
+#define DDT_MOVE_DECLARE(TAG)                                                                          \
+    hipError_t launch_move_inline_##TAG(const ItemBlock &blk, uint32_t ntasks, uint32_t grid,          \
+                                        uint64_t ubase, uint64_t pbase, hipStream_t stream);           \
+    hipError_t launch_move_##TAG(const Item *d_items, uint32_t nitems, uint32_t ntasks, uint32_t grid, \
+                                 uint64_t ubase, uint64_t pbase, hipStream_t stream);
+DDT_MOVE_DECLARE(p0)
+DDT_MOVE_DECLARE(p1)
+DDT_MOVE_DECLARE(u0)
+DDT_MOVE_DECLARE(u1)
+#undef DDT_MOVE_DECLARE
 
 hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, uint64_t ubase,
                               uint64_t pbase, hipStream_t stream, uint32_t grid_cap)
@@ -565,14 +43,11 @@ hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bo
     if (ntasks == 0 || blk.n == 0)
         return hipSuccess;
     const uint32_t g = grid_cap && grid_cap < ntasks ? grid_cap : ntasks;
-    if (dir == 0) {
-        if (lists) launch_inline<0, true>(blk, ntasks, g, ubase, pbase, stream);
-        else launch_inline<0, false>(blk, ntasks, g, ubase, pbase, stream);
-    } else {
-        if (lists) launch_inline<1, true>(blk, ntasks, g, ubase, pbase, stream);
-        else launch_inline<1, false>(blk, ntasks, g, ubase, pbase, stream);
-    }
-    return hipGetLastError();
+    if (dir == 0)
+        return lists ? launch_move_inline_p1(blk, ntasks, g, ubase, pbase, stream)
+                     : launch_move_inline_p0(blk, ntasks, g, ubase, pbase, stream);
+    return lists ? launch_move_inline_u1(blk, ntasks, g, ubase, pbase, stream)
+                 : launch_move_inline_u0(blk, ntasks, g, ubase, pbase, stream);
 }
 
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
@@ -582,10 +57,10 @@ hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, in
         return hipSuccess;
     const uint32_t g = grid_cap && grid_cap < ntasks ? grid_cap : ntasks;
     if (dir == 0)
-        launch_dir<0>(d_items, nitems, ntasks, g, lists, ubase, pbase, stream);
-    else
-        launch_dir<1>(d_items, nitems, ntasks, g, lists, ubase, pbase, stream);
-    return hipGetLastError();
+        return lists ? launch_move_p1(d_items, nitems, ntasks, g, ubase, pbase, stream)
+                     : launch_move_p0(d_items, nitems, ntasks, g, ubase, pbase, stream);
+    return lists ? launch_move_u1(d_items, nitems, ntasks, g, ubase, pbase, stream)
+                 : launch_move_u0(d_items, nitems, ntasks, g, ubase, pbase, stream);
 }
 
 // ---------------------------------------------------------------- external32

@@ -2,7 +2,7 @@
 // (MPI_Type_indexed / create_indexed_block / hindexed whose blocks are a few elements of
 // 4, 8 or 16 bytes; BASELINE config 4: 64 Mi random floats out of a 1 GiB buffer).
 //
-// The direct list kernel (ddt_kernels.hip, run_list_uni) issues one memory request per
+// The direct list kernel (ddt_move.hip.h, run_list_uni) issues one memory request per
 // element: a random 4-byte gather over a span far beyond the Infinity Cache runs at the
 // memory-side request ceiling (~44 G requests/s, profiles/r1_ubench4_requests.log), and a
 // random 4-byte scatter is a read-modify-write of a 32-byte sector (~27 G/s).  Here the

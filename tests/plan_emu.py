@@ -3,7 +3,7 @@
 The engine exposes its compiled plan (leaf streams) and the exact launch descriptors
 (``Item``, ompi_amd/csrc/ddt_device.h) a pack/unpack would run.  This module
 re-executes those descriptors with numpy, following the kernel's index arithmetic
-(ompi_amd/csrc/ddt_kernels.hip), so the plan compiler is verified bit-exactly against
+(ompi_amd/csrc/ddt_move.hip.h), so the plan compiler is verified bit-exactly against
 the oracle on CPU.  It is a checker only: the product never runs it.
 """
 from __future__ import annotations
