@@ -12,7 +12,7 @@ done
 # the opal bridge (plain C, gcc in the product build) with the same instrumentation
 /opt/rocm/llvm/bin/clang -std=gnu11 -O1 -g -fPIC -pthread -I../../include -fsanitize=address \
   -fno-omit-frame-pointer -c ../../bridge/opal_datatype_hip_bridge.c -o build_asan/opal_datatype_hip_bridge.o
-for f in ddt_kernels ddt_sorted; do
+for f in ddt_kernels ddt_sorted ddt_move_p0 ddt_move_p1 ddt_move_u0 ddt_move_u1; do
   /opt/rocm/bin/hipcc -std=c++17 -O1 -fPIC -I../../include --offload-arch=gfx950 -x hip \
     -c $f.hip -o build_asan/$f.o
 done
