@@ -14,8 +14,9 @@ done
   -fno-omit-frame-pointer -c ../../bridge/opal_datatype_hip_bridge.c -o build_asan/opal_datatype_hip_bridge.o
 for f in ddt_kernels ddt_sorted ddt_move_p0 ddt_move_p1 ddt_move_u0 ddt_move_u1; do
   /opt/rocm/bin/hipcc -std=c++17 -O1 -fPIC -I../../include --offload-arch=gfx950 -x hip \
-    -c $f.hip -o build_asan/$f.o
+    -c $f.hip -o build_asan/$f.o &
 done
+wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Xarch_host -fsanitize=address \
   -o build_asan/libddt_hip_asan.so build_asan/*.o
 cd ../..
