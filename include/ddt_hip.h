@@ -250,7 +250,8 @@ int ddt_pack_window(const ddt_datatype_t *type, size_t count, const void *buf, s
 int ddt_unpack_window(const ddt_datatype_t *type, size_t count, void *buf, size_t offset,
                       const void *src, size_t len, void *hip_stream);
 /* Device typed copy (opal_datatype_copy_content_same_ddt, opal_datatype_copy.c:141-178):
- * copies count instances from src layout to dst layout of the same type, D2D, one launch. */
+ * copies count instances from src layout to dst layout of the same type, D2D, one launch on
+ * `hip_stream`; synchronous like the reference (the data is in place on return). */
 int ddt_copy_content_same_ddt(const ddt_datatype_t *type, size_t count, void *dst, const void *src,
                               void *hip_stream);
 
