@@ -929,6 +929,49 @@ int ddt_unpack(const void *inbuf, size_t insize, size_t *position, void *outbuf,
     return DDT_SUCCESS;
 }
 
+namespace {
+
+// HBM scratch of the synchronous calls (external32, two-type sndrcv): per thread, per device and per slot,
+// grown on demand and reused (each call ends with a stream synchronisation, so the next
+// call of the thread finds it free).  Round 1 allocated per call, round 2 first with
+// stream-ordered allocations, whose pool returns the memory at every synchronisation: a
+// 16 MiB MPI_Pack_external spent ~300 us of its 357 in allocation (profiles/r2_ext_bench.jsonl).
+struct DevBuf {
+    void *p = nullptr;
+    int slot = 0;
+    explicit DevBuf(int s) : slot(s) {}
+    hipError_t alloc(size_t n)
+    {
+        struct Cache {
+            std::map<std::pair<int, int>, std::pair<void *, size_t>> bufs;   // (device, slot)
+            ~Cache()
+            {
+                for (auto &kv : bufs)
+                    (void) hipFree(kv.second.first);
+            }
+        };
+        thread_local Cache cache;
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess)
+            return e;
+        auto &b = cache.bufs[{dev, slot}];
+        if (b.second < n || !b.first) {
+            if (b.first)
+                (void) hipFree(b.first);
+            b = {nullptr, 0};
+            const size_t want = std::max<size_t>(n, 1u << 20);
+            if ((e = hipMalloc(&b.first, want)) != hipSuccess)
+                return e;
+            b.second = want;
+        }
+        p = b.first;
+        return hipSuccess;
+    }
+};
+
+}  // namespace
+
 int ddt_sndrcv(const void *sbuf, size_t scount, const ddt_datatype_t *st, void *rbuf, size_t rcount,
                const ddt_datatype_t *rt, void *stream)
 {
@@ -975,28 +1018,21 @@ int ddt_sndrcv(const void *sbuf, size_t scount, const ddt_datatype_t *st, void *
     // two datatypes: pack into HBM scratch, unpack from it (the reference pipelines 64 KiB
     // host chunks; here it is one launch per side, stream-ordered)
     const size_t n = std::min(scount * ssz, rcount * rsz);
-    void *tmp = nullptr;
-    HIPCHK(hipMallocAsync(&tmp, n ? n : 1, s));
-    rc = one_side(st, scount, sbuf, tmp, n, 0, &moved);
+    DevBuf tmp(2);
+    HIPCHK(tmp.alloc(n));
+    rc = one_side(st, scount, sbuf, tmp.p, n, 0, &moved);
     if (rc == DDT_SUCCESS && moved)
-        rc = one_side(rt, rcount, rbuf, tmp, moved, 1, &moved);
-    (void) hipFreeAsync(tmp, s);
-    if (rc != DDT_SUCCESS)
+        rc = one_side(rt, rcount, rbuf, tmp.p, moved, 1, &moved);
+    if (rc != DDT_SUCCESS) {
+        (void) hipStreamSynchronize(s);   // the scratch is reused by this thread's next call
         return rc;
+    }
     HIPCHK(hipStreamSynchronize(s));
     return scount * ssz <= rcount * rsz ? DDT_SUCCESS : fail(DDT_ERR_TRUNCATE, "send larger than receive");
 }
 
 // ---------------------------------------------------------------- external32
 namespace {
-
-// Scratch of one external32 call from the stream-ordered pool of the null stream: no
-// hipMalloc / hipFree (and their device synchronisation) per call.
-struct DevBuf {
-    void *p = nullptr;
-    hipError_t alloc(size_t n) { return hipMallocAsync(&p, n ? n : 1, nullptr); }
-    ~DevBuf() { if (p) (void) hipFreeAsync(p, nullptr); }
-};
 
 int ext_plan_for(const ddt_datatype_t *t, std::shared_ptr<ExtPlan> &X)
 {
@@ -1046,7 +1082,7 @@ int ddt_pack_external(const char *datarep, const void *inbuf, size_t incount,
         return DDT_SUCCESS;
     if ((rc = ext_upload(*X)) != DDT_SUCCESS)
         return fail(rc, "external32 table upload");
-    DevBuf tn, te;
+    DevBuf tn(0), te(1);
     HIPCHK(tn.alloc(native));
     ddt_convertor c;
     if ((rc = prepare(&c, t, incount, inbuf, true)) != DDT_SUCCESS)
@@ -1060,8 +1096,8 @@ int ddt_pack_external(const char *datarep, const void *inbuf, size_t incount,
     const bool dev_out = classify(dst) == MEM_DEVICE;
     if (!dev_out)
         HIPCHK(te.alloc(need));
-    HIPCHK(launch_ext(X->d_segs, uint32_t(X->segs.size()), X->d_runs, X->E, incount,
-                      uint64_t(t->size), X->Se, tn.p, dev_out ? dst : te.p, 0, nullptr));
+    HIPCHK(launch_ext(X->d_segs, uint32_t(X->segs.size()), X->d_runs, uint32_t(X->runs.size()), X->E,
+                      incount, uint64_t(t->size), X->Se, tn.p, dev_out ? dst : te.p, 0, X->uniform, nullptr));
     if (!dev_out)
         HIPCHK(hipMemcpy(dst, te.p, need, hipMemcpyDeviceToHost));
     HIPCHK(hipStreamSynchronize(nullptr));
@@ -1091,16 +1127,16 @@ int ddt_unpack_external(const char *datarep, const void *inbuf, ptrdiff_t insize
     if ((rc = prepare(&c, t, outcount, outbuf, false)) != DDT_SUCCESS)
         return rc;
     const char *src = static_cast<const char *>(inbuf) + *position;
-    DevBuf tn, te;
+    DevBuf tn(0), te(1);
     const bool dev_in = classify(src) == MEM_DEVICE;
     if (!dev_in) {
         HIPCHK(te.alloc(need));
         HIPCHK(hipMemcpy(te.p, src, need, hipMemcpyHostToDevice));
     }
     HIPCHK(tn.alloc(native));
-    HIPCHK(launch_ext(X->d_segs, uint32_t(X->segs.size()), X->d_runs, X->E, outcount,
-                      uint64_t(t->size), X->Se, tn.p, dev_in ? const_cast<char *>(src) : te.p, 1,
-                      nullptr));
+    HIPCHK(launch_ext(X->d_segs, uint32_t(X->segs.size()), X->d_runs, uint32_t(X->runs.size()), X->E,
+                      outcount, uint64_t(t->size), X->Se, tn.p, dev_in ? const_cast<char *>(src) : te.p, 1,
+                      X->uniform, nullptr));
     HIPCHK(hipStreamSynchronize(nullptr));
     struct iovec iov{tn.p, native};
     uint32_t n = 1;

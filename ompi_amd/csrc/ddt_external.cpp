@@ -202,6 +202,11 @@ std::shared_ptr<ExtPlan> get_ext_plan(ddt_datatype *t)
                 throw std::logic_error("external32 signature does not cover the type size");
             X->E = e0;
             X->Se = eb;
+            uint32_t c = X->runs.empty() ? 0 : X->runs[0].comp;
+            for (const ConvRun &r : X->runs)
+                if ((r.kind != CONV_COPY && r.kind != CONV_SWAP) || r.nsz != r.esz || r.comp != c)
+                    c = 0;
+            X->uniform = (c == 1 || c == 2 || c == 4 || c == 8 || c == 16) ? c : 0;
         }
     } catch (const std::length_error &ex) {
         X->error = DDT_ERR_NOT_SUPPORTED;

@@ -83,6 +83,21 @@ __device__ __forceinline__ bool swap_words(const uint8_t *from, uint8_t *to, uin
     return true;
 }
 
+// A 2*sizeof(H)-byte component whose addresses are only sizeof(H)-aligned (an 8-byte double
+// at offset 4 of a packed struct{int; double}): swap each half and exchange the halves.
+template <typename H>
+__device__ __forceinline__ bool swap_halves(const uint8_t *from, uint8_t *to, uint32_t n)
+{
+    if ((reinterpret_cast<uintptr_t>(from) | reinterpret_cast<uintptr_t>(to)) % sizeof(H))
+        return false;
+    for (uint32_t b = 0; b < n; b += 2 * sizeof(H)) {
+        const H lo = *reinterpret_cast<const H *>(from + b), hi = *reinterpret_cast<const H *>(from + b + sizeof(H));
+        *reinterpret_cast<H *>(to + b) = bswap(hi);
+        *reinterpret_cast<H *>(to + b + sizeof(H)) = bswap(lo);
+    }
+    return true;
+}
+
 // One long double component (the external stream is byte aligned: bytewise access).
 // Pack: x87 80-bit -> IEEE quad, exact (libgcc __extendxftf2 semantics: the explicit bit is
 // dropped unchecked, a NaN is quieted).  A pseudo-denormal (exponent 0, explicit bit set) has
@@ -174,19 +189,38 @@ __device__ __forceinline__ void convert_elem(const ConvRun &r, const uint8_t *fr
     }
     const uint32_t c = r.comp;
     if (c == 8 && swap_words<uint64_t>(from, to, n)) return;
+    if (c == 8 && swap_halves<uint32_t>(from, to, n)) return;
     if (c == 4 && swap_words<uint32_t>(from, to, n)) return;
+    if (c == 4 && swap_halves<uint16_t>(from, to, n)) return;
     if (c == 2 && swap_words<uint16_t>(from, to, n)) return;
     for (uint32_t base = 0; base < n; base += c)
         for (uint32_t k = 0; k < c; ++k)
             to[base + k] = from[base + c - 1 - k];
 }
 
-template <int DIR>
-__global__ __launch_bounds__(THREADS) void ddt_ext_kernel(const ConvSeg *__restrict__ segs, uint32_t nseg,
-                                                          const ConvRun *__restrict__ runs,
+// General conversion: one thread per element.  The segment/run tables are staged in LDS
+// when they fit (TAB): every element reads a segment (64 B) and a run (40 B) plus the
+// binary-search keys, which from global memory cost more vector loads than the element.
+template <int DIR, bool TAB>
+__global__ __launch_bounds__(THREADS) void ddt_ext_kernel(const ConvSeg *__restrict__ gsegs, uint32_t nseg,
+                                                          const ConvRun *__restrict__ gruns, uint32_t nruns,
                                                           uint64_t E, uint64_t total, uint64_t Sn,
                                                           uint64_t Se, uint8_t *native, uint8_t *ext)
 {
+    extern __shared__ uint64_t tab[];
+    const ConvSeg *segs = gsegs;
+    const ConvRun *runs = gruns;
+    if (TAB) {
+        constexpr uint32_t SW = sizeof(ConvSeg) / 8, RW = sizeof(ConvRun) / 8;
+        const uint64_t *gs = reinterpret_cast<const uint64_t *>(gsegs), *gr = reinterpret_cast<const uint64_t *>(gruns);
+        for (uint32_t i = threadIdx.x; i < nseg * SW; i += THREADS)
+            tab[i] = gs[i];
+        for (uint32_t i = threadIdx.x; i < nruns * RW; i += THREADS)
+            tab[nseg * SW + i] = gr[i];
+        __syncthreads();
+        segs = reinterpret_cast<const ConvSeg *>(tab);
+        runs = reinterpret_cast<const ConvRun *>(tab + nseg * SW);
+    }
     const uint64_t stride = uint64_t(gridDim.x) * THREADS;
     for (uint64_t g = uint64_t(blockIdx.x) * THREADS + threadIdx.x; g < total; g += stride) {
         const uint64_t inst = g / E, r = g - inst * E;
@@ -212,23 +246,97 @@ __global__ __launch_bounds__(THREADS) void ddt_ext_kernel(const ConvSeg *__restr
     }
 }
 
-hipError_t launch_ext(const ConvSeg *segs, uint32_t nseg, const ConvRun *runs, uint64_t E,
+// Uniform conversion: every element of the signature is a C-byte word swap (or a copy, C = 1)
+// and native and external layouts coincide, so the stream is an array of C-byte words (all
+// of MPI_DOUBLE, of MPI_FLOAT, ...).  16 bytes per lane where both ends are 16-byte aligned,
+// then one byte per lane for the tail (or the whole stream when misaligned).  The swap is
+// its own inverse: one kernel serves pack and unpack.
+template <int C>
+__device__ __forceinline__ uint32_t swap_in_word(uint32_t x)
+{
+    if (C == 4) return __builtin_bswap32(x);
+    if (C == 2) return ((x & 0x00FF00FFu) << 8) | ((x >> 8) & 0x00FF00FFu);
+    return x;
+}
+
+template <int C>
+__global__ __launch_bounds__(THREADS) void ddt_ext_uniform_kernel(const uint8_t *__restrict__ from,
+                                                                  uint8_t *__restrict__ to, uint64_t nvec,
+                                                                  uint64_t nbytes)
+{
+    typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+    const uint64_t stride = uint64_t(gridDim.x) * THREADS, t0 = uint64_t(blockIdx.x) * THREADS + threadIdx.x;
+    const v4 *f = reinterpret_cast<const v4 *>(from);
+    v4 *o = reinterpret_cast<v4 *>(to);
+    for (uint64_t i = t0; i < nvec; i += stride) {
+        const v4 v = f[i];
+        v4 w;
+        if (C == 16) {
+            w.x = __builtin_bswap32(v.w);
+            w.y = __builtin_bswap32(v.z);
+            w.z = __builtin_bswap32(v.y);
+            w.w = __builtin_bswap32(v.x);
+        } else if (C == 8) {
+            w.x = __builtin_bswap32(v.y);
+            w.y = __builtin_bswap32(v.x);
+            w.z = __builtin_bswap32(v.w);
+            w.w = __builtin_bswap32(v.z);
+        } else {
+            w.x = swap_in_word<C>(v.x);
+            w.y = swap_in_word<C>(v.y);
+            w.z = swap_in_word<C>(v.z);
+            w.w = swap_in_word<C>(v.w);
+        }
+        o[i] = w;
+    }
+    for (uint64_t b = nvec * 16 + t0; b < nbytes; b += stride) {
+        const uint64_t k = b % C;
+        to[b] = from[b - k + (C - 1 - k)];
+    }
+}
+
+hipError_t launch_ext(const ConvSeg *segs, uint32_t nseg, const ConvRun *runs, uint32_t nruns, uint64_t E,
                       uint64_t count, uint64_t Sn, uint64_t Se, void *native, void *ext, int dir,
-                      hipStream_t stream)
+                      uint32_t uniform, hipStream_t stream)
 {
     const uint64_t total = E * count;
     if (total == 0 || nseg == 0)
         return hipSuccess;
+    uint8_t *n8 = static_cast<uint8_t *>(native), *e8 = static_cast<uint8_t *>(ext);
+    if (uniform) {
+        const uint64_t nbytes = Sn * count;
+        const uint8_t *from = dir == 0 ? n8 : e8;
+        uint8_t *to = dir == 0 ? e8 : n8;
+        const bool al = ((reinterpret_cast<uintptr_t>(from) | reinterpret_cast<uintptr_t>(to)) % 16) == 0;
+        const uint64_t nvec = al ? nbytes / 16 : 0, work = nvec ? nvec : nbytes;
+        uint64_t blocks = (work + THREADS - 1) / THREADS;
+        if (blocks > (1u << 14))
+            blocks = 1u << 14;   // 64 workgroups per CU, grid-stride beyond
+        const dim3 grid{uint32_t(blocks)}, block{THREADS};
+        switch (uniform) {
+        case 16: hipLaunchKernelGGL(ddt_ext_uniform_kernel<16>, grid, block, 0, stream, from, to, nvec, nbytes); break;
+        case 8: hipLaunchKernelGGL(ddt_ext_uniform_kernel<8>, grid, block, 0, stream, from, to, nvec, nbytes); break;
+        case 4: hipLaunchKernelGGL(ddt_ext_uniform_kernel<4>, grid, block, 0, stream, from, to, nvec, nbytes); break;
+        case 2: hipLaunchKernelGGL(ddt_ext_uniform_kernel<2>, grid, block, 0, stream, from, to, nvec, nbytes); break;
+        case 1: hipLaunchKernelGGL(ddt_ext_uniform_kernel<1>, grid, block, 0, stream, from, to, nvec, nbytes); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     uint64_t blocks = (total + THREADS - 1) / THREADS;
     if (blocks > (1u << 16))
         blocks = 1u << 16;   // grid-stride beyond 16 M threads (64 waves per CU)
-    uint8_t *n8 = static_cast<uint8_t *>(native), *e8 = static_cast<uint8_t *>(ext);
-    if (dir == 0)
-        hipLaunchKernelGGL((ddt_ext_kernel<0>), dim3(uint32_t(blocks)), dim3(THREADS), 0, stream,
-                           segs, nseg, runs, E, total, Sn, Se, n8, e8);
-    else
-        hipLaunchKernelGGL((ddt_ext_kernel<1>), dim3(uint32_t(blocks)), dim3(THREADS), 0, stream,
-                           segs, nseg, runs, E, total, Sn, Se, n8, e8);
+    const size_t tb = size_t(nseg) * sizeof(ConvSeg) + size_t(nruns) * sizeof(ConvRun);
+    const bool tab = tb <= kExtTabLds;
+    const size_t lds = tab ? tb : 0;
+    const dim3 grid{uint32_t(blocks)}, block{THREADS};
+    if (dir == 0) {
+        if (tab) hipLaunchKernelGGL((ddt_ext_kernel<0, true>), grid, block, lds, stream, segs, nseg, runs, nruns, E, total, Sn, Se, n8, e8);
+        else hipLaunchKernelGGL((ddt_ext_kernel<0, false>), grid, block, 0, stream, segs, nseg, runs, nruns, E, total, Sn, Se, n8, e8);
+    } else {
+        if (tab) hipLaunchKernelGGL((ddt_ext_kernel<1, true>), grid, block, lds, stream, segs, nseg, runs, nruns, E, total, Sn, Se, n8, e8);
+        else hipLaunchKernelGGL((ddt_ext_kernel<1, false>), grid, block, 0, stream, segs, nseg, runs, nruns, E, total, Sn, Se, n8, e8);
+    }
     return hipGetLastError();
 }
 

@@ -61,9 +61,13 @@ hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, in
                        uint64_t ubase, uint64_t pbase, hipStream_t stream, uint32_t grid_cap = 0);
 
 // external32 conversion between a native packed stream and its big-endian form.
-hipError_t launch_ext(const ConvSeg *segs, uint32_t nseg, const ConvRun *runs, uint64_t E,
+// uniform = C in {1,2,4,8,16}: every element is a C-byte word swap (C = 1: a copy) with identical native
+// and external layouts -- one vectorised word-swap pass instead of the per-element walk.
+// Tables of at most kExtTabLds bytes are staged in LDS by the per-element kernel.
+constexpr size_t kExtTabLds = 32 << 10;
+hipError_t launch_ext(const ConvSeg *segs, uint32_t nseg, const ConvRun *runs, uint32_t nruns, uint64_t E,
                       uint64_t count, uint64_t Sn, uint64_t Se, void *native, void *ext, int dir,
-                      hipStream_t stream);
+                      uint32_t uniform, hipStream_t stream);
 
 // ddt_external.cpp: the external32 signature of a committed type (built once, cached).
 struct ExtPlan {
@@ -71,6 +75,7 @@ struct ExtPlan {
     std::vector<ConvRun> runs;
     uint64_t E = 0;      // elements per instance
     uint64_t Se = 0;     // external bytes per instance
+    uint32_t uniform = 0;   // C when the whole signature is C-byte word swaps (see launch_ext)
     ConvSeg *d_segs = nullptr;
     ConvRun *d_runs = nullptr;
     int error = 0;       // DDT_ERR_* when the type has no external32 form

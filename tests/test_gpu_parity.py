@@ -461,6 +461,43 @@ def test_external32_matches_oracle(device, host_ext):
     assert tested > 30
 
 
+@pytest.mark.parametrize("offset", [0, 8, 3])
+def test_external32_uniform_word_swaps(device, offset):
+    """Signatures that are one word size throughout (MPI_DOUBLE, MPI_FLOAT, MPI_SHORT, the
+    complex types, INT16/FLOAT16, bytes) take the vectorised word-swap kernel: bit-exact with
+    the oracle with the external stream 16-byte aligned, 8-byte aligned and byte-misaligned,
+    and stream lengths that leave a tail below 16 bytes."""
+    import torch
+    import ompi_amd
+    rng = random.Random(8300 + offset)
+    for tid, size in [(4, 1), (5, 2), (6, 4), (15, 4), (16, 8), (7, 8), (21, 16), (19, 4), (20, 8),
+                      (8, 16), (18, 16), (14, 2)]:
+        for recipe, count in [(("basic", tid), 1), (("contig", 7, ("basic", tid)), 3),
+                              (("vector", 5, 3, 4, ("basic", tid)), 2),
+                              (("contig", 4099, ("basic", tid)), rng.choice([1, 5]))]:
+            b = R.Built(recipe)
+            info = b.o.info()
+            span, origin = R.layout(info, count)
+            host = R.fill(span, tid + count)
+            user = _dev(host, device)
+            e = b.engine()
+            ref = b.o.pack_external(count, host, origin)
+            es = len(ref)
+            out = torch.zeros(es + 32, dtype=torch.uint8, device=device)
+            assert ompi_amd.pack_external(user.data_ptr() + origin, count, e, out.data_ptr() + offset, es, 0) == es
+            got = _host(out)
+            np.testing.assert_array_equal(got[offset:offset + es], np.frombuffer(ref, dtype=np.uint8),
+                                          err_msg=str(recipe))
+            assert not got[:offset].any() and not got[offset + es:].any(), recipe
+            if _overlapping(b.o, count):
+                continue
+            dst = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
+            exp = np.full(span, 0xA5, dtype=np.uint8)
+            b.o.unpack_external(count, exp, origin, ref)
+            assert ompi_amd.unpack_external(out.data_ptr() + offset, es, 0, dst.data_ptr() + origin, count, e) == es
+            np.testing.assert_array_equal(_host(dst), exp, err_msg=str(recipe))
+
+
 def test_external32_errors(device):
     import torch
     import ompi_amd
