@@ -936,12 +936,29 @@ namespace {
 // call of the thread finds it free).  Round 1 allocated per call, round 2 first with
 // stream-ordered allocations, whose pool returns the memory at every synchronisation: a
 // 16 MiB MPI_Pack_external spent ~300 us of its 357 in allocation (profiles/r2_ext_bench.jsonl).
+// Only buffers up to kKeepBytes are kept for reuse: a larger request (a multi-GiB message,
+// where one hipMalloc is small against the transfer) gets its own allocation, freed when the
+// call ends (hipFree waits for the device), so a thread does not pin that much HBM for good.
+constexpr size_t kKeepBytes = size_t(256) << 20;
 struct DevBuf {
     void *p = nullptr;
+    void *own = nullptr;
     int slot = 0;
     explicit DevBuf(int s) : slot(s) {}
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf()
+    {
+        if (own)
+            (void) hipFree(own);
+    }
     hipError_t alloc(size_t n)
     {
+        if (n > kKeepBytes) {
+            const hipError_t e = hipMalloc(&own, n);
+            p = own;
+            return e;
+        }
         struct Cache {
             std::map<std::pair<int, int>, std::pair<void *, size_t>> bufs;   // (device, slot)
             ~Cache()

@@ -498,6 +498,35 @@ def test_external32_uniform_word_swaps(device, offset):
             np.testing.assert_array_equal(_host(dst), exp, err_msg=str(recipe))
 
 
+def test_external32_large_message_scratch(device):
+    """A message above the per-thread scratch that is kept for reuse (256 MiB) takes its own
+    HBM scratch for the call: vector(36 Mi, 1, 2) of doubles (288 MiB packed) to external32
+    and back, twice, then a small call on the kept scratch -- big-endian words of the even
+    elements, odd elements of the receive buffer untouched."""
+    import torch
+    import ompi_amd
+    from ompi_amd import datatype as D
+    n = 36 << 20
+    t = D.create_vector(n, 1, 2, D.predefined(D.FLOAT8)).commit()
+    user = torch.randint(-2**62, 2**62, (2 * n,), dtype=torch.int64, device=device)
+    want = user[0::2].contiguous().view(torch.uint8).view(-1, 8).flip(1).reshape(-1)
+    out = torch.empty(8 * n, dtype=torch.uint8, device=device)
+    for _ in range(2):
+        out.fill_(0)
+        assert ompi_amd.pack_external(user.data_ptr(), 1, t, out.data_ptr(), 8 * n, 0) == 8 * n
+        assert torch.equal(out, want)
+        dst = torch.full((2 * n,), 0x5A5A5A5A5A5A5A5A, dtype=torch.int64, device=device)
+        assert ompi_amd.unpack_external(out.data_ptr(), 8 * n, 0, dst.data_ptr(), 1, t) == 8 * n
+        assert torch.equal(dst[0::2], user[0::2])
+        assert bool((dst[1::2] == 0x5A5A5A5A5A5A5A5A).all())
+        del dst
+    del want
+    small = D.create_vector(1000, 1, 2, D.predefined(D.FLOAT8)).commit()
+    o2 = torch.zeros(8000, dtype=torch.uint8, device=device)
+    assert ompi_amd.pack_external(user.data_ptr(), 1, small, o2.data_ptr(), 8000, 0) == 8000
+    assert torch.equal(o2, user[0:2000:2].contiguous().view(torch.uint8).view(-1, 8).flip(1).reshape(-1))
+
+
 def test_external32_errors(device):
     import torch
     import ompi_amd
