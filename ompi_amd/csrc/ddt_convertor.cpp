@@ -96,42 +96,100 @@ bool capturing(hipStream_t s)
     return cs != hipStreamCaptureStatusNone;
 }
 
-// Free retired descriptor sets whose eviction events every launching stream has passed.
-// With `block` (never inside a capture), wait for the oldest until at most kRetiredMax
-// remain: a host wait on those streams' events, not a device-wide synchronisation.
+bool events_passed(const std::vector<hipEvent_t> &evs)
+{
+    for (hipEvent_t e : evs) {
+        if (hipEventQuery(e) != hipSuccess) {
+            (void) hipGetLastError();   // hipErrorNotReady must not look like a launch error
+            return false;
+        }
+    }
+    return true;
+}
+
+// A retired set whose readers have all passed: its events go, its device memory goes back
+// to the plan's spare list for the next set that needs as much (no hipFree: that API
+// synchronises the whole device, and a free inside a stream capture would break it).
+void recycle(Plan &P, Retired &r)   // P.mu held
+{
+    for (hipEvent_t e : r.events)
+        (void) hipEventDestroy(e);
+    r.events.clear();
+    ItemSet &S = *r.set;
+    for (hipEvent_t e : S.late)
+        (void) hipEventDestroy(e);
+    S.late.clear();
+    if (S.d_items) {
+        P.spare.push_back({S.d_items, S.items.size() * sizeof(Item)});
+        S.d_items = nullptr;
+    }
+}
+
+// Recycle retired descriptor sets whose eviction events (and the late events of launches
+// enqueued after the eviction) every launching stream has passed.  With `block` (never
+// inside a capture), wait for the oldest until at most kRetiredMax remain: a host wait on
+// those streams' events, not a device-wide synchronisation.  A set with a launch still
+// being enqueued by another thread (inflight) is never touched.
 void reap(Plan &P, bool block)   // P.mu held
 {
     for (size_t i = 0; i < P.graveyard.size();) {
-        bool done = true;
-        for (hipEvent_t e : P.graveyard[i].events) {
-            if (hipEventQuery(e) != hipSuccess) {
-                (void) hipGetLastError();   // hipErrorNotReady must not look like a launch error
-                done = false;
-                break;
-            }
-        }
-        if (!done) {
+        Retired &r = P.graveyard[i];
+        if (r.set->inflight || !events_passed(r.events) || !events_passed(r.set->late)) {
             ++i;
             continue;
         }
-        for (hipEvent_t e : P.graveyard[i].events)
-            (void) hipEventDestroy(e);
+        recycle(P, r);
         P.graveyard.erase(P.graveyard.begin() + long(i));
     }
-    while (block && P.graveyard.size() > kRetiredMax) {
-        for (hipEvent_t e : P.graveyard.front().events) {
+    while (block && P.graveyard.size() > kRetiredMax && !P.graveyard.front().set->inflight) {
+        Retired &r = P.graveyard.front();
+        for (hipEvent_t e : r.events)
             (void) hipEventSynchronize(e);
-            (void) hipEventDestroy(e);
-        }
+        for (hipEvent_t e : r.set->late)
+            (void) hipEventSynchronize(e);
+        recycle(P, r);
         P.graveyard.erase(P.graveyard.begin());
     }
 }
 
+// Device memory for `bytes` of descriptors: the smallest spare block that fits, else new.
+Item *take_items_memory(Plan &P, size_t bytes)   // P.mu held
+{
+    size_t best = P.spare.size();
+    for (size_t i = 0; i < P.spare.size(); ++i)
+        if (P.spare[i].bytes >= bytes && (best == P.spare.size() || P.spare[i].bytes < P.spare[best].bytes))
+            best = i;
+    if (best < P.spare.size()) {
+        Item *d = static_cast<Item *>(P.spare[best].p);
+        P.spare.erase(P.spare.begin() + long(best));
+        return d;
+    }
+    Item *d = nullptr;
+    return hipMalloc((void **) &d, bytes) == hipSuccess ? d : nullptr;
+}
+
+// A retired set (still in the graveyard) that a captured graph now holds: pinned for the
+// plan's lifetime instead of recycled.
+void pin_retired(Plan &P, const std::shared_ptr<ItemSet> &S)   // P.mu held
+{
+    S->pinned = true;
+    for (size_t i = 0; i < P.graveyard.size(); ++i) {
+        if (P.graveyard[i].set == S) {
+            for (hipEvent_t e : P.graveyard[i].events)
+                (void) hipEventDestroy(e);
+            P.graveyard.erase(P.graveyard.begin() + long(i));
+            P.pinned.push_back(S);
+            return;
+        }
+    }
+}
+
 // An evicted set's device descriptors may still be read by launches in flight: record an
-// event behind them on every stream that launched the set, free it once they pass.  A set
-// a captured graph holds (or whose stream cannot take an event) lives as long as the plan.
+// event behind them on every stream that launched the set, recycle it once they pass.  A
+// set a captured graph holds (or whose stream cannot take an event) lives as long as the plan.
 void retire(Plan &P, const std::shared_ptr<ItemSet> &S)   // P.mu held
 {
+    S->retired = true;
     if (!S->d_items)
         return;
     if (S->pinned) {
@@ -148,6 +206,7 @@ void retire(Plan &P, const std::shared_ptr<ItemSet> &S)   // P.mu held
                 (void) hipEventDestroy(e);
             for (hipEvent_t x : r.events)
                 (void) hipEventDestroy(x);
+            S->pinned = true;
             P.pinned.push_back(S);
             return;
         }
@@ -229,6 +288,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         for (size_t i = 0; i < P.cache.size(); ++i) {
             if (P.cache[i]->key == key) {
                 S = P.cache[i];
+                ++S->inflight;   // held until this call has enqueued its launch (Hold below)
                 if (i)
                     std::rotate(P.cache.begin(), P.cache.begin() + long(i), P.cache.begin() + long(i) + 1);
                 break;
@@ -258,14 +318,19 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                 S->blk.items[i] = S->items[i];
         } else if (!S->items.empty()) {
             size_t bytes = S->items.size() * sizeof(Item);
-            hipError_t e = hipMalloc((void **) &S->d_items, bytes);
-            if (e == hipSuccess)
-                e = upload(S->d_items, S->items.data(), bytes);
+            {
+                std::lock_guard<std::mutex> g(P.mu);
+                S->d_items = take_items_memory(P, bytes);
+            }
+            if (!S->d_items)
+                return fail(DDT_ERR_OUT_OF_RESOURCE, "descriptor memory");
+            const hipError_t e = upload(S->d_items, S->items.data(), bytes);
             if (e != hipSuccess)
                 return fail(DDT_ERR_HIP, std::string("item upload: ") + hipGetErrorString(e));
         }
         const bool block = !capturing(stream);
         std::lock_guard<std::mutex> g(P.mu);
+        ++S->inflight;
         P.cache.insert(P.cache.begin(), S);
         if (P.cache.size() > kCacheEntries) {
             retire(P, P.cache.back());
@@ -273,6 +338,34 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         }
         reap(P, block);
     }
+    // The launch is enqueued outside the plan lock, so another thread may evict the set
+    // meanwhile.  This call holds it (`inflight`, taken with the lookup) so its memory is not
+    // recycled, and if it was retired, a launch by pointer leaves a late event behind it for
+    // the retirement to wait on.  A retired set that fits in the kernel arguments is launched
+    // from them instead.
+    struct Hold {
+        Plan &P;
+        std::shared_ptr<ItemSet> S;
+        hipStream_t stream;
+        bool by_pointer = false;
+        ~Hold()
+        {
+            std::lock_guard<std::mutex> g(P.mu);
+            --S->inflight;
+            if (by_pointer && S->retired && !S->pinned) {
+                hipEvent_t e = nullptr;
+                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess
+                    && hipEventRecord(e, stream) == hipSuccess) {
+                    S->late.push_back(e);
+                } else {
+                    (void) hipGetLastError();
+                    if (e)
+                        (void) hipEventDestroy(e);
+                    pin_retired(P, S);
+                }
+            }
+        }
+    } hold{P, S, stream};
     if (S->items.empty())
         return DDT_SUCCESS;
     // A descriptor set travels in the kernel-argument segment on its first launch (no upload
@@ -283,22 +376,27 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     Item *d_items = nullptr;
     {
         std::lock_guard<std::mutex> g(P.mu);
-        if (S->inline_ok && ++S->uses >= 2 && !S->d_items && tuning().ptr) {
+        if (S->inline_ok && !S->retired && ++S->uses >= 2 && !S->d_items && tuning().ptr) {
             size_t bytes = S->items.size() * sizeof(Item);
-            Item *d = nullptr;
-            if (hipMalloc((void **) &d, bytes) == hipSuccess) {
+            Item *d = take_items_memory(P, bytes);
+            if (d) {
                 if (upload(d, S->items.data(), bytes) == hipSuccess)
                     S->d_items = d;
                 else
-                    (void) hipFree(d);
+                    P.spare.push_back({d, bytes});
             }
         }
-        d_items = (S->inline_ok && !tuning().ptr) ? nullptr : S->d_items;
+        d_items = (S->inline_ok && (!tuning().ptr || S->retired)) ? nullptr : S->d_items;
         if (d_items) {
-            if (capturing(stream))
-                S->pinned = true;   // the graph keeps this pointer: never free before the plan
+            if (capturing(stream)) {
+                // the graph keeps this pointer: never recycle it before the plan goes
+                if (S->retired && !S->pinned)
+                    pin_retired(P, S);
+                S->pinned = true;
+            }
             if (std::find(S->streams.begin(), S->streams.end(), stream) == S->streams.end())
                 S->streams.push_back(stream);
+            hold.by_pointer = true;
         }
     }
     if (!d_items)

@@ -117,8 +117,21 @@ struct ItemSet {
     bool pinned = false;          // launched by pointer inside a stream capture: a graph holds
                                   // d_items, so it lives as long as the plan
     std::vector<hipStream_t> streams;  // streams that launched d_items (retirement events)
+    // A launch by pointer is enqueued outside the plan lock: `inflight` counts launches
+    // between taking d_items and enqueuing them, and a launch that finds the set evicted
+    // meanwhile records a `late` event behind itself for the retirement to wait on too.
+    uint32_t inflight = 0;
+    bool retired = false;
+    std::vector<hipEvent_t> late;
     ItemBlock blk{};
     ~ItemSet();
+};
+
+// Device memory of retired descriptor sets, kept for reuse (hipFree implies a device-wide
+// synchronisation; buffers are released only with the plan).
+struct DevBlock {
+    void *p = nullptr;
+    size_t bytes = 0;
 };
 
 // An evicted descriptor set waits here until every stream that launched it has passed the
@@ -140,6 +153,7 @@ struct Plan {
     std::vector<std::shared_ptr<ItemSet>> cache;      // most recent first
     std::vector<Retired> graveyard;                   // evicted, freed once their events pass
     std::vector<std::shared_ptr<ItemSet>> pinned;     // evicted but held by captured graphs
+    std::vector<DevBlock> spare;                      // reusable descriptor memory (recycled)
     // address-ordered plan of a one-leaf single-element index list (ddt_sorted.hip):
     // 0 = not tried yet, 1 = built, -1 = not applicable
     int sorted_state = 0;

@@ -77,6 +77,9 @@ Plan::~Plan()
             (void) hipEventDestroy(e);
     graveyard.clear();
     pinned.clear();
+    for (DevBlock &b : spare)
+        (void) hipFree(b.p);
+    spare.clear();
     for (DevList &d : dev) {
         if (d.disp) (void) hipFree(d.disp);
         if (d.len) (void) hipFree(d.len);
@@ -86,6 +89,10 @@ Plan::~Plan()
 
 ItemSet::~ItemSet()
 {
+    for (hipEvent_t e : late)
+        (void) hipEventDestroy(e);
+    // a retired set's memory went back to its plan's spare list (reap); a live set is freed
+    // only with its plan, after the plan's device synchronisation
     if (d_items)
         (void) hipFree(d_items);
 }

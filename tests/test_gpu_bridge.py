@@ -616,6 +616,70 @@ def test_descriptor_sets_follow_shape_not_buffers_and_survive_capture(device):
         np.testing.assert_array_equal(_host(pks[k])[:100 * W], refs[k][:100 * W])
 
 
+@pytest.mark.parametrize("rec", [
+    ("vector", 4096, 3, 7, ("basic", FLOAT4)),
+    # nine interleaved leaves: every window's descriptor set is beyond the kernel-argument
+    # block and lives in HBM from its first launch
+    ("struct", [1] * 9, [4 * i for i in range(9)], [("vector", 2048, 1, 9, ("basic", FLOAT4))] * 9),
+])
+def test_descriptor_sets_shared_by_threads(device, rec):
+    """One committed datatype driven by four host threads at once, each on its own stream:
+    48 distinct windows (shared shapes across threads, so the threads hit each other's
+    descriptor sets), swept three times so sets are launched by pointer, and more shapes than
+    the 32-entry cache, so sets are evicted and recycled while other threads are enqueuing
+    launches of them.  Every window of every sweep is bit-exact with the oracle."""
+    import threading
+    import torch
+    import ompi_amd
+    b = R.Built(rec)
+    e = b.engine()
+    info = b.o.info()
+    size = info["size"]
+    span, origin = R.layout(info, 1)
+    host = R.fill(span, 77)
+    user = _dev(host, device)
+    ref = np.frombuffer(b.o.pack(1, host, origin, 0, size, element_granular=False), dtype=np.uint8)
+    NW, SWEEPS, NT = 48, 3, 4
+    W = size // NW // 4 * 4
+    streams = [torch.cuda.Stream(device) for _ in range(NT)]
+    outs = [torch.zeros(SWEEPS * size, dtype=torch.uint8, device=device) for _ in range(NT)]
+    errors = []
+    lib = ompi_amd.lib()
+
+    def worker(t):
+        try:
+            rng = random.Random(500 + t)
+            for sweep in range(SWEEPS):
+                order = list(range(NW))
+                rng.shuffle(order)
+                base = outs[t].data_ptr() + sweep * size
+                for w in order:
+                    rc = lib.ddt_pack_window(e.handle, 1, user.data_ptr() + origin, w * W, base + w * W, W, None,
+                                             streams[t].cuda_stream)
+                    if rc < 0:
+                        errors.append((t, sweep, w, rc))
+                        return
+            streams[t].synchronize()
+        except Exception as ex:   # pragma: no cover - reported below
+            errors.append((t, repr(ex)))
+
+    torch.cuda.synchronize()
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(NT)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors
+    torch.cuda.synchronize()
+    for t in range(NT):
+        got = _host(outs[t])
+        for sweep in range(SWEEPS):
+            np.testing.assert_array_equal(got[sweep * size: sweep * size + NW * W], ref[:NW * W],
+                                          err_msg=f"thread {t} sweep {sweep}")
+    ci = e.cache_info()
+    assert ci["cached"] <= 32, ci
+
+
 def test_bridge_from_c(device):
     """bridge/bridge_demo.c: the same drop-in driven from C on opal_datatype_t /
     opal_convertor_t structs compiled against include/opal_layout.h -- prepare as
