@@ -1151,47 +1151,86 @@ struct RawData {
     int64_t extent, disp;
 };
 
-void flush_data(std::vector<RawData> &run, std::vector<Node> &out)
-{
-    if (run.size() >= kFoldMin) {
-        auto L = std::make_shared<IndexList>();
-        L->esize = kSize[run[0].type];
-        size_t nb = 0;
-        for (const RawData &r : run)
-            nb += r.count;
-        L->disp.reserve(nb);
-        L->len.reserve(nb);
-        for (const RawData &r : run)
-            for (uint32_t k = 0; k < r.count; ++k) {
-                L->disp.push_back(r.disp + int64_t(k) * r.extent);
-                L->len.push_back(r.blen);
+// A run of foldable DATA entries of one type, streamed: the first kFoldMin entries wait in
+// `head`; from then on blocks go straight into the index list, whose per-block lengths are
+// materialised only once two of them differ (cfg4's 33.5 M entries import without a second
+// copy of the description or a length array).
+struct Fold {
+    uint16_t type = 0;
+    std::vector<RawData> head;
+    std::shared_ptr<IndexList> L;
+    bool uni = true;
+    uint64_t ulen = 0;
+
+    bool empty() const { return head.empty() && !L; }
+    void add_blocks(const RawData &r)
+    {
+        for (uint32_t k = 0; k < r.count; ++k) {
+            L->disp.push_back(r.disp + int64_t(k) * r.extent);
+            if (uni && r.blen != ulen) {
+                uni = false;
+                L->len.assign(L->disp.size() - 1, ulen);
             }
-        Node n;
-        n.kind = Node::LIST;
-        n.esize = L->esize;
-        n.tid = run[0].type;
-        n.list = finish_list(L);
-        out.push_back(std::move(n));
-    } else {
-        for (const RawData &r : run) {
-            Node n;
-            n.kind = Node::DATA;
-            n.esize = kSize[r.type];
-            n.tid = r.type;
-            n.count = r.count;
-            n.blen = r.blen;
-            n.extent = r.extent;
-            n.disp = r.disp;
-            out.push_back(n);
+            if (!uni)
+                L->len.push_back(r.blen);
         }
     }
-    run.clear();
-}
+    void push(const RawData &r)
+    {
+        if (empty())
+            type = r.type;
+        if (L) {
+            add_blocks(r);
+            return;
+        }
+        head.push_back(r);
+        if (head.size() < kFoldMin)
+            return;
+        L = std::make_shared<IndexList>();
+        L->esize = kSize[type];
+        uni = true;
+        ulen = head[0].blen;
+        for (const RawData &h : head)
+            add_blocks(h);
+        head.clear();
+    }
+    void flush(std::vector<Node> &out)
+    {
+        if (L) {
+            if (uni) {
+                L->ulen = ulen;
+                L->len.clear();
+            }
+            Node n;
+            n.kind = Node::LIST;
+            n.esize = L->esize;
+            n.tid = type;
+            n.list = finish_list(L);
+            out.push_back(std::move(n));
+            L.reset();
+        }
+        for (const RawData &r : head)
+            out.push_back(data_node(r));
+        head.clear();
+    }
+    static Node data_node(const RawData &r)
+    {
+        Node n;
+        n.kind = Node::DATA;
+        n.esize = kSize[r.type];
+        n.tid = r.type;
+        n.count = r.count;
+        n.blen = r.blen;
+        n.extent = r.extent;
+        n.disp = r.disp;
+        return n;
+    }
+};
 
 bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<Node> &out)
 {
     size_t i = begin;
-    std::vector<RawData> run;
+    Fold run;
     while (i < end) {
         const unsigned char *p = raw + 32 * i;
         uint16_t flags, type;
@@ -1209,14 +1248,15 @@ bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<
                 return false;
             const RawData d{type, count, blocklen * uint64_t(kSize[type]), extent, disp};
             const bool foldable = count >= 1 && count <= kFoldCount && d.blen > 0;
-            if (!run.empty() && (!foldable || run[0].type != type))
-                flush_data(run, out);
-            run.push_back(d);
-            if (!foldable)
-                flush_data(run, out);
+            if (!run.empty() && (!foldable || run.type != type))
+                run.flush(out);
+            if (foldable)
+                run.push(d);
+            else
+                out.push_back(Fold::data_node(d));
             ++i;
         } else if (type == 0) {   // LOOP
-            flush_data(run, out);
+            run.flush(out);
             uint32_t items, loops;
             int64_t extent;
             std::memcpy(&items, p + 4, 4);
@@ -1256,7 +1296,7 @@ bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<
             return false;   // stray END_LOOP
         }
     }
-    flush_data(run, out);   // a run that ends the description
+    run.flush(out);   // a run that ends the description
     return true;
 }
 }  // namespace
