@@ -223,9 +223,12 @@ def cpu_baseline(name, srec, scount, what, host_user, origin, gpu_prefix, budget
 
 # ------------------------------------------------------------------ latency
 def single_face_latency(dev, stream, user, origin, reps=200):
-    """one 512 KiB face of one field is launch-bound.  Reports the
-    kernel time (HIP events) and the synchronous MPI_Pack call time (host wall clock, plan
-    cached) of packing ONE x face and ONE z face of field 0."""
+    """one 512 KiB face of one field is launch-bound.  Reports, for
+    packing ONE x face and ONE z face of field 0: `call_to_done_us`, HIP events around the
+    call on an idle stream (host enqueue + launch + kernel); `device_us`, the same events with
+    the stream held by a sleep kernel while the host enqueues (launch + kernel + one event
+    record, scripts/face_scaling.py); and the synchronous MPI_Pack call time (host wall clock,
+    plan cached)."""
     import torch
     import ompi_amd
     from ompi_amd import recipe as ER
@@ -250,12 +253,22 @@ def single_face_latency(dev, stream, user, origin, reps=200):
             evs.append((a, b))
             torch.cuda.synchronize()
         k_us = float(np.median([a.elapsed_time(b) for a, b in evs])) * 1e3
+        held = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(min(reps, 50))]
+        torch.cuda._sleep(int(5e7))   # hold the stream while the host enqueues
+        for a, b in held:
+            a.record(stream)
+            c.prepare_for_send(ft, 1, user.data_ptr() + origin)
+            c.pack([(buf, fs)])
+            b.record(stream)
+        torch.cuda.synchronize()
+        d_us = float(np.median([a.elapsed_time(b) for a, b in held])) * 1e3
         walls = []
         for _ in range(reps):
             t0 = time.perf_counter()
             ompi_amd.pack(user.data_ptr() + origin, 1, ft, buf, fs, 0)   # synchronous MPI_Pack
             walls.append(time.perf_counter() - t0)
-        out[name] = {"bytes": fs, "kernel_us": round(k_us, 2),
+        out[name] = {"bytes": fs, "call_to_done_us": round(k_us, 2), "device_us": round(d_us, 2),
                      "mpi_pack_call_us": round(float(np.median(walls)) * 1e6, 2)}
     return out
 
