@@ -57,7 +57,12 @@ MemKind classify(const void *p)
 }
 
 // Pinned (page-locked, device-mapped) host memory: the device address of [p, p + n), or 0
-// for pageable memory, device memory or a range whose two ends do not map contiguously.
+// for pageable memory, device memory or a range not inside one pinned allocation.  On ROCm a
+// pinned page's device address equals its host address, so matching ends alone would also
+// accept a range running from one pinned allocation through pageable pages into another:
+// the allocation's bounds decide when the runtime reports them (hipHostMalloc memory); for
+// hipHostRegister'ed memory it reports the size but no base (scripts/probe_hostrange.cpp),
+// and the two ends must map contiguously.
 uint64_t pinned_device_range(const void *p, uint64_t n)
 {
     auto dev_of = [](const void *q) -> uint64_t {
@@ -73,6 +78,14 @@ uint64_t pinned_device_range(const void *p, uint64_t n)
     const uint64_t d0 = dev_of(p);
     if (!d0 || n == 0)
         return d0;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(uintptr_t(d0))) == hipSuccess
+        && base) {
+        const uint64_t b = uint64_t(uintptr_t(base));
+        return d0 >= b && n <= size && d0 - b <= size - n ? d0 : 0;
+    }
+    (void) hipGetLastError();
     const uint64_t d1 = dev_of(static_cast<const char *>(p) + (n - 1));
     return d1 == d0 + (n - 1) ? d0 : 0;
 }
