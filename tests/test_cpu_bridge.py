@@ -152,6 +152,69 @@ def test_exported_descriptions_round_trip():
     assert loops > 50
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_streamed_import_of_folded_runs(seed):
+    """ddt_type_from_opal_desc streams runs of small DATA entries into one index list: runs
+    around the 64-entry fold threshold, block lengths that start to differ after the list has
+    begun (the lengths array is materialised mid-run), a type change that starts a new list,
+    short runs kept as DATA entries and non-foldable entries between them.  The imported type
+    map must be the description's blocks in order."""
+    import random
+    import numpy as np
+    from ompi_amd import datatype as D
+    from tests import plan_emu as E
+    rng = random.Random(900 + seed)
+    sizes = {FLOAT4: 4, FLOAT8: 8, INT4: 4}
+    ents, blocks, pos = [], [], 0
+    for _ in range(rng.randint(3, 6)):
+        tid = rng.choice([FLOAT4, FLOAT8, INT4])
+        esz = sizes[tid]
+        n = rng.choice([1, 20, 63, 64, 65, 130, 300])
+        change_at = rng.choice([None, 0, 1, n // 2, n - 1])
+        for i in range(n):
+            count = rng.randint(1, 16) if rng.random() < 0.97 else rng.randint(17, 40)   # > 16: not foldable
+            blen = 1 if change_at is None or i < change_at else rng.randint(1, 3)
+            extent = esz * rng.randint(blen + 1, blen + 5)
+            disp = pos
+            ents.append(S.data(tid, count, blen, extent, disp))
+            for k in range(count):
+                blocks.append((disp + k * extent, blen * esz))
+            pos = disp + count * extent + esz * rng.randint(0, 3)
+    size = sum(b[1] for b in blocks)
+    desc = b"".join(ents)
+    t = D.from_opal_desc(desc, size, 0, pos, 0, pos)
+    want, p = [], 0
+    for d, ln in blocks:
+        want.append((d, p, ln))
+        p += ln
+    np.testing.assert_array_equal(E.engine_blocks(t), E.merge_runs(np.array(want, dtype=np.int64)))
+
+
+def test_streamed_import_materialises_lengths_mid_run():
+    """130 one-type entries whose block length changes at entry 100 (after the list began at
+    entry 64): one list leaf with per-block lengths, blocks in description order."""
+    import numpy as np
+    from ompi_amd import datatype as D
+    from tests import plan_emu as E
+    ents, blocks, pos = [], [], 0
+    for i in range(130):
+        blen = 1 if i < 100 else 2
+        ents.append(S.data(FLOAT4, 2, blen, 16, pos))
+        blocks += [(pos, 4 * blen), (pos + 16, 4 * blen)]
+        pos += 40
+    size = sum(b[1] for b in blocks)
+    t = D.from_opal_desc(b"".join(ents), size, 0, pos, 0, pos)
+    lv = E.leaves(t)
+    assert len(lv) == 1 and lv[0]["kind"] != 0
+    _, ln = E.plan_list(t, lv[0]["index"])
+    assert list(ln) == [4] * 200 + [8] * 60
+    want, p = [], 0
+    for d, n in blocks:
+        want.append((d, p, n))
+        p += n
+    np.testing.assert_array_equal(E.engine_blocks(t), E.merge_runs(np.array(want, dtype=np.int64)))
+
+
 def test_import_cache_under_concurrent_threads():
     """One thread per convertor is the reference's contract, but many threads share the
     datatypes: eight threads attach convertors to the same six descriptions at once (ctypes
