@@ -532,15 +532,17 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 2), "peak": 8000.0,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": None},
         }
+        # the committed PMC passes were measured on the config's default (weak) message; a
+        # --strong message of another size does not inherit them
         tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-        if os.path.exists(tfile):
+        if os.path.exists(tfile) and not split:
             with open(tfile) as f:
                 result["roofline"]["traffic"] = json.load(f).get("bytes_per_step")
         # Memory-side request roofline: the sparse faces are bound by requests,
         # not bytes.  Request counts per step come from the committed rocprofv3 PMC pass
         # (scripts/requests.py); the rate uses this run's own kernel time.
         rfile = os.path.join(ROOT, "profiles", f"requests_{args.config}.json")
-        if os.path.exists(rfile):
+        if os.path.exists(rfile) and not split:
             with open(rfile) as f:
                 rq = json.load(f)
             ops = rq["ops_per_step"]
