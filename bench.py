@@ -322,8 +322,10 @@ def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z")):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    # ~35 ms timed at the default config: long enough that one rank's launch jitter does not
+    # set the max-over-ranks time of a multi-GPU run
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-faces", action="store_true", help="skip the per-face measurement")
