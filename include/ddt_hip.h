@@ -286,13 +286,17 @@ int ddt_type_cache_info(const ddt_datatype_t *type, int64_t *out4);
  * ddt_debug_items: the launch descriptors (ddt_device.h Item, raw bytes) that pack/unpack would
  *   run for the packed window [w0, w1) of `count` instances at `user` with the packed pointer
  *   `pk` holding byte w0; *nitems receives the count, *item_size the size of one Item.
- * ddt_type_plan_list: host copy of index-list leaf `leaf`: block displacements and lengths. */
+ * ddt_type_plan_list: host copy of index-list leaf `leaf`: block displacements and lengths.
+ * ddt_debug_host_window: 1 (and the device address) when a host iovec [p, p + n) would be moved
+ *   by the kernel itself over PCIe (inside one pinned allocation or registration), else 0: the
+ *   iovec goes through HBM staging. */
 int64_t ddt_type_plan_leaves(const ddt_datatype_t *type, int64_t *out, size_t cap);
 int ddt_debug_items(const ddt_datatype_t *type, size_t count, uint64_t user, uint64_t pk,
                     uint64_t w0, uint64_t w1, int same_layout, void *out, size_t cap_bytes,
                     size_t *nitems, size_t *item_size);
 int64_t ddt_type_plan_list(const ddt_datatype_t *type, size_t leaf, int64_t *disp, uint64_t *len,
                            size_t cap);
+int ddt_debug_host_window(const void *p, size_t n, uint64_t *device_addr);
 /* Tuning knobs for A/B measurements (affect descriptor sets built afterwards):
  * "nt" = user-side non-temporal gathers (-1 auto, 0 off, 1 on); "task_kb" = packed KiB per
  * workgroup (0 adaptive); "policy" = task sizing (0 v0, 1 per-leaf passes); "interleave" =

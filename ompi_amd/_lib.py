@@ -96,6 +96,7 @@ SIGNATURES = {
     "ddt_debug_items": (c_int, [c_void_p, c_size_t, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                 ctypes.c_uint64, c_int, c_void_p, c_size_t, P(c_size_t), P(c_size_t)]),
     "ddt_type_plan_list": (c_int64, [c_void_p, c_size_t, c_void_p, c_void_p, c_size_t]),
+    "ddt_debug_host_window": (c_int, [c_void_p, c_size_t, P(ctypes.c_uint64)]),
     "ddt_tune": (c_int, [ctypes.c_char_p, ctypes.c_long]),
     "ddt_selftest": (c_int, []),
     "ddt_version": (ctypes.c_char_p, []),

@@ -57,37 +57,34 @@ MemKind classify(const void *p)
 }
 
 // Pinned (page-locked, device-mapped) host memory: the device address of [p, p + n), or 0
-// for pageable memory, device memory or a range not inside one pinned allocation.  On ROCm a
-// pinned page's device address equals its host address, so matching ends alone would also
-// accept a range running from one pinned allocation through pageable pages into another:
-// the allocation's bounds decide when the runtime reports them (hipHostMalloc memory); for
-// hipHostRegister'ed memory it reports the size but no base (scripts/probe_hostrange.cpp),
-// and the two ends must map contiguously.
+// for pageable memory, device memory or a range not inside ONE pinned allocation or
+// registration.  On ROCm a pinned page's device address equals its host address, so matching
+// ends would also accept a range running from one registration through unregistered pages
+// into another, and the kernel would fault on the gap: the runtime's range attributes
+// (start and size, reported for hipHostMalloc and hipHostRegister memory alike,
+// scripts/probe_hostrange.cpp) decide.  Anything the runtime cannot describe is staged.
 uint64_t pinned_device_range(const void *p, uint64_t n)
 {
-    auto dev_of = [](const void *q) -> uint64_t {
-        hipPointerAttribute_t a;
-        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
-            (void) hipGetLastError();
-            return 0;
-        }
-        if (a.type != hipMemoryTypeHost || !a.devicePointer)
-            return 0;
-        return uint64_t(uintptr_t(a.devicePointer));
-    };
-    const uint64_t d0 = dev_of(p);
-    if (!d0 || n == 0)
-        return d0;
-    hipDeviceptr_t base = nullptr;
-    size_t size = 0;
-    if (hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(uintptr_t(d0))) == hipSuccess
-        && base) {
-        const uint64_t b = uint64_t(uintptr_t(base));
-        return d0 >= b && n <= size && d0 - b <= size - n ? d0 : 0;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void) hipGetLastError();
+        return 0;
     }
-    (void) hipGetLastError();
-    const uint64_t d1 = dev_of(static_cast<const char *>(p) + (n - 1));
-    return d1 == d0 + (n - 1) ? d0 : 0;
+    if (a.type != hipMemoryTypeHost || !a.devicePointer)
+        return 0;
+    const uint64_t d0 = uint64_t(uintptr_t(a.devicePointer));
+    if (n == 0)
+        return d0;
+    void *start = nullptr;
+    size_t size = 0;
+    hipDeviceptr_t q = reinterpret_cast<hipDeviceptr_t>(const_cast<void *>(p));
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, q) != hipSuccess
+        || hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, q) != hipSuccess || !start) {
+        (void) hipGetLastError();
+        return 0;
+    }
+    const uint64_t s0 = uint64_t(uintptr_t(start)), h = uint64_t(uintptr_t(p));
+    return h >= s0 && n <= size && h - s0 <= size - n ? d0 : 0;
 }
 
 struct Window {
@@ -1467,6 +1464,14 @@ int64_t ddt_type_plan_list(const ddt_datatype_t *t, size_t leaf, int64_t *disp, 
         len[k] = X.len.empty() ? X.ulen : X.len[k];
     }
     return int64_t(n);
+}
+
+int ddt_debug_host_window(const void *p, size_t n, uint64_t *device_addr)
+{
+    if (!device_addr)
+        return DDT_ERR_BAD_PARAM;
+    *device_addr = pinned_device_range(p, n);
+    return *device_addr ? 1 : 0;
 }
 
 int ddt_debug_items(const ddt_datatype_t *t, size_t count, uint64_t user, uint64_t pk, uint64_t w0,

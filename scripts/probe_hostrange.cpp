@@ -19,6 +19,15 @@ static void probe(const char *what, void *p, size_t n)
         printf("  +%zu: range %s base %p size %zu (alloc %p + %zu)\n", off, hipGetErrorString(e), base, size,
                p, n);
         (void) hipGetLastError();
+        void *start = nullptr;
+        size_t rsize = 0;
+        hipError_t e1 = hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
+                                               (hipDeviceptr_t)((char *) p + off));
+        hipError_t e2 = hipPointerGetAttribute(&rsize, HIP_POINTER_ATTRIBUTE_RANGE_SIZE,
+                                               (hipDeviceptr_t)((char *) p + off));
+        printf("        attribute range: %s start %p / %s size %zu\n", hipGetErrorString(e1), start,
+               hipGetErrorString(e2), rsize);
+        (void) hipGetLastError();
     }
 }
 
@@ -33,6 +42,18 @@ int main()
     if (hipHostRegister(r, n, hipHostRegisterDefault) != hipSuccess)
         return 2;
     probe("hipHostRegister", r, n);
+    // two registrations of one pageable buffer with an unregistered page gap between them
+    char *g = (char *) aligned_alloc(4096, 3 * 4096 * 16);
+    if (hipHostRegister(g, 4096 * 16, hipHostRegisterDefault) != hipSuccess
+        || hipHostRegister(g + 4096 * 32, 4096 * 16, hipHostRegisterDefault) != hipSuccess)
+        return 4;
+    probe("gap: first registration", g, 4096 * 16);
+    probe("gap: second registration", g + 4096 * 32, 4096 * 16);
+    hipPointerAttribute_t ga;
+    hipError_t ge = hipPointerGetAttributes(&ga, g + 4096 * 20);
+    printf("gap page: attr %s type %d dev %p\n", hipGetErrorString(ge), int(ge == hipSuccess ? ga.type : -1),
+           ge == hipSuccess ? ga.devicePointer : nullptr);
+    (void) hipGetLastError();
     void *d = nullptr;
     if (hipMalloc(&d, n) != hipSuccess)
         return 3;

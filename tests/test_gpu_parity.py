@@ -741,6 +741,54 @@ def sorted_from(request):
     L.ddt_tune(b"sorted", -1)
 
 
+def test_pinned_window_across_registrations_is_staged(device):
+    """A host buffer with two hipHostRegister'ed ranges and an unregistered gap between them:
+    both ends of the whole buffer are pinned and map 1:1, but the kernel must not touch the
+    gap.  The engine's decision is checked without moving data (a window inside one
+    registration is moved directly by the kernel, one that spans or straddles the gap goes
+    to HBM staging, whose pageable path other tests cover; no copy here ever targets the gap),
+    then MPI_Pack / MPI_Unpack through the second registration are bit-exact."""
+    import ctypes
+    import torch
+    import ompi_amd
+    from ompi_amd import datatype as D
+    L = ompi_amd.lib()
+    paths = {ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln}
+    if len(paths) != 1:
+        pytest.skip(f"HIP runtime not unique in this process: {sorted(paths)}")
+    hip = ctypes.CDLL(paths.pop())
+    hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    page, R1 = 4096, 64 * 4096
+    raw = np.zeros(3 * R1 + page, dtype=np.uint8)
+    base = (raw.ctypes.data + page - 1) // page * page
+    assert hip.hipHostRegister(base, R1, 0) == 0
+    assert hip.hipHostRegister(base + 2 * R1, R1, 0) == 0
+    try:
+        dev = ctypes.c_uint64()
+        decide = lambda p, n: L.ddt_debug_host_window(p, n, ctypes.byref(dev))   # noqa: E731
+        assert decide(base, R1) == 1 and dev.value == base
+        assert decide(base + 2 * R1 + 8, R1 - 8) == 1
+        assert decide(base, 3 * R1) == 0            # spans the unregistered gap
+        assert decide(base + R1 - 8, 16) == 0       # straddles into it
+        assert decide(base + R1 + 8, 64) == 0       # inside it
+        n = R1 // 8
+        t = D.create_vector(n, 1, 2, D.predefined(D.FLOAT8)).commit()
+        user = torch.randint(-2**62, 2**62, (2 * n,), dtype=torch.int64, device=device)
+        win = base + 2 * R1
+        off = win - raw.ctypes.data
+        assert ompi_amd.pack(user, 1, t, win, R1, 0) == R1
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(raw[off:off + R1].view(np.int64), user[0::2].cpu().numpy())
+        dst = torch.full((2 * n,), 0x5A5A5A5A5A5A5A5A, dtype=torch.int64, device=device)
+        assert ompi_amd.unpack(win, R1, 0, dst, 1, t) == R1
+        assert torch.equal(dst[0::2], user[0::2])
+        assert bool((dst[1::2] == 0x5A5A5A5A5A5A5A5A).all())
+    finally:
+        hip.hipHostUnregister(base)
+        hip.hipHostUnregister(base + 2 * R1)
+
+
 @pytest.mark.parametrize("seed", range(int(__import__("os").environ.get("DDT_FUZZ_PINNED_SEEDS", "2"))))
 def test_fuzz_pinned_host_iovecs_capped_grid(device, seed):
     """Random types packed into and unpacked from PINNED host memory, which the kernel moves
