@@ -18,7 +18,9 @@ message, device iovec) + one unpack of the same message.
                convertor) on the host cores of the same box, bounded sample.
 
 Other BASELINE configs: --config cfg1|cfg3|cfg4|cfg5 (cfg2 is the default).
-Launch: python bench.py --gpus N --steps K --warmup W (N > 1 via torch.distributed.run).
+Launch: python bench.py --gpus N --steps K --warmup W.  For N > 1 the driver starts one rank
+per GPU with torch.distributed.run; run by hand without WORLD_SIZE, bench.py starts that
+launcher itself as a child process (before anything touches the GPU) and exits with its code.
 """
 from __future__ import annotations
 
@@ -274,12 +276,17 @@ def single_face_latency(dev, stream, user, origin, reps=200):
 
 
 # ------------------------------------------------------------------ per-face throughput
-def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z")):
+def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z"), flush=True):
     """The north star's per-face figure: ONE face type of the 256^3
     double grid over `fields` fields in one launch (count = fields), pack then unpack, each
     timed with HIP events (median over `steps`).  With 512 fields a face's working set
-    (user lines + packed stream, 2 x 256 MiB) is twice the 256 MiB Infinity Cache, so the
-    loop streams from HBM; at the bench's 16 fields a face is 8 MiB and launch-bound."""
+    (user lines + packed stream, 2 x 256 MiB) is twice the 256 MiB Infinity Cache; at the
+    bench's 16 fields a face is 8 MiB and launch-bound.
+
+    flush=True ("exceed the 256 MB Infinity Cache, or flush it between reps"):
+    before every pack and between the pack and the unpack, outside the events, the stream
+    writes a 1 GiB scribble buffer (4x the Infinity Cache, 64x the L2s), so each operation
+    starts with neither its inputs nor the other operation's dirty lines cached."""
     import torch
     import ompi_amd
     from ompi_amd import recipe as ER
@@ -287,8 +294,9 @@ def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z")):
     field = 256 ** 3 * 8
     user = torch.empty(fields * field, dtype=torch.uint8, device=dev)
     user.fill_(0x5A)
+    scribble = torch.empty(1 << 30, dtype=torch.uint8, device=dev) if flush else None
     stream = torch.cuda.current_stream(dev)
-    out = {"fields": fields}
+    out = {"fields": fields, "flushed": flush}
     for k in faces:
         ft = ER.build_committed(recs[k])
         fS = ft.info()["size"] * fields
@@ -297,25 +305,87 @@ def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z")):
         c1.set_stream(stream, True)
         evs = []
         for i in range(warmup + steps):
-            a, b_, c_ = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            a, b_, c_, d_ = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+            if flush:
+                scribble.fill_(i & 0xFF)
             a.record(stream)
             c1.prepare_for_send(ft, fields, user.data_ptr())
             c1.pack([(fp, fS)])
             b_.record(stream)
+            if flush:
+                scribble.fill_((i + 128) & 0xFF)
+            c_.record(stream)
             c1.prepare_for_recv(ft, fields, user.data_ptr())
             c1.unpack([(fp, fS)])
-            c_.record(stream)
+            d_.record(stream)
             if i >= warmup:
-                evs.append((a, b_, c_))
+                evs.append((a, b_, c_, d_))
         torch.cuda.synchronize()
-        tp = float(np.median([a.elapsed_time(b_) for a, b_, _ in evs])) / 1e3
-        tu = float(np.median([b_.elapsed_time(c_) for _, b_, c_ in evs])) / 1e3
+        tp = float(np.median([a.elapsed_time(b_) for a, b_, _, _ in evs])) / 1e3
+        tu = float(np.median([c_.elapsed_time(d_) for _, _, c_, d_ in evs])) / 1e3
         out[k] = {"packed_bytes": fS, "pack_us": round(tp * 1e6, 2), "unpack_us": round(tu * 1e6, 2),
-                  "GiBs": round(2 * fS / (tp + tu) / GiB, 1), "frac": round(4 * fS / (tp + tu) / HBM_PEAK, 4)}
+                  "GiBs": round(2 * fS / (tp + tu) / GiB, 1), "frac": round(4 * fS / (tp + tu) / HBM_PEAK, 4),
+                  "pack_frac": round(2 * fS / tp / HBM_PEAK, 4), "unpack_frac": round(2 * fS / tu / HBM_PEAK, 4)}
         del fp
-    del user
+    del user, scribble
     torch.cuda.empty_cache()
     return out
+
+
+# ------------------------------------------------------------------ multi-rank harness
+def self_launch_argv(gpus, argv, port):
+    """The launcher command for `--gpus N` run by hand: one rank per GPU on this node, the
+    same command line, rendezvous on 127.0.0.1 (torch.distributed.run sets RANK, LOCAL_RANK,
+    WORLD_SIZE and MASTER_*; every rank binds cuda:LOCAL_RANK)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def timed_region(step, steps, world, sync, reduce_max, barrier):
+    """Time exactly `steps` calls of step(i) between a barrier + device synchronize on both
+    sides; returns the wall time, max over ranks (the driver contract)."""
+    if world > 1:
+        barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    sync()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        wall = reduce_max(wall)
+        barrier()
+    return wall
+
+
+def gather_check(packed, S, world, rank, dev, backend):
+    """The RCCL leg of SURVEY.md §8e, outside the timed region: the packed shards are
+    all-gathered (backend "nccl" = RCCL over xGMI) and every rank checks that its slice of the
+    gathered stream is its own shard."""
+    import torch
+    import torch.distributed as dist
+    from ompi_amd import shard
+    side = dev if backend == "nccl" else "cpu"
+    g0 = time.perf_counter()
+    full = shard.gather_packed(packed if backend == "nccl" else packed.cpu())
+    if backend == "nccl":
+        torch.cuda.synchronize()
+    g_s = time.perf_counter() - g0
+    sizes = [torch.zeros(1, dtype=torch.int64, device=side) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([S], dtype=torch.int64, device=side))
+    off = sum(int(x.item()) for x in sizes[:rank])
+    ok = torch.tensor([1 if torch.equal(full[off:off + S].to(packed.device), packed) else 0],
+                      dtype=torch.int64, device=side)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    return {"backend": backend, "gathered_bytes": int(full.numel()), "ok": bool(ok.item()),
+            "seconds": round(g_s, 4)}
 
 
 # ------------------------------------------------------------------ main
@@ -343,6 +413,12 @@ def main():
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-face latency probe (profiling runs: one workload per trace)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # run by hand: start one rank per GPU as child processes, before any HIP call here
+        import subprocess
+        rc = subprocess.call(self_launch_argv(args.gpus, sys.argv[1:], free_port()))
+        sys.exit(rc)
 
     import torch
     import torch.distributed as dist
@@ -436,29 +512,27 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) if (args.steps - 1 - i) % every == 0 else None
           for i in range(args.steps)]   # counted from the last step: step 0 (host enqueue lag) is skipped
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for es in ev:
+
+    def step(i):
+        es = ev[i]
         if es is None:
             pack()
             unpack()
-            continue
+            return
         e0, e1, e2 = es
         e0.record(stream)
         pack()
         e1.record(stream)
         unpack()
         e2.record(stream)
-    torch.cuda.synchronize()
-    ev = [es for es in ev if es is not None]
-    wall = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([wall], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
+
+    def reduce_max(x):
+        t = torch.tensor([x], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.barrier()
-        wall = float(t.item())
+        return float(t.item())
+
+    wall = timed_region(step, args.steps, world, torch.cuda.synchronize, reduce_max, dist.barrier)
+    ev = [es for es in ev if es is not None]
     tp = float(np.mean([a.elapsed_time(b) for a, b, _ in ev])) / 1e3
     tu = float(np.mean([b.elapsed_time(c) for _, b, c in ev])) / 1e3
 
@@ -492,21 +566,7 @@ def main():
     # xGMI); every rank checks that its slice of the gathered stream is its own shard.
     rccl = None
     if world > 1 and not args.no_gather:
-        from ompi_amd import shard
-        g0 = time.perf_counter()
-        full = shard.gather_packed(packed if backend == "nccl" else packed.cpu())
-        torch.cuda.synchronize()
-        g_s = time.perf_counter() - g0
-        sizes = [torch.zeros(1, dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
-                 for _ in range(world)]
-        dist.all_gather(sizes, torch.tensor([S], dtype=torch.int64, device=sizes[0].device))
-        off = sum(int(x.item()) for x in sizes[:rank])
-        ok = torch.tensor([1 if torch.equal(full[off:off + S].to(packed.device), packed) else 0],
-                          dtype=torch.int64, device=sizes[0].device)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        rccl = {"backend": backend, "gathered_bytes": int(full.numel()), "ok": bool(ok.item()),
-                "seconds": round(g_s, 4)}
-        del full
+        rccl = gather_check(packed, S, world, rank, dev, backend)
 
     result = None
     if rank == 0:
@@ -515,7 +575,10 @@ def main():
         achieved = 4.0 * S / (tp + tu)
         result = {
             "metric": "pack+unpack GiB/s/GPU (device-resident), 256^3 double 3D-vector; %HBM peak",
+            # value = the whole job's packed bytes in and out / wall time (the driver
+            # contract: units all ranks processed / max-over-ranks time); per GPU beside it
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "per_gpu_GiBs": round(value / world, 3), "aggregate_GiBs": round(value, 3),
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "strong" if split else "weak", "vs_baseline": None,
             "dtype": "u8", "data": "synthetic",
@@ -561,6 +624,8 @@ def main():
         # per-face figure of the north star: each face type alone, batched over many fields
         # (beyond the Infinity Cache), and at the bench's own 16 fields (launch-bound)
         result["faces"] = face_throughput(dev, args.face_fields, max(5, min(args.steps, 20)))
+        result["faces_unflushed"] = face_throughput(dev, args.face_fields, max(5, min(args.steps, 20)),
+                                                    flush=False)
         result["faces_at_bench_fields"] = face_throughput(dev, count, max(5, min(args.steps, 20)))
 
     if rank == 0 and base_sample is not None:

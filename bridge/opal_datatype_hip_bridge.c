@@ -34,6 +34,10 @@ typedef struct bridge_entry {
     ptrdiff_t lb, ub, true_lb, true_ub;
     uint64_t sig;
     ddt_datatype_t *type;
+    /* calls between bridge_type_of and bridge_release; an entry unlinked by a destruct or a
+     * stale-address eviction while calls still use it is freed by the last of them */
+    size_t inflight;
+    int unlinked;
     struct bridge_entry *next;
 } bridge_entry;
 
@@ -73,8 +77,32 @@ static int same_fingerprint(const bridge_entry *e, const opal_datatype_t *dt, co
            && e->ub == dt->ub && e->true_lb == dt->true_lb && e->true_ub == dt->true_ub && e->sig == sig;
 }
 
-/* The committed engine type of the convertor's description (imported on first use). */
-static ddt_datatype_t *bridge_type_of(const opal_convertor_t *conv, int *err)
+/* Called with g_mu held on an entry already taken off its bucket list. */
+static void retire_locked(bridge_entry *e)
+{
+    --g_entries;
+    if (e->inflight) {   /* a call on another thread still moves data with it */
+        e->unlinked = 1;
+        return;
+    }
+    ddt_type_destroy(&e->type);
+    free(e);
+}
+
+static void bridge_release(bridge_entry *e)
+{
+    pthread_mutex_lock(&g_mu);
+    if (--e->inflight == 0 && e->unlinked) {
+        ddt_type_destroy(&e->type);
+        free(e);
+    }
+    pthread_mutex_unlock(&g_mu);
+}
+
+/* The cache entry of the convertor's description (imported on first use), held for the
+ * caller until bridge_release: a destruct or an eviction on another thread in between only
+ * unlinks it. */
+static bridge_entry *bridge_type_of(const opal_convertor_t *conv, int *err)
 {
     const opal_datatype_t *dt = conv->pDesc;
     const dt_type_desc_t *ud = conv->use_desc ? conv->use_desc : (dt ? &dt->opt_desc : NULL);
@@ -92,16 +120,15 @@ static ddt_datatype_t *bridge_type_of(const opal_convertor_t *conv, int *err)
             continue;
         if (same_fingerprint(*pp, dt, ud, sig)) {
             ++g_hits;
-            ddt_datatype_t *t = (*pp)->type;
+            bridge_entry *e = *pp;
+            ++e->inflight;
             pthread_mutex_unlock(&g_mu);
-            return t;
+            return e;
         }
         /* a different description at this address: the old datatype died unseen */
         bridge_entry *old = *pp;
         *pp = old->next;
-        ddt_type_destroy(&old->type);
-        free(old);
-        --g_entries;
+        retire_locked(old);
         ++g_stale;
         break;
     }
@@ -130,12 +157,13 @@ static ddt_datatype_t *bridge_type_of(const opal_convertor_t *conv, int *err)
     e->true_ub = dt->true_ub;
     e->sig = sig;
     e->type = t;
+    e->inflight = 1;
     e->next = g_buckets[b];
     g_buckets[b] = e;
     ++g_entries;
     ++g_imports;
     pthread_mutex_unlock(&g_mu);
-    return t;
+    return e;
 }
 
 void opal_hip_bridge_datatype_destruct(const opal_datatype_t *dt)
@@ -145,9 +173,7 @@ void opal_hip_bridge_datatype_destruct(const opal_datatype_t *dt)
         if ((*pp)->key == dt) {
             bridge_entry *old = *pp;
             *pp = old->next;
-            ddt_type_destroy(&old->type);
-            free(old);
-            --g_entries;
+            retire_locked(old);
         } else {
             pp = &(*pp)->next;
         }
@@ -162,11 +188,9 @@ void opal_hip_bridge_finalize(void)
         while (g_buckets[b]) {
             bridge_entry *old = g_buckets[b];
             g_buckets[b] = old->next;
-            ddt_type_destroy(&old->type);
-            free(old);
+            retire_locked(old);
         }
     }
-    g_entries = 0;
     pthread_mutex_unlock(&g_mu);
 }
 
@@ -223,24 +247,19 @@ static int32_t opal_code(int rc)
     }
 }
 
-static int32_t bridge_advance(opal_convertor_t *conv, struct iovec *iov, uint32_t *out_size,
-                              size_t *max_data, int pack)
+/* The hipStream_t of an accelerator stream object: the rocm component keeps it in a malloc'ed
+ * cell that opal_accelerator_stream_t::stream points to (GET_STREAM,
+ * accelerator_rocm_module.c:80; created at :176-182). */
+static void *hip_stream_of(const opal_accelerator_stream_t *s)
 {
-    if (!conv || !out_size || !max_data || (*out_size && !iov))
-        return OPAL_ERR_BAD_PARAM;
-    if (conv->flags & CONVERTOR_COMPLETED) {   /* opal_convertor_pack/unpack guard (:258-261) */
-        if (*out_size)
-            iov[0].iov_len = 0;
-        *out_size = 0;
-        *max_data = 0;
-        return 1;
-    }
-    if (!(conv->flags & CONVERTOR_HOMOGENEOUS))   /* as the accelerator movers assert (:180) */
-        return OPAL_ERR_NOT_SUPPORTED;
-    int err;
-    ddt_datatype_t *t = bridge_type_of(conv, &err);
-    if (!t)
-        return err;
+    if (!s || s == OPAL_ACCELERATOR_STREAM_DEFAULT || !s->stream)
+        return NULL;
+    return *(void *const *) s->stream;
+}
+
+static int32_t bridge_move(opal_convertor_t *conv, ddt_datatype_t *t, struct iovec *iov,
+                           uint32_t *out_size, size_t *max_data, int pack)
+{
     ddt_convertor_t *h = thread_convertor();
     if (!h)
         return OPAL_ERR_OUT_OF_RESOURCE;
@@ -257,15 +276,37 @@ static int32_t bridge_advance(opal_convertor_t *conv, struct iovec *iov, uint32_
     int async = 0;
     if (conv->flags & CONVERTOR_ACCELERATOR_ASYNC) {
         async = 1;
-        if (conv->stream && conv->stream != OPAL_ACCELERATOR_STREAM_DEFAULT)
-            stream = conv->stream->stream;
+        stream = hip_stream_of(conv->stream);
     }
     ddt_convertor_set_stream(h, stream, async);
     int32_t r = pack ? ddt_convertor_pack(h, iov, out_size, max_data)
                      : ddt_convertor_unpack(h, iov, out_size, max_data);
     ddt_convertor_set_stream(h, NULL, 0);
+    return r < 0 ? opal_code(r) : r;
+}
+
+static int32_t bridge_advance(opal_convertor_t *conv, struct iovec *iov, uint32_t *out_size,
+                              size_t *max_data, int pack)
+{
+    if (!conv || !out_size || !max_data || (*out_size && !iov))
+        return OPAL_ERR_BAD_PARAM;
+    if (conv->flags & CONVERTOR_COMPLETED) {   /* opal_convertor_pack/unpack guard (:258-261) */
+        if (*out_size)
+            iov[0].iov_len = 0;
+        *out_size = 0;
+        *max_data = 0;
+        return 1;
+    }
+    if (!(conv->flags & CONVERTOR_HOMOGENEOUS))   /* as the accelerator movers assert (:180) */
+        return OPAL_ERR_NOT_SUPPORTED;
+    int err;
+    bridge_entry *e = bridge_type_of(conv, &err);
+    if (!e)
+        return err;
+    int32_t r = bridge_move(conv, e->type, iov, out_size, max_data, pack);
+    bridge_release(e);
     if (r < 0)
-        return opal_code(r);
+        return r;
     conv->bConverted += *max_data;
     conv->partial_length = 0;
     if (conv->bConverted == conv->local_size) {
@@ -289,10 +330,26 @@ int32_t opal_position_hip(opal_convertor_t *conv, size_t *position)
 {
     if (!conv || !position)
         return OPAL_ERR_BAD_PARAM;
-    /* opal_convertor_set_position has clamped to the packed size and cleared COMPLETED */
-    conv->bConverted = *position;
+    /* opal_convertor_set_position has clamped to the packed size and cleared COMPLETED.
+     * opal_convertor_position_generic (opal_convertor.c:445-471) walks the description to the
+     * position (opal_datatype_position.c:167-367); a send convertor then drops the partial
+     * predefined element (bConverted -= partial_length) and reports the snapped position.
+     * The snap follows the imported use_desc, so a UINT4 blen 5 carrier snaps to 4 bytes. */
+    size_t p = *position;
+    if (conv->flags & CONVERTOR_SEND) {
+        int err;
+        bridge_entry *e = bridge_type_of(conv, &err);
+        if (!e)
+            return err;
+        const int rc = ddt_type_snap_position(e->type, p, &p);
+        bridge_release(e);
+        if (rc != DDT_SUCCESS)
+            return opal_code(rc);
+    }
+    conv->bConverted = p;
     conv->partial_length = 0;
     conv->stack_pos = 0;
+    *position = p;
     return OPAL_SUCCESS;
 }
 
@@ -303,8 +360,10 @@ int opal_hip_bridge_attach(opal_convertor_t *conv)
     if (!(conv->flags & CONVERTOR_ACCELERATOR) || !(conv->flags & CONVERTOR_HOMOGENEOUS))
         return OPAL_ERR_NOT_SUPPORTED;   /* host buffers keep the reference movers */
     int err;
-    if (!bridge_type_of(conv, &err))
+    bridge_entry *e = bridge_type_of(conv, &err);
+    if (!e)
         return err;
+    bridge_release(e);
     conv->fAdvance = (conv->flags & CONVERTOR_SEND) ? opal_pack_hip : opal_unpack_hip;
     conv->fPosition = opal_position_hip;
     return OPAL_SUCCESS;

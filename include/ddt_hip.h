@@ -198,8 +198,15 @@ int32_t ddt_convertor_pack(ddt_convertor_t *conv, struct iovec *iov, uint32_t *o
  * (opal_datatype_unpack_accelerator.c:210-368).  Accepts arbitrary byte windows. */
 int32_t ddt_convertor_unpack(ddt_convertor_t *conv, struct iovec *iov, uint32_t *out_size,
                              size_t *max_data);
-/* opal_convertor_set_position (opal_convertor.h:357-394) */
+/* opal_convertor_set_position (opal_convertor.h:357-394).  A send convertor that is not NO_OP
+ * (the type has gaps and is not one contiguous instance) lands on the predefined-element
+ * boundary at or below *position and returns it there, as opal_convertor_position_generic
+ * does (opal_convertor.c:458-470); a receive convertor takes any byte. */
 int ddt_convertor_set_position(ddt_convertor_t *conv, size_t *position);
+/* The send-side snap alone: the packed position of the predefined-element boundary of the
+ * committed type map at or below `position` (opal_datatype_position.c:167-367 followed by
+ * bConverted -= partial_length, opal_convertor.c:465-468).  For the fPosition of a bridge. */
+int ddt_type_snap_position(const ddt_datatype_t *type, size_t position, size_t *snapped);
 /* opal_convertor_get_packed_size / get_unpacked_size (opal_convertor.h:240-262) */
 int ddt_convertor_get_packed_size(const ddt_convertor_t *conv, size_t *size);
 /* bConverted and CONVERTOR_COMPLETED (opal_convertor.h:137-148) */

@@ -36,8 +36,11 @@ int32_t opal_pack_hip(opal_convertor_t *conv, struct iovec *iov, uint32_t *out_s
  * accepts any byte window, mid-element splits included (:344-352). */
 int32_t opal_unpack_hip(opal_convertor_t *conv, struct iovec *iov, uint32_t *out_size, size_t *max_data);
 /* convertor_position_fct_t (opal_convertor.h:104), called by opal_convertor_set_position
- * (:357-394) for a position inside the stream: the engine resumes from the byte position
- * alone, so this records it (bConverted) and clears the descriptor stack. */
+ * (:357-394) for a position inside the stream; replaces opal_convertor_position_generic
+ * (opal_convertor.c:445-471).  A send convertor lands on the predefined-element boundary of
+ * use_desc at or below *position and returns it there (:465-469); a receive convertor takes
+ * the byte.  The engine resumes from the byte position alone, so this records it
+ * (bConverted) and clears the descriptor stack. */
 int32_t opal_position_hip(opal_convertor_t *conv, size_t *position);
 
 /* Post-prepare hook: for a homogeneous accelerator convertor (CONVERTOR_ACCELERATOR set by

@@ -140,7 +140,8 @@ typedef struct dt_stack_t {
 
 typedef struct opal_accelerator_stream_t {
     opal_object_t super;
-    void *stream;                     /* hipStream_t for the rocm component */
+    void *stream;                     /* rocm component: a malloc'ed hipStream_t cell, i.e. a
+                                         hipStream_t * (accelerator_rocm_module.c:80,176-182) */
 } opal_accelerator_stream_t;
 /* MCA_ACCELERATOR_STREAM_DEFAULT (accelerator.h:123): the default stream, not an object */
 #define OPAL_ACCELERATOR_STREAM_DEFAULT ((opal_accelerator_stream_t *) 0x00000002)

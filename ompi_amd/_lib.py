@@ -68,6 +68,7 @@ SIGNATURES = {
     "ddt_convertor_prepare_for_raw": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "ddt_convertor_raw": (c_int32, [c_void_p, P(IOVec), P(c_uint32), P(c_size_t)]),
     "ddt_convertor_set_position": (c_int, [c_void_p, P(c_size_t)]),
+    "ddt_type_snap_position": (c_int, [c_void_p, c_size_t, P(c_size_t)]),
     "ddt_convertor_get_packed_size": (c_int, [c_void_p, P(c_size_t)]),
     "ddt_convertor_get_position": (c_int, [c_void_p, P(c_size_t)]),
     "ddt_convertor_is_completed": (c_int, [c_void_p]),

@@ -624,6 +624,13 @@ int prepare(ddt_convertor *c, const ddt_datatype *t, size_t count, const void *b
     return DDT_SUCCESS;
 }
 
+// OPAL_CONVERTOR_PREPARE leaves CONVERTOR_NO_OP set, and fPosition NULL, for a type without
+// gaps or one contiguous instance (opal_convertor.c:562-567)
+bool is_no_op(const ddt_convertor *c)
+{
+    return (c->dt->flags & F_NO_GAPS) || ((c->dt->flags & F_CONTIGUOUS) && c->count == 1);
+}
+
 int32_t advance(ddt_convertor *c, struct iovec *iov, uint32_t *out_size, size_t *max_data, int dir)
 {
     if (!c || !c->prepared || !out_size || !max_data || (*out_size && !iov))
@@ -644,7 +651,7 @@ int32_t advance(ddt_convertor *c, struct iovec *iov, uint32_t *out_size, size_t 
     // gaps, or one contiguous instance) is moved by opal_convertor_pack's memcpy loop
     // (:262-302), which fills every iovec to the byte; other types go through the movers,
     // which never split a predefined element (_pack_accelerator.c:52-58).
-    const bool no_op = (c->dt->flags & F_NO_GAPS) || ((c->dt->flags & F_CONTIGUOUS) && c->count == 1);
+    const bool no_op = is_no_op(c);
     for (uint32_t i = 0; i < *out_size; ++i) {
         if (pos >= c->local_size)
             break;
@@ -728,7 +735,26 @@ int ddt_convertor_set_position(ddt_convertor_t *c, size_t *position)
         return DDT_SUCCESS;
     }
     c->completed = false;
-    c->bConverted = *position;
+    // A send convertor never stops inside a predefined element: opal_convertor_position_generic
+    // (opal_convertor.c:458-470) walks to the position (opal_datatype_position.c:167-367), then
+    // drops the partial element (bConverted -= partial_length) and hands back the snapped
+    // position.  A NO_OP convertor has no fPosition and lands on the byte (opal_convertor.h:389-392);
+    // a receive convertor accepts split elements.
+    uint64_t p = *position;
+    if (c->send && !is_no_op(c))
+        p = snap_down_to_element(c->dt, p);
+    c->bConverted = p;
+    *position = size_t(p);
+    return DDT_SUCCESS;
+}
+
+int ddt_type_snap_position(const ddt_datatype_t *t, size_t position, size_t *snapped)
+{
+    if (!t || !snapped)
+        return fail(DDT_ERR_BAD_PARAM, "null datatype or result");
+    if (!(t->flags & F_COMMITTED))
+        return fail(DDT_ERR_NOT_COMMITTED, "datatype not committed");
+    *snapped = size_t(snap_down_to_element(t, position));
     return DDT_SUCCESS;
 }
 

@@ -133,6 +133,14 @@ class Datatype:
         check(lib().ddt_type_cache_info(self.handle, out), "ddt_type_cache_info")
         return dict(zip(("cached", "retiring", "pinned", "device"), list(out)))
 
+    def snap_position(self, position: int) -> int:
+        """Predefined-element boundary at or below a packed position: where a send convertor's
+        set_position lands (opal_convertor_position_generic, opal_convertor.c:458-470)."""
+        s = ctypes.c_size_t()
+        check(lib().ddt_type_snap_position(self.handle, position, ctypes.byref(s)),
+              "ddt_type_snap_position")
+        return int(s.value)
+
     def __repr__(self):
         return f"Datatype({self.name}, {self.info()})"
 

@@ -691,6 +691,38 @@ int64_t ort_pack(ort_type *t, int64_t count, const void *base, int64_t position,
     return done;
 }
 
+/*
+ * opal_convertor_set_position (opal_convertor.h:357-394) followed by fPosition =
+ * opal_convertor_position_generic (opal_convertor.c:445-471) on a freshly prepared
+ * convertor of `count` instances.  Returns the position the convertor lands on:
+ *   - at or beyond the packed size: the packed size (:371-377);
+ *   - a NO_OP convertor (no gaps, or one contiguous instance) has fPosition == NULL
+ *     (OPAL_CONVERTOR_PREPARE :534, :562-567) and lands on the byte (:389-392);
+ *   - a receive convertor: generic_simple_position (opal_datatype_position.c:167-367)
+ *     stops with partial_length bytes into an element and keeps the byte;
+ *   - a send convertor drops those bytes (bConverted -= partial_length, :465-468).
+ * The walk skips whole instances by the packed size (:196-218), then whole blocks
+ * (position_predefined_data :73-165); what remains short of one element is partial_length
+ * (:336-338): in the flattened map, the offset inside the element run modulo the element
+ * size.
+ */
+int64_t ort_set_position(ort_type *t, int64_t count, int64_t position, int send)
+{
+    const int64_t total = count * t->size;
+    if (total <= position)
+        return total;
+    if (position <= 0)
+        return 0;
+    if ((t->flags & ORT_FLAG_NO_GAPS) || ((t->flags & ORT_FLAG_CONTIGUOUS) && count == 1))
+        return position;
+    if (!send)
+        return position;
+    ort_prefix(t);
+    int64_t inst, run, within;
+    ort_locate(t, position, &inst, &run, &within);
+    return position - within % t->runs[run].esize;
+}
+
 /* Byte-exact transfer of the packed window [position, position+len): dir 0 packs
  * (user -> stream), dir 1 unpacks (stream -> user).  Returns bytes moved. */
 static int64_t ort_xfer(ort_type *t, int64_t count, char *user, int64_t position, char *stream,

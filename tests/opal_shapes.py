@@ -211,8 +211,11 @@ class Convertor:
         if device:
             c.flags |= CONVERTOR_ACCELERATOR
         if stream is not None:   # pml_ob1_recvfrag.c:761-769: stream attached, ASYNC set
+            # the rocm component's stream object holds a pointer to a malloc'ed hipStream_t
+            # cell, not the handle itself (accelerator_rocm_module.c:80, :176-182)
+            self.stream_cell = ctypes.c_void_p(stream)
             self.stream_obj = AccelStream()
-            self.stream_obj.stream = stream
+            self.stream_obj.stream = ctypes.addressof(self.stream_cell)
             c.stream = ctypes.addressof(self.stream_obj)
             c.flags |= CONVERTOR_ACCELERATOR_ASYNC
         # OPAL_CONVERTOR_PREPARE (opal_convertor.c:526-591)

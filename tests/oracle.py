@@ -47,6 +47,7 @@ def lib():
             "ort_run_tid": (i64, [vp, i64]),
             "ort_pack": (i64, [vp, i64, vp, i64, vp, i64]),
             "ort_pack_bytes": (i64, [vp, i64, vp, i64, vp, i64]),
+            "ort_set_position": (i64, [vp, i64, i64, i]),
             "ort_unpack": (i64, [vp, i64, vp, i64, vp, i64]),
             "ort_run_mt": (i64, [vp, i64, vp, vp, i, i]),
             "ort_raw": (i64, [vp, i64, i64, i64, i64, vp, vp, vp]),
@@ -124,6 +125,11 @@ class OType:
         base = user.ctypes.data + origin
         return lib().ort_unpack(self.h, count, ctypes.c_void_p(base), position,
                                 src.ctypes.data_as(ctypes.c_void_p), len(data))
+
+    def set_position(self, count: int, position: int, send: bool = True) -> int:
+        """Where opal_convertor_set_position leaves a fresh convertor of `count` instances
+        (send convertors snap to the predefined-element boundary, opal_convertor.c:458-470)."""
+        return int(lib().ort_set_position(self.h, count, position, int(send)))
 
     def pack_all(self, count: int, user: np.ndarray, origin: int) -> bytes:
         total = count * self.size

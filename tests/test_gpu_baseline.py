@@ -22,7 +22,7 @@ from . import recipes as R
 pytestmark = pytest.mark.gpu
 
 
-def _expected_units(name, torch, dev):
+def _expected_units(name, torch, dev, fields=None):
     """(unit dtype, type-space unit indices of the packed stream in type-map order)."""
     if name == "cfg1":                      # vector(1024,1,2) double x 2048, extent 16376 B
         i = torch.arange(2048, device=dev, dtype=torch.int64)[:, None]
@@ -47,7 +47,7 @@ def _expected_units(name, torch, dev):
                  (a[:, None] * n * n + (n - 1) * n + a[None, :]).reshape(-1),
                  ((a[:, None] * n + a[None, :]) * n + (n - 1)).reshape(-1)]
         one = torch.cat(faces)
-        f = torch.arange(8, device=dev, dtype=torch.int64)[:, None]
+        f = torch.arange(fields or 8, device=dev, dtype=torch.int64)[:, None]
         return torch.int32, (f * n ** 3 + one[None, :]).reshape(-1)
     if name == "cfg4":                      # indexed_block(1, LCG disps) of float
         return torch.int32, torch.from_numpy(bench.lcg_disps(64 << 20)).to(dev)
@@ -57,13 +57,19 @@ def _expected_units(name, torch, dev):
     raise AssertionError(name)
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5", "cfg3_64"])
 def test_baseline_config_full_size(device, name):
+    """cfg3_64: BASELINE config 3 as `bench.py --config cfg3 --strong` runs it on one GPU,
+    all 64 fields (a 32 GiB user span: 64-bit offsets in every item)."""
     import torch
     import ompi_amd
     from ompi_amd import recipe as ER
 
+    fields = None
+    if name == "cfg3_64":
+        name, fields = "cfg3", 64
     recipe, count, _ = bench.make_workload(name)
+    count = fields or count
     dt = ER.build_committed(recipe)
     info = dt.info()
     S = info["size"] * count
@@ -74,7 +80,7 @@ def test_baseline_config_full_size(device, name):
     packed = torch.zeros(S, dtype=torch.uint8, device=device)
     assert ompi_amd.pack(user.data_ptr() + origin, count, dt, packed, S, 0) == S
 
-    ut, idx = _expected_units(name, torch, device)
+    ut, idx = _expected_units(name, torch, device, fields)
     unit = torch.tensor([], dtype=ut).element_size()
     assert idx.numel() * unit == S
     assert origin % unit == 0 and span % unit == 0

@@ -594,20 +594,19 @@ def test_darray_roundtrip(device):
 
 
 def _segments(total, seg):
-    """position.c create_segments + shuffle_segments (position.c:45-112)."""
-    segs = [(p, min(seg, total - p)) for p in range(0, total, seg)]
-    n = len(segs)
-    for i in range(0, n // 2, 2):
-        segs[i], segs[n - i - 1] = segs[n - i - 1], segs[i]
-    return segs
+    """Raw `seg`-byte windows of the stream, shuffled like position.c:87-98."""
+    from .positioning import shuffle_segments
+    return shuffle_segments([(p, min(seg, total - p)) for p in range(0, total, seg)])
 
 
 @pytest.mark.parametrize("case", ["position", "position_noncontig"])
-def test_reference_position_tests(device, case):
-    """position.c (MPI_LONG_DOUBLE_INT x 2048) and position_noncontig.c (vector(150,1,2)
-    of int): 113-byte segments, shuffled, packed as byte windows (the UCX form) and
-    unpacked through set_position; the receive buffer must equal the send buffer (gaps of
-    the vector keep 0xdeadbeef)."""
+def test_position_shapes_in_byte_windows(device, case):
+    """The shapes of position.c (MPI_LONG_DOUBLE_INT x 2048) and position_noncontig.c
+    (vector(150,1,2) of int) cut into raw 113-byte windows -- the UCX generic-datatype form
+    (ddt_pack_window, pml_ucx_datatype.c:72-88), which may split elements -- shuffled and
+    unpacked through a receive convertor's set_position; the receive buffer must equal the
+    send buffer (gaps of the vector keep 0xdeadbeef).  The reference's own flow (segments from a
+    send convertor's snapped set_position) is test_gpu_position.py."""
     import torch
     import ompi_amd
     from ompi_amd import datatype as D

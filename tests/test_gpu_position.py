@@ -1,0 +1,241 @@
+"""Send-side positioning on the GPU: position.c and
+position_noncontig.c restated faithfully (ompi/test/datatype/position.c:42-272,
+position_noncontig.c:42-230) through the opal bridge and through the engine convertor, plus
+send convertors positioned at random mid-element offsets and packed from there.
+
+The reference's flow: create_segments cuts the stream with a SEND convertor's
+set_position(start + 113), which snaps back to a predefined-element boundary
+(opal_convertor_position_generic, opal_convertor.c:458-470); pack_segments packs each segment
+after set_position(segment.position) on a send convertor and fails if the returned position
+differs or max_size != segment.size (position.c:100-135); unpack_segments does the same on a
+receive convertor; the receive buffer must then hold the sent values.
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+import pytest
+
+from . import corpus
+from . import opal_shapes as S
+from . import oracle as O
+from . import recipes as R
+from .positioning import create_segments, shuffle_segments
+
+pytestmark = pytest.mark.gpu
+
+UINT4, FLOAT8, FLOAT12, INT4 = 11, 16, 17, 6
+
+
+def _dev(arr, device):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(arr)).to(device)
+
+
+def _host(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+class _BridgeSide:
+    """Open MPI's convertor with the bridge in its slots (tests/opal_shapes.py)."""
+
+    def __init__(self, ot, count):
+        self.ot, self.count = ot, count
+
+    def send(self, buf):
+        c = S.Convertor()
+        assert c.prepare(self.ot, self.count, buf, send=True) == S.OPAL_SUCCESS
+        assert not (c.c.flags & S.CONVERTOR_NO_OP)
+        return c
+
+    def recv(self, buf):
+        c = S.Convertor()
+        assert c.prepare(self.ot, self.count, buf, send=False) == S.OPAL_SUCCESS
+        return c
+
+
+class _EngineSide:
+    """The engine's own convertor (include/ddt_hip.h) on an engine type."""
+
+    def __init__(self, et, count):
+        self.et, self.count = et, count
+
+    def send(self, buf):
+        import ompi_amd
+        return ompi_amd.Convertor().prepare_for_send(self.et, self.count, buf)
+
+    def recv(self, buf):
+        import ompi_amd
+        return ompi_amd.Convertor().prepare_for_recv(self.et, self.count, buf)
+
+
+def _position_test(side, oo, count, send_host, recv_host, device, expect_sizes=None):
+    """position.c main (:211-272) on `side`: segments from a send convertor (checked against
+    the oracle's walk), shuffled, packed through set_position + pack (position and max_size
+    checked like :116-131), unpacked through set_position + unpack; returns the receive
+    buffer."""
+    import torch
+    total = count * oo.size
+    send = _dev(send_host, device)
+    recv = _dev(recv_host, device)
+    # create_segments on a send convertor prepared on the send buffer (the reference prepares
+    # it on NULL: positioning reads no data)
+    pos_conv = side.send(send.data_ptr())
+    segs = create_segments(total, 113, pos_conv.set_position)
+    assert segs == create_segments(total, 113, lambda p: oo.set_position(count, p, send=True))
+    if expect_sizes is not None:
+        assert [n for _, n in segs] == expect_sizes
+    segs = shuffle_segments(segs)
+    bufs = [torch.zeros(max(n, 1), dtype=torch.uint8, device=device) for _, n in segs]
+    # pack_segments (:100-135): one send convertor, set_position to each segment start
+    pc = side.send(send.data_ptr())
+    for (p, n), b in zip(segs, bufs):
+        assert pc.set_position(p) == p
+        rc, _, md = pc.pack([(b.data_ptr(), n)])
+        assert rc >= 0 and md == n, (p, n, md)
+    # every segment is the oracle's stream slice
+    ref = np.frombuffer(oo.pack(count, send_host, 0, 0, total, element_granular=False), dtype=np.uint8)
+    for (p, n), b in zip(segs, bufs):
+        np.testing.assert_array_equal(_host(b)[:n], ref[p:p + n])
+    # unpack_segments (:137-173)
+    uc = side.recv(recv.data_ptr())
+    for (p, n), b in zip(segs, bufs):
+        assert uc.set_position(p) == p
+        rc, _, md = uc.unpack([(b.data_ptr(), n)])
+        assert rc >= 0 and md == n
+    return _host(recv)
+
+
+def _ldi_buffers():
+    """position.c:219-226: {long double ld; int i;} x 2048 with ld = i + i/100000, i = i.  The
+    receive buffer starts as 0xA5 (the reference copies the send buffer: stricter here, the
+    12 bytes of padding of every record must stay untouched)."""
+    n = 2048
+    rec = np.zeros((n, 32), dtype=np.uint8)
+    ld = np.array([i + i / 100000.0 for i in range(n)], dtype=np.longdouble)
+    rec[:, :16] = np.frombuffer(ld.tobytes(), dtype=np.uint8).reshape(n, 16)
+    rec[:, 10:16] = 0x3C   # x87 padding bytes: any value travels (copied as UINT4 carriers)
+    rec[:, 16:20] = np.arange(n, dtype=np.int32).view(np.uint8).reshape(n, 4)
+    rec[:, 20:] = 0x77
+    send = rec.reshape(-1)
+    recv = np.full(send.size, 0xA5, dtype=np.uint8)
+    want = recv.copy().reshape(n, 32)
+    want[:, :20] = rec[:, :20]
+    return send, recv, want.reshape(-1)
+
+
+def test_position_c_through_bridge(device):
+    """position.c on MPI_LONG_DOUBLE_INT x 2048 as the reference commits it (opt_desc
+    UINT4 count 1 blen 5, ub 32; ompi_datatype_module.c:449-474, opal_datatype_optimize.c:
+    581-611): 365 segments of 112 bytes and one of 80, every segment packed from its snapped
+    position, shuffled unpack rebuilds the records."""
+    ot = S.OpalType([S.data(UINT4, 1, 5, 20, 0)], 20, 0, 32, 0, 20, flags=S.F_CONTIGUOUS)
+    oo = O.resized(O.contiguous(5, O.basic(UINT4)), 0, 32)
+    send, recv, want = _ldi_buffers()
+    got = _position_test(_BridgeSide(ot, 2048), oo, 2048, send, recv, device,
+                         expect_sizes=[112] * 365 + [80])
+    np.testing.assert_array_equal(got, want)
+    ot.destruct()
+
+
+@pytest.mark.parametrize("form", ["reference_carriers", "typed_struct"])
+def test_position_c_through_engine(device, form):
+    """position.c through the engine convertor.  `reference_carriers`: the type the reference's
+    optimizer produces (5 UINT4, extent 32) -> the same 366 segments as the reference.
+    `typed_struct`: struct{MPI_LONG_DOUBLE @0, MPI_INT @16} resized to 32 built with the engine's
+    constructors, whose commit keeps the typed elements (DESIGN.md §1 deviation 3): segments
+    follow the 16/4-byte element grid, as the oracle's walk of the same type map does."""
+    from ompi_amd import datatype as D
+    if form == "reference_carriers":
+        et = D.create_resized(D.create_contiguous(5, D.predefined(UINT4)), 0, 32).commit()
+        oo = O.resized(O.contiguous(5, O.basic(UINT4)), 0, 32)
+        sizes = [112] * 365 + [80]
+    else:
+        st = D.create_struct([1, 1], [0, 16], [D.predefined(FLOAT12), D.predefined(INT4)])
+        et = D.create_resized(st, 0, 32).commit()
+        oo = O.resized(O.struct([1, 1], [0, 16], [O.basic(FLOAT12), O.basic(INT4)]), 0, 32)
+        sizes = None
+    send, recv, want = _ldi_buffers()
+    got = _position_test(_EngineSide(et, 2048), oo, 2048, send, recv, device, expect_sizes=sizes)
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("through", ["bridge", "engine"])
+def test_position_noncontig_c(device, through):
+    """position_noncontig.c (:180-230): vector(150, 1, 2) of MPI_INT, count 1, 113-byte
+    fragments -> five 112-byte segments and one of 40; odd ints keep 0xdeadbeef."""
+    from ompi_amd import datatype as D
+    oo = O.vector(150, 1, 2, O.basic(INT4))
+    if through == "bridge":
+        ot = S.OpalType([S.data(INT4, 150, 1, 8, 0)], 600, 0, 149 * 8 + 4, 0, 149 * 8 + 4)
+        side = _BridgeSide(ot, 1)
+    else:
+        side = _EngineSide(D.create_vector(150, 1, 2, D.predefined(INT4)).commit(), 1)
+    send = np.arange(300, dtype=np.int32).view(np.uint8)
+    recv = np.full(300, 0xdeadbeef - 2 ** 32, dtype=np.int32).view(np.uint8)
+    got = _position_test(side, oo, 1, send, recv, device, expect_sizes=[112] * 5 + [40])
+    want = np.where(np.arange(300) % 2 == 1, np.int32(0xdeadbeef - 2 ** 32), np.arange(300, dtype=np.int32))
+    np.testing.assert_array_equal(got.view(np.int32), want)
+
+
+def _mid_element_packs(side, oo, count, host, origin, device, rng, n_pos=24):
+    """Send convertors positioned at random (mostly mid-element) offsets: set_position returns
+    the oracle's snapped position and the pack that follows produces the oracle's
+    element-granular window from there, whatever the fragment size."""
+    import torch
+    total = count * oo.size
+    user = _dev(host, device)
+    out = torch.zeros(total + 64, dtype=torch.uint8, device=device)
+    for _ in range(n_pos):
+        p = rng.randrange(total)
+        want_p = oo.set_position(count, p, send=True)
+        c = side.send(user.data_ptr() + origin)
+        got_p = c.set_position(p)
+        assert got_p == want_p, (p, got_p, want_p)
+        frag = rng.choice([3, 7, 12, 16, 40, 113, 4096])
+        cap = min(frag, total - got_p)
+        rc, _, md = c.pack([(out.data_ptr(), cap)])
+        want = oo.pack(count, host, origin, got_p, cap, element_granular=True)
+        assert md == len(want), (p, got_p, frag, md, len(want))
+        np.testing.assert_array_equal(_host(out)[:md], np.frombuffer(want, dtype=np.uint8))
+
+
+@pytest.mark.parametrize("name", sorted(corpus.CORPUS))
+def test_send_set_position_mid_element_corpus(device, name):
+    """Every corpus type through the bridge (flat description) and the engine convertor."""
+    rec, _ = corpus.CORPUS[name]()
+    b = R.Built(rec)
+    info = b.o.info()
+    rng = random.Random("pos" + name)
+    for count in (1, 5):
+        if info["size"] == 0 or (info["flags"] & 0x20) or ((info["flags"] & 0x10) and count == 1):
+            continue   # NO_OP: no fPosition, byte positions (opal_convertor.h:389-392)
+        span, origin = R.layout(info, count)
+        host = R.fill(span, 0x33)
+        ot = S.flat_from_oracle(b.o)
+        _mid_element_packs(_BridgeSide(ot, count), b.o, count, host, origin, device, rng)
+        _mid_element_packs(_EngineSide(b.engine(), count), b.o, count, host, origin, device, rng)
+        ot.destruct()
+
+
+def test_send_set_position_cfg5_promoted_record(device):
+    """cfg5's committed description (UINT4 count N blen 5 extent 32 for
+    hvector(N, 1, 32 B) of struct{double, int[3]}) at N = 64 Ki through the bridge: send
+    positions snap to the 4-byte carriers, not to the double/int elements of the type map."""
+    n = 64 * 1024
+    ot = S.OpalType([S.data(UINT4, n, 5, 32, 0)], 20 * n, 0, 32 * (n - 1) + 20, 0, 32 * (n - 1) + 20)
+    oo = O.hvector(n, 1, 32, O.contiguous(5, O.basic(UINT4)))
+    span = 32 * n
+    host = R.fill(span, 5)
+    rng = random.Random(55)
+    _mid_element_packs(_BridgeSide(ot, 1), oo, 1, host, 0, device, rng, n_pos=64)
+    # the engine's own struct type snaps on its typed elements (double @0, ints @8..19)
+    from ompi_amd import datatype as D
+    st = D.create_struct([1, 3], [0, 8], [D.predefined(FLOAT8), D.predefined(INT4)])
+    et = D.create_hvector(n, 1, 32, st).commit()
+    ost = O.struct([1, 3], [0, 8], [O.basic(FLOAT8), O.basic(INT4)])
+    _mid_element_packs(_EngineSide(et, 1), O.hvector(n, 1, 32, ost), 1, host, 0, device, rng, n_pos=64)
+    ot.destruct()
