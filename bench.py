@@ -276,17 +276,22 @@ def single_face_latency(dev, stream, user, origin, reps=200):
 
 
 # ------------------------------------------------------------------ per-face throughput
-def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z"), flush=True):
+def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z"), flush="read"):
     """The north star's per-face figure: ONE face type of the 256^3
     double grid over `fields` fields in one launch (count = fields), pack then unpack, each
     timed with HIP events (median over `steps`).  With 512 fields a face's working set
     (user lines + packed stream, 2 x 256 MiB) is twice the 256 MiB Infinity Cache; at the
     bench's 16 fields a face is 8 MiB and launch-bound.
 
-    flush=True ("exceed the 256 MB Infinity Cache, or flush it between reps"):
-    before every pack and between the pack and the unpack, outside the events, the stream
-    writes a 1 GiB scribble buffer (4x the Infinity Cache, 64x the L2s), so each operation
-    starts with neither its inputs nor the other operation's dirty lines cached."""
+    flush ("exceed the 256 MB Infinity Cache, or flush it between reps"): before
+    every pack and between the pack and the unpack, outside the events, the stream touches a
+    1 GiB scribble buffer (4x the Infinity Cache, 32x the L2s).
+      "read"  (default): a reduction reads it, so each operation starts cold AND clean: none
+               of its inputs cached, and the other operation's dirty lines already written back
+               (during the flush, outside the events);
+      "write": a fill writes it, so each operation starts cold but with up to 256 MiB of dirty
+               scribble lines whose write-back it pays inside its own events;
+      None:    no flush (the face's own 512 MiB working set, partly cache-resident)."""
     import torch
     import ompi_amd
     from ompi_amd import recipe as ER
@@ -294,9 +299,15 @@ def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z"), flush=T
     field = 256 ** 3 * 8
     user = torch.empty(fields * field, dtype=torch.uint8, device=dev)
     user.fill_(0x5A)
-    scribble = torch.empty(1 << 30, dtype=torch.uint8, device=dev) if flush else None
+    scribble = torch.full((1 << 27,), 3, dtype=torch.int64, device=dev) if flush else None
     stream = torch.cuda.current_stream(dev)
-    out = {"fields": fields, "flushed": flush}
+    out = {"fields": fields, "flush": flush}
+
+    def touch(i):
+        if flush == "write":
+            scribble.fill_(i)
+        elif flush == "read":
+            scribble.sum()
     for k in faces:
         ft = ER.build_committed(recs[k])
         fS = ft.info()["size"] * fields
@@ -307,13 +318,13 @@ def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z"), flush=T
         for i in range(warmup + steps):
             a, b_, c_, d_ = (torch.cuda.Event(enable_timing=True) for _ in range(4))
             if flush:
-                scribble.fill_(i & 0xFF)
+                touch(2 * i)
             a.record(stream)
             c1.prepare_for_send(ft, fields, user.data_ptr())
             c1.pack([(fp, fS)])
             b_.record(stream)
             if flush:
-                scribble.fill_((i + 128) & 0xFF)
+                touch(2 * i + 1)
             c_.record(stream)
             c1.prepare_for_recv(ft, fields, user.data_ptr())
             c1.unpack([(fp, fS)])
@@ -625,7 +636,7 @@ def main():
         # (beyond the Infinity Cache), and at the bench's own 16 fields (launch-bound)
         result["faces"] = face_throughput(dev, args.face_fields, max(5, min(args.steps, 20)))
         result["faces_unflushed"] = face_throughput(dev, args.face_fields, max(5, min(args.steps, 20)),
-                                                    flush=False)
+                                                    flush=None)
         result["faces_at_bench_fields"] = face_throughput(dev, count, max(5, min(args.steps, 20)))
 
     if rank == 0 and base_sample is not None:

@@ -1582,7 +1582,7 @@ int ddt_tune(const char *key, long value)
     else if (k == "sorted")
         tuning().sorted = value;
     else if (k == "wt")
-        tuning().wt = value < 0 ? -1 : int(value > 2 ? 2 : value);
+        tuning().wt = value < 0 ? -1 : int(value > 3 ? 3 : value);
     else if (k == "hostdirect")
         tuning().hostdirect = int(value & 3);
     else if (k == "hd_grid")
@@ -1599,6 +1599,8 @@ int ddt_tune(const char *key, long value)
         tuning().stage_mb = value < 1 ? 1 : value;
     else if (k == "snt")
         tuning().snt = value < -1 ? -2 : (value < 0 ? -1 : (value >= 3 && value <= 5 ? int(value) : (value ? 1 : 0)));
+    else if (k == "stask")
+        tuning().stask = value < 0 ? 0 : value;
     else if (k == "spass")
         tuning().spass = value < 1 ? 1 : value;
     else if (k == "reset")

@@ -86,7 +86,8 @@ struct Item {
     int64_t w0, w1;         // LIST_VAR / FRAG: window [w0, w1) in packed-stream coordinates
     uint64_t nbytes;        // FRAG: bytes
     uint32_t wt;            // store policy: 1 = user-side stores (unpack) write through L2 (sc1);
-                            // 2 = every store of the launch sc1
+                            // 2 = every store of the launch sc1; 3 = user-side stores of an
+                            // unpack non-temporal (affine leaves)
     uint32_t slab;          // XCD task mapping (move_body): 0 round-robin, SLAB_FULL one
                             // contiguous slab per XCD, else runs of `slab` tasks per XCD;
                             // keeps sizeof(Item) == 512

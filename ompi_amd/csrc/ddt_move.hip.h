@@ -139,7 +139,8 @@ template <typename T, bool WT> __device__ __forceinline__ void st(T *p, T v)
 
 // NT: 0 plain; 1 non-temporal user-side loads (pack of sparse gathers, Item::nt == 1);
 // streaming leaves (Item::nt >= 2): 2 every load and store non-temporal, 3 loads only,
-// 4 stores only, 5 loads only and only when packing (the user-side rows).
+// 4 stores only, 5 loads only and only when packing (the user-side rows); 6 non-temporal
+// user-side stores of an unpack (isolated narrow blocks, Item::wt == 3).
 template <int U, int DIR, int ND, int NT, bool WT>
 __device__ __forceinline__ void run_affine(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
 {
@@ -170,10 +171,10 @@ __device__ __forceinline__ void run_affine(const Item *it, Bases bs, uint32_t ub
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (dst[k]) {
-                if constexpr (NT == 2 || NT == 4)
+                if constexpr (NT == 2 || NT == 4 || NT == 6)
                     __builtin_nontemporal_store(v[k], dst[k]);
                 else
-                    st<T, WT>(dst[k], v[k]);   // (nt scattered stores measured slower: 51 vs 18 us)
+                    st<T, WT>(dst[k], v[k]);
             }
     }
 }
@@ -377,7 +378,7 @@ __device__ __forceinline__ void dispatch_affine(const Item *it, Bases bs, uint32
 template <int DIR>
 __device__ __forceinline__ bool wt_stores(const Item *it)
 {
-    return it->wt == 2 || (DIR == 1 && it->wt == 1);
+    return it->wt == 2 || (DIR == 1 && (it->wt == 1 || it->wt == 3));
 }
 
 template <int DIR, bool WT>
@@ -441,6 +442,8 @@ __device__ __forceinline__ void move_task(const Item *__restrict__ items, uint32
                 else if (it->nt == 4) dispatch_affine_u<16, DIR, 4, false>(it, bs, uint32_t(ub), uint32_t(ue));
                 else if (it->nt == 5) dispatch_affine_u<16, DIR, 5, false>(it, bs, uint32_t(ub), uint32_t(ue));
                 else dispatch_affine_u<16, DIR, 2, false>(it, bs, uint32_t(ub), uint32_t(ue));
+            } else if (DIR == 1 && it->wt == 3) {
+                dispatch_affine<DIR, 6, false>(it, bs, uint32_t(ub), uint32_t(ue));
             } else if (wt_stores<DIR>(it)) {
                 if (DIR == 0 && it->nt == 1) dispatch_affine<DIR, 1, true>(it, bs, uint32_t(ub), uint32_t(ue));
                 else dispatch_affine<DIR, 0, true>(it, bs, uint32_t(ub), uint32_t(ue));

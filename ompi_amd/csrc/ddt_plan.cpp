@@ -435,13 +435,19 @@ bool use_nt(uint32_t U, uint64_t blen, const std::vector<LeafDim> &dims)
     return span > (192ull << 20);
 }
 
-// Write-through (sc1) stores: a scattered narrow store that misses L2 is sent on to the
-// memory side at once instead of allocating a partially dirty L2 line that is evicted
-// later.  Measured (scripts/ab.py, profiles/r1_wt_ab.log): the unpack-only loop of both x
-// faces 38.3 -> 29.1 us; neutral in pack+unpack pairs (the memory-side work is the same);
-// 3 % slower on dense partial-line leaves (cfg5 records), so auto = isolated small blocks
-// only: blen <= 8 and every stride >= 128 B (one block per L2 line).  Returns Item::wt.
-// DDT_WT / ddt_tune("wt"): 0 off, 1 every sparse leaf (U <= 8, blen <= 64), 2 all stores.
+// User-side store policy of an unpack (Item::wt).  An isolated narrow block (blen <= 8, every
+// stride >= 128 B: one block per line, the x faces) is a partial-line write that the memory
+// side completes with a read-modify-write.  With plain or write-through (sc1) stores the
+// partial lines linger dirty in the caches and the NEXT kernel pays their write-back: in the
+// bench's pack+unpack loop the halo pack took 100.6 us against 58.4 us packing alone
+// (profiles/r3_halo_split.jsonl).  Non-temporal stores (3) make the unpack pay its own
+// write-backs and cost less in total: pack+unpack step cfg2 176.4 -> 173.4 us, both x faces
+// 153.8 -> 143.5, cfg3 173.5 -> 167.9, its dim-2 face 149.9 -> 138.9, cfg1 unchanged
+// (profiles/r3_ab_wt.jsonl); bare kernels agree (scripts/ubench_xpair.hip: 153.7 -> 148.9).
+// Round 1 chose sc1 (1) from the unpack-only loop (38.3 -> 29.1 us), which hides the
+// write-backs.  Dense partial-line leaves (cfg5 records) keep plain stores.
+// DDT_WT / ddt_tune("wt"): -1 auto (3 for isolated narrow blocks), 0 off, 1 sc1 on every
+// sparse leaf (U <= 8, blen <= 64), 2 sc1 on all stores.
 uint32_t use_wt(uint32_t U, uint64_t blen, const std::vector<LeafDim> *dims)
 {
     const int force = tuning().wt;
@@ -455,7 +461,7 @@ uint32_t use_wt(uint32_t U, uint64_t blen, const std::vector<LeafDim> *dims)
     for (const LeafDim &d : *dims)
         if (d.cnt > 1 && absu(d.sstr) < 128)
             return 0;
-    return 1;
+    return 3;
 }
 
 // Cache policy of streaming leaves (16-byte units, blocks >= 256 B), Item::nt 2..5.  Measured
@@ -463,8 +469,11 @@ uint32_t use_wt(uint32_t U, uint64_t blen, const std::vector<LeafDim> *dims)
 // loop (profiles/r2_ab_y_policy.log, r2_ab_z_policy.log, r2_ab_stream_nt_modes.jsonl):
 //   z face (512 KiB planes): non-temporal LOADS only (3): 0.818 of 8 TB/s, against 0.686
 //     plain and 0.717 with non-temporal loads and stores (2, the first round-2 rule);
-//   y face (2 KiB rows): non-temporal loads in the PACK only (5): 0.757, plain 0.716;
-//     non-temporal loads in the unpack too cost it 82 -> 90 us, stores 0.680.
+//   y face (2 KiB rows): round 2 chose non-temporal loads in the PACK only (5): 0.757, plain
+//     0.716.  Round 3 measured with the cache cold and clean before every operation (1 GiB
+//     read between operations, profiles/r3_ab_stream_flush.jsonl): loads non-temporal in both
+//     directions (3) 0.795 against 0.778 for (5) (unpack 88.3 -> 84.6 us), and without the
+//     flush 0.785 against 0.789; stores non-temporal (1) 0.684.  So (3) for every stream.
 // The halo and cfg3 (x/dim-2 gathers in the same launch) move by <= 1 % either way.
 // ddt_tune("snt"): -1 this rule, -2 the first rule, 0 off, 1 / 3 / 4 / 5 forced.
 uint32_t use_snt(uint32_t U, uint64_t blen)   // Item::nt of a streaming leaf, 0 = none
@@ -476,7 +485,7 @@ uint32_t use_snt(uint32_t U, uint64_t blen)   // Item::nt of a streaming leaf, 0
         return force && blen >= 256 ? (force == 1 ? 2u : uint32_t(force)) : 0u;
     if (force == -2)  // round-2 first rule: long runs every access non-temporal
         return blen >= (64u << 10) ? 2u : 0u;
-    return blen >= (64u << 10) ? 3u : (blen >= 256 ? 5u : 0u);
+    return blen >= 256 ? 3u : 0u;
 }
 
 uint64_t units_per_task(uint32_t U)
@@ -735,6 +744,8 @@ void assign_tasks(std::vector<Item> &items)
                 const uint64_t pass = uint64_t(THREADS) * unroll_of(it.U) * it.U;
                 const bool sparse = it.upb * it.U <= 64;
                 cap = pass * uint64_t(sparse ? 1 : std::max<long>(1, tuning().spass));
+                if (!sparse && tuning().stask > 0)
+                    cap = uint64_t(tuning().stask);
             }
             const uint64_t b = tb < cap ? tb : cap;
             uint64_t u = b / it.U;

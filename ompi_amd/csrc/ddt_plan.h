@@ -27,6 +27,7 @@ struct Tuning {
     int snt = -1;         // streaming leaves (U = 16, blocks >= 256 B): non-temporal loads and
                           // stores; -1 auto (blocks >= 64 KiB), 0 off, 1 on
     long spass = 1;       // task of a streaming leaf: this many unrolled workgroup passes
+    long stask = 0;       // task of a streaming leaf in bytes (overrides spass; 0 = spass passes)
     int hostdirect = 3;   // pinned host iovecs moved by the kernel itself over PCIe (no HBM
                           // staging): bit 0 unpack, bit 1 pack (end to end)
     long stage_mb = 256;  // HBM staging buffer (one per convertor) for pageable host iovecs: the

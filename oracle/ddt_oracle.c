@@ -59,7 +59,17 @@ typedef struct ort_type {
     ort_run *runs;
     int64_t nruns, cap;
     int64_t *pref; /* packed offset of each run (built lazily at first pack) */
+    struct ort_group *grp; /* the runs as arithmetic progressions (built with pref) */
+    int64_t ngrp;
 } ort_type;
+
+/* Blocks of equal length at a constant stride (runs abutting in memory fused): the DATA entry
+ * (count n, blocklen len, extent stride) the reference's description would hold for them
+ * (opal_datatype_internal.h:130-136).  The movers walk these, not one run at a time, so the
+ * oracle's speed as the CPU baseline follows the reference's walk of opt_desc. */
+typedef struct ort_group {
+    int64_t disp, len, esize, stride, n, pref;
+} ort_group;
 
 /* OPAL predefined ids (opal/datatype/opal_datatype_internal.h:71-99) and the
  * LP64 x86-64 sizes of opal_datatype_module.c:143-180 (alignment = natural). */
@@ -87,6 +97,7 @@ void ort_free(ort_type *t)
         return;
     free(t->runs);
     free(t->pref);
+    free(t->grp);
     free(t);
 }
 
@@ -153,6 +164,8 @@ ort_type *ort_dup(const ort_type *o)
     memcpy(t->runs, o->runs, (size_t) o->nruns * sizeof(ort_run));
     t->cap = o->nruns;
     t->pref = NULL;
+    t->grp = NULL;
+    t->ngrp = 0;
     return t;
 }
 
@@ -608,13 +621,63 @@ static void ort_prefix(ort_type *t)
 {
     if (t->pref)
         return;
-    t->pref = (int64_t *) malloc((size_t) (t->nruns + 1) * sizeof(int64_t));
+    int64_t *pref = (int64_t *) malloc((size_t) (t->nruns + 1) * sizeof(int64_t));
     int64_t acc = 0;
     for (int64_t r = 0; r < t->nruns; r++) {
-        t->pref[r] = acc;
+        pref[r] = acc;
         acc += t->runs[r].len;
     }
-    t->pref[t->nruns] = acc;
+    pref[t->nruns] = acc;
+    /* group the runs into arithmetic progressions of equal blocks.  Byte movement does not
+     * care about element boundaries, so runs that abut in memory are fused first (the
+     * reference's optimizer fuses them the same way, opal_datatype_optimize.c:581-611: a
+     * struct{double,int[3]} record becomes one 20-byte block) */
+    ort_group *g = (ort_group *) malloc((size_t) (t->nruns ? t->nruns : 1) * sizeof(ort_group));
+    int64_t ng = 0;
+    for (int64_t r = 0; r < t->nruns;) {
+        ort_run x = t->runs[r];
+        const int64_t p0 = pref[r];
+        for (r++; r < t->nruns && t->runs[r].disp == x.disp + x.len; r++)
+            x.len += t->runs[r].len;
+        if (ng > 0) {
+            ort_group *c = &g[ng - 1];
+            if (c->len == x.len) {
+                if (c->n == 1) {
+                    c->stride = x.disp - c->disp;
+                    c->n = 2;
+                    continue;
+                }
+                if (x.disp == c->disp + c->n * c->stride) {
+                    c->n++;
+                    continue;
+                }
+            }
+        }
+        g[ng++] = (ort_group){x.disp, x.len, 1, 0, 1, p0};
+    }
+    t->grp = g;
+    t->ngrp = ng;
+    t->pref = pref;
+}
+
+/* Packed position p (< count*size): instance, group, block within the group, offset in it. */
+static void ort_locate_group(const ort_type *t, int64_t p, int64_t *inst, int64_t *grp, int64_t *blk,
+                             int64_t *within)
+{
+    *inst = p / t->size;
+    int64_t q = p - *inst * t->size;
+    int64_t lo = 0, hi = t->ngrp - 1;
+    while (lo < hi) { /* last group with pref <= q */
+        int64_t mid = (lo + hi + 1) / 2;
+        if (t->grp[mid].pref <= q)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    const ort_group *g = &t->grp[lo];
+    *grp = lo;
+    *blk = (q - g->pref) / g->len;
+    *within = (q - g->pref) % g->len;
 }
 
 /* Locate packed position p (< count*size): instance and run index, offset within run. */
@@ -733,26 +796,58 @@ static int64_t ort_xfer(ort_type *t, int64_t count, char *user, int64_t position
         return 0;
     ort_prefix(t);
     const int64_t ext = ort_extent(t);
-    int64_t inst, run, within, done = 0;
+    int64_t inst, gi, k, within, done = 0;
     if (len > total - position)
         len = total - position;
-    ort_locate(t, position, &inst, &run, &within);
+    ort_locate_group(t, position, &inst, &gi, &k, &within);
     while (done < len) {
-        const ort_run *r = &t->runs[run];
-        int64_t n = r->len - within;
-        if (n > len - done)
-            n = len - done;
-        char *u = user + inst * ext + r->disp + within;
-        if (dir)
-            memcpy(u, stream + done, (size_t) n);
-        else
-            memcpy(stream + done, u, (size_t) n);
-        done += n;
-        within += n;
-        if (within == r->len) {
+        const ort_group *g = &t->grp[gi];
+        char *ub = user + inst * ext + g->disp;
+        if (within == 0 && len - done >= (g->n - k) * g->len) {
+            /* whole blocks to the end of the group: the reference's block loop */
+            const int64_t bl = g->len, st = g->stride, m = g->n - k;
+            char *s = stream + done, *u = ub + k * st;
+#define ORT_BLOCKS(BL)                                                   \
+    do {                                                                 \
+        if (dir)                                                         \
+            for (int64_t j = 0; j < m; j++, s += (BL), u += st)          \
+                memcpy(u, s, (size_t) (BL));                             \
+        else                                                             \
+            for (int64_t j = 0; j < m; j++, s += (BL), u += st)          \
+                memcpy(s, u, (size_t) (BL));                             \
+    } while (0)
+            switch (bl) {   /* the element sizes get fixed-size (inlined) copies */
+            case 1: ORT_BLOCKS(1); break;
+            case 2: ORT_BLOCKS(2); break;
+            case 4: ORT_BLOCKS(4); break;
+            case 8: ORT_BLOCKS(8); break;
+            case 16: ORT_BLOCKS(16); break;
+            case 20: ORT_BLOCKS(20); break;
+            default: ORT_BLOCKS(bl); break;
+            }
+#undef ORT_BLOCKS
+            k = g->n;
+            done = s - stream;
+        } else {
+            int64_t n = g->len - within;
+            if (n > len - done)
+                n = len - done;
+            char *u = ub + k * g->stride + within;
+            if (dir)
+                memcpy(u, stream + done, (size_t) n);
+            else
+                memcpy(stream + done, u, (size_t) n);
+            done += n;
+            within += n;
+            if (within < g->len)
+                continue;
             within = 0;
-            if (++run == t->nruns) {
-                run = 0;
+            k++;
+        }
+        if (k == g->n) {
+            k = 0;
+            if (++gi == t->ngrp) {
+                gi = 0;
                 inst++;
             }
         }

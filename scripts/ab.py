@@ -33,6 +33,9 @@ def main():
                          "(fields, faces and rows reversed; xx and cfg2), to test Infinity Cache reuse")
     ap.add_argument("--prewarm", type=float, default=0.0, help="seconds of HBM copies first")
     ap.add_argument("--count", type=int, default=0, help="override the instance (field) count")
+    ap.add_argument("--flush", default="none", choices=["read", "write", "none"],
+                    help="touch a 1 GiB scribble before each operation, outside the events "
+                         "(bench.face_throughput's protocol)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     faces = bench.face_recipes()
@@ -86,6 +89,14 @@ def main():
             b.copy_(a)
             torch.cuda.synchronize()
         del a, b
+    scribble = torch.full((1 << 27,), 3, dtype=torch.int64, device=dev) if args.flush != "none" else None
+
+    def touch(i):
+        if args.flush == "write":
+            scribble.fill_(i)
+        elif args.flush == "read":
+            scribble.sum()
+
     res = {json.dumps(v): {"pack": [], "unpack": []} for v in variants}
     for _ in range(args.rounds):
         for v in variants:
@@ -102,25 +113,28 @@ def main():
             cu.set_stream(st, True)
             evs = []
             for i in range(args.steps + 3):
-                a, b, c = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                a, b, b2, c = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+                touch(2 * i)
                 a.record()
                 if args.mode != "unpack":
                     cp.prepare_for_send(dt, count, uptr)
                     cp.pack([(packed, S)])
                 b.record()
+                touch(2 * i + 1)
+                b2.record()
                 if args.mode != "pack":
                     cu.prepare_for_recv(udt, ucount, uptr)
                     cu.unpack([(packed, S)])
                 c.record()
                 if i >= 3:
-                    evs.append((a, b, c))
+                    evs.append((a, b, b2, c))
             torch.cuda.synchronize()
             r = res[json.dumps(v)]
-            r["pack"].append(statistics.median(a.elapsed_time(b) for a, b, _ in evs) * 1e3)
-            r["unpack"].append(statistics.median(b.elapsed_time(c) for _, b, c in evs) * 1e3)
+            r["pack"].append(statistics.median(a.elapsed_time(b) for a, b, _, _ in evs) * 1e3)
+            r["unpack"].append(statistics.median(b2.elapsed_time(c) for _, _, b2, c in evs) * 1e3)
     for k, r in res.items():
         p, u = statistics.median(r["pack"]), statistics.median(r["unpack"])
-        print(json.dumps({"config": args.config, "variant": json.loads(k), "pack_us": round(p, 1),
+        print(json.dumps({"config": args.config, "flush": args.flush, "variant": json.loads(k), "pack_us": round(p, 1),
                           "unpack_us": round(u, 1), "step_us": round(p + u, 1),
                           "frac": round(4 * S / ((p + u) * 1e-6) / 8e12, 4),
                           "pack_rounds": [round(x, 1) for x in r["pack"]],

@@ -21,10 +21,11 @@ def main():
     ap.add_argument("--fields", type=int, default=512)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--faces", default="x,y,z")
-    ap.add_argument("--no-flush", action="store_true", help="skip the 1 GiB scribble between operations")
+    ap.add_argument("--flush", default="read", choices=["read", "write", "none"],
+                    help="1 GiB scribble touched between operations (bench.face_throughput)")
     args = ap.parse_args()
     r = bench.face_throughput(torch.device("cuda:0"), args.fields, args.steps,
-                              faces=tuple(args.faces.split(",")), flush=not args.no_flush)
+                              faces=tuple(args.faces.split(",")), flush=None if args.flush == "none" else args.flush)
     print(json.dumps(r), flush=True)
 
 
