@@ -286,6 +286,16 @@ int ddt_type_engine_info(const ddt_datatype_t *type, int64_t *out4);
  * retirement events, sets held for captured graphs, HIP device of the plan (-1 before first
  * use)].  Sets are keyed by the request's shape and pointer alignment, not by buffer address. */
 int ddt_type_cache_info(const ddt_datatype_t *type, int64_t *out4);
+/* Device memory of the engine's own metadata (descriptor sets, index lists, address-ordered
+ * tables, staging and scratch) is cached, not freed: destroying a datatype never waits for
+ * the device nor calls hipFree (which synchronises the whole device and breaks another
+ * thread's stream capture).  Its memory is reused once the streams that launched its work
+ * pass fence events recorded at destruction; memory a captured graph may read is kept.
+ * ddt_trim (torch.cuda.empty_cache's analogue) synchronises the device and returns every
+ * cached block to HIP.  ddt_pool_info: out6 = [free blocks, free bytes, fenced blocks, fenced
+ * bytes, blocks kept for graphs, blocks in use]. */
+int ddt_trim(void);
+int ddt_pool_info(int64_t *out6);
 /* ---- introspection for the CPU test-suite (no data movement; never used by pack/unpack) ----
  * ddt_type_plan_leaves: serialises the plan's leaf streams as int64 records
  *   [kind, blen, src_off, dst_off, ndim, list_leaf_index, (cnt, sstr, dstr) x ndim] and returns

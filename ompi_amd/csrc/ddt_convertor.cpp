@@ -20,6 +20,7 @@
 #include "ddt_core.h"
 #include "ddt_hip.h"
 #include "ddt_plan.h"
+#include "ddt_pool.h"
 
 using namespace ddt;
 
@@ -163,8 +164,13 @@ void reap(Plan &P, bool block)   // P.mu held
 }
 
 // Device memory for `bytes` of descriptors: the smallest spare block that fits, else new.
-Item *take_items_memory(Plan &P, size_t bytes)   // P.mu held
+// Retired sets are reaped here, when memory is wanted, and not on every new set: the event
+// queries of a reap (like any allocation or upload) would invalidate a global-mode stream
+// capture running in another thread (scripts/probe_capture.cpp), while an inline set -- a
+// new window shape of a small type -- needs no HIP call but its launch.
+Item *take_items_memory(Plan &P, size_t bytes, bool block)   // P.mu held
 {
+    reap(P, block);
     size_t best = P.spare.size();
     for (size_t i = 0; i < P.spare.size(); ++i)
         if (P.spare[i].bytes >= bytes && (best == P.spare.size() || P.spare[i].bytes < P.spare[best].bytes))
@@ -174,8 +180,7 @@ Item *take_items_memory(Plan &P, size_t bytes)   // P.mu held
         P.spare.erase(P.spare.begin() + long(best));
         return d;
     }
-    Item *d = nullptr;
-    return hipMalloc((void **) &d, bytes) == hipSuccess ? d : nullptr;
+    return static_cast<Item *>(pool_alloc(bytes));
 }
 
 // A retired set (still in the graveyard) that a captured graph now holds: pinned for the
@@ -223,6 +228,23 @@ void retire(Plan &P, const std::shared_ptr<ItemSet> &S)   // P.mu held
         r.events.push_back(e);
     }
     P.graveyard.push_back(std::move(r));
+}
+
+// Every stream that launched work reading a plan's device memory: the plan's destruction
+// fences its memory behind them (~Plan, ddt_pool.h).  A launch inside a capture marks the
+// plan: a graph may read its memory after the datatype is gone.
+void note_stream_locked(Plan &P, hipStream_t stream)   // P.mu held
+{
+    if (std::find(P.streams.begin(), P.streams.end(), stream) == P.streams.end())
+        P.streams.push_back(stream);
+    if (capturing(stream))
+        P.captured = true;
+}
+
+void note_stream(Plan &P, hipStream_t stream)
+{
+    std::lock_guard<std::mutex> g(P.mu);
+    note_stream_locked(P, stream);
 }
 
 // Find or build the descriptor set of one launch and run it on `stream`.
@@ -281,6 +303,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         if (SL && count > 1 && uint64_t(t->extent() < 0 ? -t->extent() : t->extent()) % SL->esz != 0)
             SL = nullptr;
         if (SL) {
+            note_stream(P, stream);
             const Leaf &L = P.leaves[0];
             for (uint64_t i = 0; i < count; ++i) {
                 uint8_t *u = reinterpret_cast<uint8_t *>(user + uint64_t(L.list_shift) + uint64_t(P.dev[0].disp_base)
@@ -330,7 +353,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             size_t bytes = S->items.size() * sizeof(Item);
             {
                 std::lock_guard<std::mutex> g(P.mu);
-                S->d_items = take_items_memory(P, bytes);
+                S->d_items = take_items_memory(P, bytes, !capturing(stream));
             }
             if (!S->d_items)
                 return fail(DDT_ERR_OUT_OF_RESOURCE, "descriptor memory");
@@ -338,7 +361,6 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             if (e != hipSuccess)
                 return fail(DDT_ERR_HIP, std::string("item upload: ") + hipGetErrorString(e));
         }
-        const bool block = !capturing(stream);
         std::lock_guard<std::mutex> g(P.mu);
         ++S->inflight;
         P.cache.insert(P.cache.begin(), S);
@@ -346,7 +368,6 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             retire(P, P.cache.back());
             P.cache.pop_back();
         }
-        reap(P, block);
     }
     // The launch is enqueued outside the plan lock, so another thread may evict the set
     // meanwhile.  This call holds it (`inflight`, taken with the lookup) so its memory is not
@@ -388,7 +409,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         std::lock_guard<std::mutex> g(P.mu);
         if (S->inline_ok && !S->retired && ++S->uses >= 2 && !S->d_items && tuning().ptr) {
             size_t bytes = S->items.size() * sizeof(Item);
-            Item *d = take_items_memory(P, bytes);
+            Item *d = take_items_memory(P, bytes, !capturing(stream));
             if (d) {
                 if (upload(d, S->items.data(), bytes) == hipSuccess)
                     S->d_items = d;
@@ -406,9 +427,12 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             }
             if (std::find(S->streams.begin(), S->streams.end(), stream) == S->streams.end())
                 S->streams.push_back(stream);
+            note_stream_locked(P, stream);
             hold.by_pointer = true;
         }
     }
+    if (!d_items && S->has_lists)
+        note_stream(P, stream);   // an inline launch of index lists reads the plan's lists
     if (!d_items)
         HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, ubase, pbase, stream, grid_cap));
     else
@@ -445,20 +469,32 @@ struct ddt_convertor {
     hipEvent_t ev_chunk[2] = {nullptr, nullptr};
     hipEvent_t ev_free = nullptr;
     bool rec_free = false;
+    // No host wait: a convertor without host staging holds no device memory, and the staging
+    // buffers of one that has it go to the engine's pool behind fences on the user stream and
+    // the copy stream (their last readers), like a destroyed plan's (ddt_pool.h).  So an
+    // OBJ_RELEASE of a convertor never stalls, even during another thread's stream capture.
     ~ddt_convertor()
     {
-        if (stream)
-            (void) hipStreamSynchronize(stream);
-        if (copy_stream) {
-            (void) hipStreamSynchronize(copy_stream);
-            (void) hipStreamDestroy(copy_stream);
+        if (stage || !outgrown.empty()) {
+            std::vector<void *> blocks(outgrown);
+            if (stage)
+                blocks.push_back(stage);
+            std::vector<hipEvent_t> fences;
+            bool unknown = false;
+            std::vector<hipStream_t> ss{stream};
+            if (copy_stream)
+                ss.push_back(copy_stream);
+            if (pool_fences(ss, fences, unknown)) {
+                pool_release(blocks, fences, unknown);
+            } else {   // a capturing stream: its graph may read the staging buffer
+                for (hipEvent_t e : fences)
+                    (void) hipEventDestroy(e);
+                for (void *p : blocks)
+                    pool_keep(p);
+            }
         }
-        if (ev_free && rec_free)
-            (void) hipEventSynchronize(ev_free);
-        if (stage)
-            (void) hipFree(stage);
-        for (void *p : outgrown)
-            (void) hipFree(p);
+        if (copy_stream)
+            (void) hipStreamDestroy(copy_stream);   // queued copies still complete
         for (hipEvent_t e : {ev_chunk[0], ev_chunk[1], ev_free})
             if (e)
                 (void) hipEventDestroy(e);
@@ -476,8 +512,9 @@ struct ddt_convertor {
         if (stage_size >= want)
             return DDT_SUCCESS;
         want = std::max(want, std::min(cap, stage_size * 2));
-        void *p = nullptr;
-        HIPCHK(hipMalloc(&p, want));
+        void *p = pool_alloc(want);
+        if (!p)
+            return fail(DDT_ERR_OUT_OF_RESOURCE, "staging buffer");
         if (stage)
             outgrown.push_back(stage);   // may still be read by queued work: kept until destruction
         stage = p;
@@ -1070,9 +1107,10 @@ namespace {
 // call of the thread finds it free).  Round 1 allocated per call, round 2 first with
 // stream-ordered allocations, whose pool returns the memory at every synchronisation: a
 // 16 MiB MPI_Pack_external spent ~300 us of its 357 in allocation (profiles/r2_ext_bench.jsonl).
-// Only buffers up to kKeepBytes are kept for reuse: a larger request (a multi-GiB message,
-// where one hipMalloc is small against the transfer) gets its own allocation, freed when the
-// call ends (hipFree waits for the device), so a thread does not pin that much HBM for good.
+// Only buffers up to kKeepBytes are kept by the thread: a larger request (a multi-GiB message)
+// gets a block of its own for the call, back to the engine's pool when the call ends (the
+// call has synchronised its stream), so a thread does not hold that much HBM for good;
+// ddt_trim() returns pooled memory to HIP.
 constexpr size_t kKeepBytes = size_t(256) << 20;
 struct DevBuf {
     void *p = nullptr;
@@ -1081,24 +1119,20 @@ struct DevBuf {
     explicit DevBuf(int s) : slot(s) {}
     DevBuf(const DevBuf &) = delete;
     DevBuf &operator=(const DevBuf &) = delete;
-    ~DevBuf()
-    {
-        if (own)
-            (void) hipFree(own);
-    }
+    ~DevBuf() { pool_free(own); }
     hipError_t alloc(size_t n)
     {
         if (n > kKeepBytes) {
-            const hipError_t e = hipMalloc(&own, n);
+            own = pool_alloc(n);
             p = own;
-            return e;
+            return own ? hipSuccess : hipErrorOutOfMemory;
         }
         struct Cache {
             std::map<std::pair<int, int>, std::pair<void *, size_t>> bufs;   // (device, slot)
             ~Cache()
             {
                 for (auto &kv : bufs)
-                    (void) hipFree(kv.second.first);
+                    pool_free(kv.second.first);
             }
         };
         thread_local Cache cache;
@@ -1108,12 +1142,11 @@ struct DevBuf {
             return e;
         auto &b = cache.bufs[{dev, slot}];
         if (b.second < n || !b.first) {
-            if (b.first)
-                (void) hipFree(b.first);
+            pool_free(b.first);   // the thread's previous call synchronised its stream
             b = {nullptr, 0};
             const size_t want = std::max<size_t>(n, 1u << 20);
-            if ((e = hipMalloc(&b.first, want)) != hipSuccess)
-                return e;
+            if (!(b.first = pool_alloc(want)))
+                return hipErrorOutOfMemory;
             b.second = want;
         }
         p = b.first;
@@ -1556,6 +1589,16 @@ int ddt_selftest(void)
             return 2;
     }
     return 0;
+}
+
+int ddt_trim(void) { return pool_trim(); }
+
+int ddt_pool_info(int64_t *out6)
+{
+    if (!out6)
+        return DDT_ERR_BAD_PARAM;
+    pool_stats(out6);
+    return DDT_SUCCESS;
 }
 
 int ddt_tune(const char *key, long value)

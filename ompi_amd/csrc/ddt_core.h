@@ -128,7 +128,7 @@ struct ItemSet {
 };
 
 // Device memory of retired descriptor sets, kept for reuse (hipFree implies a device-wide
-// synchronisation; buffers are released only with the plan).
+// synchronisation; a destroyed plan hands its buffers to the pool, ddt_pool.h).
 struct DevBlock {
     void *p = nullptr;
     size_t bytes = 0;
@@ -154,6 +154,8 @@ struct Plan {
     std::vector<Retired> graveyard;                   // evicted, freed once their events pass
     std::vector<std::shared_ptr<ItemSet>> pinned;     // evicted but held by captured graphs
     std::vector<DevBlock> spare;                      // reusable descriptor memory (recycled)
+    std::vector<hipStream_t> streams;                 // every stream that launched this plan's work
+    bool captured = false;                            // a launch was enqueued inside a capture
     // address-ordered plan of a one-leaf single-element index list (ddt_sorted.hip):
     // 0 = not tried yet, 1 = built, -1 = not applicable
     int sorted_state = 0;

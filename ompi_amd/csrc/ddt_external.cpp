@@ -27,6 +27,7 @@
 #include "ddt_core.h"
 #include "ddt_hip.h"
 #include "ddt_plan.h"
+#include "ddt_pool.h"
 
 namespace ddt {
 
@@ -132,12 +133,22 @@ Flat flatten(const std::vector<Node> &nodes)
 
 ExtPlan::~ExtPlan()
 {
-    if (d_segs || d_runs)
-        (void) hipDeviceSynchronize();
-    if (d_segs)
-        (void) hipFree(d_segs);
-    if (d_runs)
-        (void) hipFree(d_runs);
+    // external32 calls run on the default stream and synchronise it before returning; the
+    // tables still go to the pool behind a fence on that stream (no device-wide wait, no
+    // hipFree: see ddt_pool.h)
+    if (!d_segs && !d_runs)
+        return;
+    std::vector<void *> blocks{d_segs, d_runs};
+    std::vector<hipEvent_t> fences;
+    bool unknown = false;
+    if (pool_fences({hipStream_t(nullptr)}, fences, unknown)) {
+        pool_release(blocks, fences, unknown);
+    } else {
+        for (hipEvent_t e : fences)
+            (void) hipEventDestroy(e);
+        for (void *p : blocks)
+            pool_keep(p);
+    }
 }
 
 std::shared_ptr<ExtPlan> get_ext_plan(ddt_datatype *t)
@@ -229,11 +240,11 @@ int ext_upload(ExtPlan &X)
     const size_t sb = X.segs.size() * sizeof(ConvSeg), rb = X.runs.size() * sizeof(ConvRun);
     ConvSeg *ds = nullptr;
     ConvRun *dr = nullptr;
-    if (hipMalloc((void **) &ds, sb) != hipSuccess || hipMalloc((void **) &dr, rb) != hipSuccess
+    if (!(ds = static_cast<ConvSeg *>(pool_alloc(sb))) || !(dr = static_cast<ConvRun *>(pool_alloc(rb)))
         || upload(ds, X.segs.data(), sb) != hipSuccess
         || upload(dr, X.runs.data(), rb) != hipSuccess) {
-        if (ds) (void) hipFree(ds);
-        if (dr) (void) hipFree(dr);
+        pool_free(ds);
+        pool_free(dr);
         return DDT_ERR_HIP;
     }
     X.d_runs = dr;

@@ -17,6 +17,7 @@
 
 #include "ddt_core.h"
 #include "ddt_plan.h"
+#include "ddt_pool.h"
 
 namespace ddt {
 
@@ -40,7 +41,7 @@ Tuning &tuning()
 // Host -> device uploads of plan metadata run on a library-private non-blocking stream,
 // one per device: they never synchronise with (or invalidate a capture on) the caller's
 // stream, so a plan's first use may sit inside a HIP-graph capture.
-hipError_t upload(void *dst, const void *src, size_t n)
+hipError_t private_stream(hipStream_t *out)
 {
     static std::mutex mu;
     static std::map<int, hipStream_t> streams;
@@ -48,53 +49,92 @@ hipError_t upload(void *dst, const void *src, size_t n)
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess)
         return e;
-    hipStream_t s = nullptr;
-    {
-        std::lock_guard<std::mutex> g(mu);
-        auto it = streams.find(dev);
-        if (it == streams.end()) {
-            if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess)
-                return e;
-            streams[dev] = s;
-        } else {
-            s = it->second;
-        }
+    std::lock_guard<std::mutex> g(mu);
+    auto it = streams.find(dev);
+    if (it == streams.end()) {
+        hipStream_t s = nullptr;
+        if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess)
+            return e;
+        it = streams.emplace(dev, s).first;
     }
+    *out = it->second;
+    return hipSuccess;
+}
+
+hipError_t upload(void *dst, const void *src, size_t n)
+{
+    hipStream_t s = nullptr;
+    hipError_t e = private_stream(&s);
+    if (e != hipSuccess)
+        return e;
     if ((e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s)) != hipSuccess)
         return e;
     return hipStreamSynchronize(s);
 }
 
+// The datatype is being destroyed (the reference frees its description at once,
+// opal_datatype_destruct, opal_datatype_create.c:61-91) but launches that read these
+// descriptors, lists or tables may still be queued.  No device-wide wait and no hipFree
+// (either stalls every stream of the device, and fails inside another thread's capture):
+// the memory goes to the pool behind one event per stream that launched this plan's work,
+// and is reused once they pass.  Memory a captured graph may read (a launch was captured,
+// or a launching stream is capturing now) is kept for good.
 Plan::~Plan()
 {
-    // launches that read these descriptors or lists may still be in flight (the datatype is
-    // being destroyed: the reference frees its description at once, opal_datatype_destruct)
-    if (!cache.empty() || !graveyard.empty() || !pinned.empty() || dev_ready)
-        (void) hipDeviceSynchronize();
-    cache.clear();
-    for (Retired &r : graveyard)
+    std::vector<void *> blocks;
+    auto take_set = [&](ItemSet &S) {
+        for (hipEvent_t e : S.late)
+            (void) hipEventDestroy(e);
+        S.late.clear();
+        if (!S.d_items)
+            return;
+        if (S.pinned)
+            pool_keep(S.d_items);
+        else
+            blocks.push_back(S.d_items);
+        S.d_items = nullptr;
+    };
+    for (auto &S : cache)
+        take_set(*S);
+    for (Retired &r : graveyard) {
         for (hipEvent_t e : r.events)
             (void) hipEventDestroy(e);
+        take_set(*r.set);
+    }
+    for (auto &S : pinned)
+        take_set(*S);
+    for (DevBlock &b : spare)
+        pool_free(b.p);   // recycled: its readers have passed
+    for (DevList &d : dev)
+        for (void *p : {d.disp, (void *) d.len, (void *) d.goff})
+            if (p)
+                blocks.push_back(p);
+    if (sorted)
+        sorted->take_blocks(blocks);
+    std::vector<hipEvent_t> fences;
+    bool unknown = false;
+    if (captured || !pool_fences(streams, fences, unknown)) {
+        for (hipEvent_t e : fences)
+            (void) hipEventDestroy(e);
+        for (void *p : blocks)
+            pool_keep(p);
+    } else {
+        pool_release(blocks, fences, unknown);
+    }
+    cache.clear();
     graveyard.clear();
     pinned.clear();
-    for (DevBlock &b : spare)
-        (void) hipFree(b.p);
     spare.clear();
-    for (DevList &d : dev) {
-        if (d.disp) (void) hipFree(d.disp);
-        if (d.len) (void) hipFree(d.len);
-        if (d.goff) (void) hipFree(d.goff);
-    }
 }
 
 ItemSet::~ItemSet()
 {
     for (hipEvent_t e : late)
         (void) hipEventDestroy(e);
-    // a retired set's memory went back to its plan's spare list (reap); a live set is freed
-    // only with its plan, after the plan's device synchronisation
+    // a launched set's memory is handed to the pool by its plan (retirement or ~Plan); a set
+    // still holding memory here never ran
     if (d_items)
-        (void) hipFree(d_items);
+        pool_free(d_items);
 }
 
 namespace {
@@ -231,13 +271,13 @@ void ensure_device_lists(Plan &P)
             std::vector<int32_t> tmp(n);
             for (size_t k = 0; k < n; ++k)
                 tmp[k] = int32_t(X.disp[k] - D.disp_base);
-            if (hipMalloc(&D.disp, n * 4) != hipSuccess)
+            if (!(D.disp = pool_alloc(n * 4)))
                 throw std::runtime_error("hipMalloc(list disp)");
             if (upload(D.disp, tmp.data(), n * 4) != hipSuccess)
                 throw std::runtime_error("hipMemcpy(list disp)");
             P.dev_bytes += n * 4;
         } else {
-            if (hipMalloc(&D.disp, n * 8) != hipSuccess)
+            if (!(D.disp = pool_alloc(n * 8)))
                 throw std::runtime_error("hipMalloc(list disp)");
             if (upload(D.disp, X.disp.data(), n * 8) != hipSuccess)
                 throw std::runtime_error("hipMemcpy(list disp)");
@@ -254,8 +294,8 @@ void ensure_device_lists(Plan &P)
             std::vector<uint64_t> goff(ng);
             for (size_t gi = 0; gi < ng; ++gi)
                 goff[gi] = X.poff[gi * 64];
-            if (hipMalloc((void **) &D.len, n * 4) != hipSuccess
-                || hipMalloc((void **) &D.goff, ng * 8) != hipSuccess)
+            if (!(D.len = static_cast<uint32_t *>(pool_alloc(n * 4)))
+                || !(D.goff = static_cast<uint64_t *>(pool_alloc(ng * 8))))
                 throw std::runtime_error("hipMalloc(list len)");
             if (upload(D.len, len.data(), n * 4) != hipSuccess
                 || upload(D.goff, goff.data(), ng * 8) != hipSuccess)
@@ -315,11 +355,17 @@ SortedList *sorted_plan(const ddt_datatype *t, Plan &P, uint64_t user, hipStream
         return nullptr;   // this buffer only: the typed element loads need alignment
     std::lock_guard<std::mutex> g_(P.mu);
     if (P.sorted_state == 0) {
-        // the build allocates and synchronises: never inside a stream capture (a graph
-        // captured before the first eager use keeps the per-block kernel)
+        // the build allocates and waits for its own stream: never while the caller's stream
+        // captures (a graph captured before the first eager use keeps the per-block kernel)
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
             return nullptr;
+        // the tables are built from the plan's own index list on the library-private stream:
+        // the caller's stream is neither drained nor waited on, and the host sees the tables
+        // complete when build() returns
+        hipStream_t bs = nullptr;
+        if (private_stream(&bs) != hipSuccess)
+            throw std::runtime_error("sorted list: private stream");
         // element displacements (bytes, relative to the list minimum): the device list
         // itself when every block is one element, else expanded here
         const int32_t *ed = static_cast<const int32_t *>(D.disp);
@@ -333,9 +379,8 @@ SortedList *sorted_plan(const ddt_datatype *t, Plan &P, uint64_t user, hipStream
                 for (uint64_t q = 0; q < len; q += esz)
                     h[e++] = int32_t(b + int64_t(q));
             }
-            if (hipMalloc(&tmp, ne * 4 + 16) != hipSuccess
-                || upload(tmp, h.data(), ne * 4) != hipSuccess) {
-                if (tmp) (void) hipFree(tmp);
+            if (!(tmp = pool_alloc(ne * 4 + 16)) || upload(tmp, h.data(), ne * 4) != hipSuccess) {
+                pool_free(tmp);
                 throw std::runtime_error("sorted list: element displacement upload");
             }
             ed = static_cast<const int32_t *>(tmp);
@@ -343,12 +388,12 @@ SortedList *sorted_plan(const ddt_datatype *t, Plan &P, uint64_t user, hipStream
         auto S = std::make_unique<SortedList>();
         bool ok = false;
         try {
-            ok = S->build(ed, uint32_t(ne), uint32_t(esz), span_elems, uint32_t(segb), stream);
+            ok = S->build(ed, uint32_t(ne), uint32_t(esz), span_elems, uint32_t(segb), bs);
         } catch (...) {
-            if (tmp) (void) hipFree(tmp);
+            pool_free(tmp);   // build() has drained its stream before throwing
             throw;
         }
-        if (tmp) (void) hipFree(tmp);
+        pool_free(tmp);
         if (ok) {
             P.dev_bytes += S->dev_bytes;
             P.sorted = std::move(S);

@@ -43,6 +43,8 @@ struct Tuning {
 Tuning &tuning();
 // Synchronous host -> device copy on a library-private stream (capture-safe).
 hipError_t upload(void *dst, const void *src, size_t n);
+// The library-private non-blocking stream of the current device (uploads, table builds).
+hipError_t private_stream(hipStream_t *out);
 
 void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t user, uint64_t pk,
                  uint64_t W0, uint64_t W1, bool same_layout, std::vector<Item> &items);

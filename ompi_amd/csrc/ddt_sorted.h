@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <mutex>
+#include <vector>
 
 #include <hip/hip_runtime.h>
 
@@ -34,6 +35,8 @@ struct SortedList {
     bool used = false;
     std::mutex mu;               // run() from several host threads: one launch sequence at a time
     ~SortedList();
+    // hand the tables and U to `out` (the plan releases them behind its stream fences)
+    void take_blocks(std::vector<void *> &out);
     bool build(const int32_t *disp, uint32_t n, uint32_t esz, uint64_t span_elems, uint32_t segb,
                hipStream_t stream);
     // pol: access policy bits (POL_* in ddt_sorted.hip; ddt_tune "spol")

@@ -34,6 +34,7 @@
 #include <string>
 
 #include "ddt_sorted.h"
+#include "ddt_pool.h"
 
 namespace ddt {
 
@@ -503,22 +504,33 @@ uint32_t grid_for(uint64_t n, uint32_t threads)
 template <typename T>
 T *dalloc(size_t n, uint64_t &bytes)
 {
-    void *p = nullptr;
-    HK(hipMalloc(&p, n * sizeof(T) + 16));
+    void *p = pool_alloc(n * sizeof(T) + 16);
+    if (!p)
+        throw std::runtime_error("sorted list: out of device memory");
     bytes += n * sizeof(T);
     return static_cast<T *>(p);
 }
 
 }  // namespace
 
+void SortedList::take_blocks(std::vector<void *> &out)
+{
+    for (void **p : {(void **) &A, (void **) &A16, (void **) &Abase, (void **) &SL, (void **) &off16,
+                     (void **) &ub, (void **) &bstart, (void **) &upos, &U})
+        if (*p) {
+            out.push_back(*p);
+            *p = nullptr;
+        }
+}
+
 SortedList::~SortedList()
 {
-    if (done)
-        (void) hipEventSynchronize(done);
-    for (void *p : {(void *) A, (void *) A16, (void *) Abase, (void *) SL, (void *) off16, (void *) ub,
-                    (void *) bstart, (void *) upos, U})
-        if (p)
-            (void) hipFree(p);
+    std::vector<void *> left;
+    take_blocks(left);
+    if (!left.empty() && done)
+        (void) hipEventSynchronize(done);   // only a plan that was never released to the pool
+    for (void *p : left)
+        pool_free(p);
     if (done)
         (void) hipEventDestroy(done);
 }
@@ -545,11 +557,10 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
     uint32_t *bm = nullptr, *wpre = nullptr, *dup = nullptr, *cnt = nullptr, *padT = nullptr, *ubT = nullptr;
     uint16_t *rr = nullptr;
     void *scan_tmp = nullptr;
-    auto release = [&] {
+    auto release = [&] {   // the build's stream has been drained before every call
         for (void *p : {(void *) bm, (void *) wpre, (void *) dup, (void *) cnt, (void *) padT, (void *) ubT,
                         (void *) rr, scan_tmp})
-            if (p)
-                (void) hipFree(p);
+            pool_free(p);
     };
     try {
         bm = dalloc<uint32_t>(words, tmp_bytes);
@@ -567,7 +578,8 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
         size_t tb = 0, tb2 = 0;
         HK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, wpre, wpre, int(words), stream));
         HK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, padT, ubT, int(runs + 1), stream));
-        HK(hipMalloc(&scan_tmp, std::max(tb, tb2) + 16));
+        if (!(scan_tmp = pool_alloc(std::max(tb, tb2) + 16)))
+            throw std::runtime_error("sorted list: out of device memory");
         HK(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, wpre, wpre, int(words), stream));
         uint32_t hdup = 0;
         HK(hipMemcpyAsync(&hdup, dup, 4, hipMemcpyDeviceToHost, stream));
@@ -594,12 +606,12 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
             HK(hipMemcpyAsync(&span, dup, 4, hipMemcpyDeviceToHost, stream));
             HK(hipStreamSynchronize(stream));
             if (span == 0) {   // every d <= 0xFFFF
-                HK(hipFree(A));
+                pool_free(A);
                 A = nullptr;
                 bytes += cb - uint64_t(n) * 4;
             } else {
-                HK(hipFree(A16));
-                HK(hipFree(Abase));
+                pool_free(A16);
+                pool_free(Abase);
                 A16 = nullptr;
                 Abase = nullptr;
             }
@@ -623,7 +635,12 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
         HK(hipStreamSynchronize(stream));
         dev_bytes = bytes;
     } catch (...) {
+        (void) hipStreamSynchronize(stream);   // queued build kernels may still use the temporaries
         release();
+        std::vector<void *> mine;
+        take_blocks(mine);
+        for (void *p : mine)
+            pool_free(p);
         throw;
     }
     release();
