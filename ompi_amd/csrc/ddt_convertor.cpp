@@ -341,8 +341,11 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         S->ntasks = total_tasks(S->items);
         for (Item &it : S->items)
             it.slab = use_slab(it) ? (tuning().xchunk > 0 ? uint32_t(tuning().xchunk) : SLAB_FULL) : 0;
-        for (const Item &it : S->items)
+        S->all_dense = !S->items.empty();
+        for (const Item &it : S->items) {
             S->has_lists = S->has_lists || it.kind == ITEM_LIST_UNI || it.kind == ITEM_LIST_VAR;
+            S->all_dense = S->all_dense && it.kind == ITEM_AFFINE && it.nbytes && !it.idx64;
+        }
         if (S->items.size() <= INLINE_ITEMS) {
             // small sets travel in the kernel-argument segment: no device allocation
             S->inline_ok = true;
@@ -434,10 +437,11 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     if (!d_items && S->has_lists)
         note_stream(P, stream);   // an inline launch of index lists reads the plan's lists
     if (!d_items)
-        HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, ubase, pbase, stream, grid_cap));
+        HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, ubase, pbase, stream, grid_cap,
+                                  S->all_dense));
     else
         HIPCHK(launch_move(d_items, uint32_t(S->items.size()), S->ntasks, dir, S->has_lists, ubase, pbase,
-                           stream, grid_cap));
+                           stream, grid_cap, S->all_dense));
     return DDT_SUCCESS;
 }
 
@@ -1642,6 +1646,8 @@ int ddt_tune(const char *key, long value)
         tuning().stage_mb = value < 1 ? 1 : value;
     else if (k == "snt")
         tuning().snt = value < -1 ? -2 : (value < 0 ? -1 : (value >= 3 && value <= 5 ? int(value) : (value ? 1 : 0)));
+    else if (k == "dense")
+        tuning().dense = value < 0 ? -1 : int(value);
     else if (k == "stask")
         tuning().stask = value < 0 ? 0 : value;
     else if (k == "spass")

@@ -111,6 +111,7 @@ struct ItemSet {
     Item *d_items = nullptr;
     uint32_t ntasks = 0;
     bool has_lists = false;
+    bool all_dense = false;       // every item line-dense: the dense kernel runs the launch
     bool inline_ok = false;       // <= INLINE_ITEMS: launched from the kernarg segment
     uint32_t uses = 0;            // launches so far; a reused inline set is uploaded once and
                                   // launched by pointer (see run_windows)

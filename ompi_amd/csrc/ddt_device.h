@@ -17,6 +17,8 @@ constexpr int THREADS = 256;        // workgroup size (4 wave64)
 constexpr uint32_t SLAB_FULL = 0xffffffffu;
 // units each thread loads before storing, per pass of the affine loop
 constexpr int unroll_of(uint32_t U) { return U >= 16 ? 4 : 8; }
+// user-span bytes a workgroup stages in LDS per task of the line-dense path (run_dense)
+constexpr uint32_t DENSE_LDS = 4096;
 
 enum LeafKind : int { LEAF_AFFINE = 0, LEAF_LIST = 1 };
 
@@ -84,7 +86,8 @@ struct Item {
     uint32_t same;          // typed copy: the packed side uses the user-side layout too
     uint32_t nt;            // user-side accesses non-temporal (sparse gathers over > MALL spans)
     int64_t w0, w1;         // LIST_VAR / FRAG: window [w0, w1) in packed-stream coordinates
-    uint64_t nbytes;        // FRAG: bytes
+    uint64_t nbytes;        // FRAG: bytes.  AFFINE: records per task of the line-dense path
+                            // (run_dense, LDS-staged whole-line accesses), 0 = the unit loop
     uint32_t wt;            // store policy: 1 = user-side stores (unpack) write through L2 (sc1);
                             // 2 = every store of the launch sc1; 3 = user-side stores of an
                             // unpack non-temporal (affine leaves)

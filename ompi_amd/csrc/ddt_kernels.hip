@@ -36,13 +36,20 @@ DDT_MOVE_DECLARE(p1)
 DDT_MOVE_DECLARE(u0)
 DDT_MOVE_DECLARE(u1)
 #undef DDT_MOVE_DECLARE
+hipError_t launch_dense_inline_p0(const ItemBlock &, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t);
+hipError_t launch_dense_inline_u0(const ItemBlock &, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t);
+hipError_t launch_dense_p0(const Item *, uint32_t, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t);
+hipError_t launch_dense_u0(const Item *, uint32_t, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t);
 
 hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, uint64_t ubase,
-                              uint64_t pbase, hipStream_t stream, uint32_t grid_cap)
+                              uint64_t pbase, hipStream_t stream, uint32_t grid_cap, bool dense)
 {
     if (ntasks == 0 || blk.n == 0)
         return hipSuccess;
     const uint32_t g = grid_cap && grid_cap < ntasks ? grid_cap : ntasks;
+    if (dense && !lists)
+        return dir == 0 ? launch_dense_inline_p0(blk, ntasks, g, ubase, pbase, stream)
+                        : launch_dense_inline_u0(blk, ntasks, g, ubase, pbase, stream);
     if (dir == 0)
         return lists ? launch_move_inline_p1(blk, ntasks, g, ubase, pbase, stream)
                      : launch_move_inline_p0(blk, ntasks, g, ubase, pbase, stream);
@@ -51,11 +58,14 @@ hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bo
 }
 
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
-                       uint64_t ubase, uint64_t pbase, hipStream_t stream, uint32_t grid_cap)
+                       uint64_t ubase, uint64_t pbase, hipStream_t stream, uint32_t grid_cap, bool dense)
 {
     if (ntasks == 0 || nitems == 0)
         return hipSuccess;
     const uint32_t g = grid_cap && grid_cap < ntasks ? grid_cap : ntasks;
+    if (dense && !lists)
+        return dir == 0 ? launch_dense_p0(d_items, nitems, ntasks, g, ubase, pbase, stream)
+                        : launch_dense_u0(d_items, nitems, ntasks, g, ubase, pbase, stream);
     if (dir == 0)
         return lists ? launch_move_p1(d_items, nitems, ntasks, g, ubase, pbase, stream)
                      : launch_move_p0(d_items, nitems, ntasks, g, ubase, pbase, stream);

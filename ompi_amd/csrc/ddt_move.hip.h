@@ -179,6 +179,130 @@ __device__ __forceinline__ void run_affine(const Item *it, Bases bs, uint32_t ub
     }
 }
 
+// Line-dense records (round 3): blocks of blen bytes at a user stride S with blen < S <= 4 blen
+// (BASELINE config 5: 20-byte records every 32 bytes), packed contiguously.  The unit loop moves
+// one U-byte unit per lane (5 four-byte loads per record, partial lines per instruction); here a
+// workgroup moves its task in chunks of R whole records (R * S <= DENSE_LDS bytes) through LDS:
+// pack loads a chunk's user span with whole 16-byte loads (gap bytes included: they sit on lines
+// the records touch anyway) and writes the packed stream with 16-byte stores when it is 16-byte
+// aligned; unpack loads the packed span with 16-byte loads and writes each record with the widest
+// aligned stores (gap bytes untouched).  The next chunk's loads are issued before the current
+// chunk is written out.  A task is several chunks (Item::nbytes = R, the planner sizes tasks to
+// ~16 KiB of packed stream), so the per-workgroup prologue is paid once per 16 KiB
+// (scripts/ubench_dense2.hip, profiles/r3_ubench_dense2.log).  Returns false (nothing moved)
+// when the task's records cross a run of the innermost dim; the caller runs the unit loop.
+template <int DIR>
+__device__ __forceinline__ bool run_dense(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
+{
+    __shared__ u32x4 buf[DENSE_LDS / 16 + 2];
+    uint32_t *lds = reinterpret_cast<uint32_t *>(buf);
+    constexpr uint32_t NV = DENSE_LDS / 16 + 2, PER = (NV + THREADS - 1) / THREADS;   // 2 vectors / lane
+    const uint32_t upb = uint32_t(it->upb), U = it->U;
+    const uint32_t b0 = ub / upb, nrec = (ue - ub) / upb;
+    const uint32_t nd = it->ndim, inner = nd - 1;
+    const uint32_t cin = uint32_t(it->cnt[inner]);
+    if (b0 % cin + nrec > cin)
+        return false;
+    int64_t uo = 0, po = 0;
+    {   // offsets of the task's first record
+        uint32_t blk = b0;
+        for (int j = int(nd) - 1; j > 0; --j) {
+            const uint32_t q = fastdiv(blk, it->fd[j]);
+            const uint32_t idx = blk - q * uint32_t(it->cnt[j]);
+            blk = q;
+            uo += int64_t(idx) * it->ustr[j];
+            po += int64_t(idx) * it->pstr[j];
+        }
+        uo += int64_t(blk) * it->ustr[0];
+        po += int64_t(blk) * it->pstr[0];
+    }
+    const uint32_t blen = upb * U, S = uint32_t(it->ustr[inner]), R = uint32_t(it->nbytes);
+    const FastDiv fw = it->fd_nblk;   // division by the record's 4-byte words (blen / 4)
+    const uint64_t ubase = bs.u + it->user + uint64_t(uo), pbase = bs.p + it->packed + uint64_t(po);
+    const bool ntl = DIR == 1 || it->nt == 1;
+    // the chunk starting at record r0: its 16-byte-aligned source span
+    auto span = [&](uint32_t r0, uint32_t n, uint64_t &a16, uint32_t &head, uint32_t &nvec) {
+        const uint64_t a = DIR == 0 ? ubase + uint64_t(r0) * S : pbase + uint64_t(r0) * blen;
+        a16 = a & ~uint64_t(15);
+        head = uint32_t(a - a16);
+        nvec = (head + (DIR == 0 ? (n - 1) * S + blen : n * blen) + 15) / 16;
+    };
+    auto load = [&](uint32_t r0, u32x4 *v) {
+        uint64_t a16;
+        uint32_t head, nvec;
+        span(r0, min(R, nrec - r0), a16, head, nvec);
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(a16);
+#pragma unroll
+        for (uint32_t k = 0; k < PER; ++k) {
+            const uint32_t i = threadIdx.x + k * THREADS;
+            if (i < nvec)
+                v[k] = ntl ? __builtin_nontemporal_load(src + i) : src[i];
+        }
+    };
+    u32x4 v[PER];
+    load(0, v);
+    for (uint32_t r0 = 0; r0 < nrec; r0 += R) {
+        const uint32_t n = min(R, nrec - r0);
+        uint64_t a16;
+        uint32_t head, nvec;
+        span(r0, n, a16, head, nvec);
+        __syncthreads();   // the previous chunk's readers are done with the LDS
+#pragma unroll
+        for (uint32_t k = 0; k < PER; ++k) {
+            const uint32_t i = threadIdx.x + k * THREADS;
+            if (i < nvec)
+                buf[i] = v[k];
+        }
+        __syncthreads();
+        if (r0 + R < nrec)
+            load(r0 + R, v);   // in flight while this chunk is written out
+        if (DIR == 0) {
+            const uint64_t pstart = pbase + uint64_t(r0) * blen;
+            const uint32_t pbytes = n * blen;
+            if ((pstart & 15) == 0 && (pbytes & 15) == 0) {
+                u32x4 *dst = reinterpret_cast<u32x4 *>(pstart);
+                for (uint32_t c = threadIdx.x; c < pbytes / 16; c += THREADS) {
+                    uint32_t w[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint32_t q = 4 * c + uint32_t(i), r = fastdiv(q, fw);
+                        w[i] = lds[(head + r * S) / 4 + (q - r * fw.d)];
+                    }
+                    dst[c] = u32x4{w[0], w[1], w[2], w[3]};
+                }
+            } else {
+                uint32_t *dst = reinterpret_cast<uint32_t *>(pstart);
+                for (uint32_t q = threadIdx.x; q < pbytes / 4; q += THREADS) {
+                    const uint32_t r = fastdiv(q, fw);
+                    dst[q] = lds[(head + r * S) / 4 + (q - r * fw.d)];
+                }
+            }
+        } else {
+            for (uint32_t r = threadIdx.x; r < n; r += THREADS) {
+                uint8_t *d = reinterpret_cast<uint8_t *>(ubase + uint64_t(r0 + r) * S);
+                const uint32_t l0 = (head + r * blen) / 4;
+                uint32_t o = 0;
+                // widest stores the record's alignment allows (every record is 4-byte aligned)
+                while (o < blen) {
+                    const uint64_t a = uint64_t(uintptr_t(d + o));
+                    const uint32_t w = l0 + o / 4;
+                    if ((a & 15) == 0 && blen - o >= 16) {
+                        *reinterpret_cast<u32x4 *>(d + o) = u32x4{lds[w], lds[w + 1], lds[w + 2], lds[w + 3]};
+                        o += 16;
+                    } else if ((a & 7) == 0 && blen - o >= 8) {
+                        *reinterpret_cast<u32x2 *>(d + o) = u32x2{lds[w], lds[w + 1]};
+                        o += 8;
+                    } else {
+                        *reinterpret_cast<uint32_t *>(d + o) = lds[w];
+                        o += 4;
+                    }
+                }
+            }
+        }
+    }
+    return true;
+}
+
 template <int U, int DIR>
 __device__ __noinline__ void run_list_uni64(const Item *it, Bases bs, uint64_t ub, uint64_t ue)
 {
@@ -395,8 +519,9 @@ __device__ __forceinline__ void dispatch_list_uni(const Item *it, Bases bs, uint
 
 // LISTS = false: affine + fragment items only (vector/hvector/subarray/struct nests), a
 // lean register budget; LISTS = true adds the index-list paths.
-template <int DIR, bool LISTS>
-__device__ __forceinline__ void move_task(const Item *__restrict__ items, uint32_t nitems, Bases bs, uint32_t b)
+// Task b of a launch: its item (scalar binary search over task_begin) and unit range.
+__device__ __forceinline__ const Item *locate_task(const Item *__restrict__ items, uint32_t nitems, uint32_t b,
+                                                   uint64_t &ub, uint64_t &ue)
 {
     uint32_t lo = 0, hi = nitems - 1;
     while (lo < hi) {
@@ -423,9 +548,17 @@ __device__ __forceinline__ void move_task(const Item *__restrict__ items, uint32
             }
         }
     }
-    const uint64_t ub = it->u0 + t * it->units_per_task;
-    uint64_t ue = ub + it->units_per_task;
+    ub = it->u0 + t * it->units_per_task;
+    ue = ub + it->units_per_task;
     if (ue > it->u1) ue = it->u1;
+    return it;
+}
+
+template <int DIR, bool LISTS>
+__device__ __forceinline__ void move_task(const Item *__restrict__ items, uint32_t nitems, Bases bs, uint32_t b)
+{
+    uint64_t ub, ue;
+    const Item *it = locate_task(items, nitems, b, ub, ue);
     switch (it->kind) {
     case ITEM_AFFINE:
         if (it->idx64) {
@@ -482,6 +615,67 @@ __device__ __forceinline__ void move_task(const Item *__restrict__ items, uint32
     }
 }
 
+// The fallback of a line-dense task whose records cross a run of the innermost dim: one U-byte
+// unit per lane as 4-byte words, generic nest (few registers, so the dense kernel keeps its
+// occupancy).
+template <int DIR>
+__device__ __forceinline__ void run_units_light(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
+{
+    const uint64_t user = bs.u + it->user, packed = bs.p + it->packed;
+    const uint32_t U = it->U, upb = uint32_t(it->upb), nd = it->ndim;
+    const FastDiv fdu = it->fd_upb;
+    for (uint32_t u = ub + threadIdx.x; u < ue; u += THREADS) {
+        uint32_t blk = fastdiv(u, fdu);
+        const uint32_t within = u - blk * upb;
+        int64_t uo = int64_t(within) * U, po = uo;
+        for (int j = int(nd) - 1; j > 0; --j) {
+            const uint32_t q = fastdiv(blk, it->fd[j]);
+            const uint32_t idx = blk - q * uint32_t(it->cnt[j]);
+            blk = q;
+            uo += int64_t(idx) * it->ustr[j];
+            po += int64_t(idx) * it->pstr[j];
+        }
+        uo += int64_t(blk) * it->ustr[0];
+        po += int64_t(blk) * it->pstr[0];
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(DIR == 0 ? user + uo : packed + po);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(DIR == 0 ? packed + po : user + uo);
+        for (uint32_t w = 0; w < U / 4; ++w)
+            dst[w] = src[w];
+    }
+}
+
+// A launch whose items are all line-dense (Item::nbytes, ItemSet::all_dense) runs this kernel;
+// in a launch that mixes them with other items they take the unit loop of the general kernel.
+// Kept apart so neither kernel pays the other's registers or LDS (the general kernel stays at
+// 56-58 VGPRs, 8 waves per SIMD, for pack and unpack; this one needs 28).
+template <int DIR>
+__device__ __forceinline__ void dense_body(const Item *__restrict__ items, uint32_t nitems, Bases bs, uint32_t ntasks)
+{
+    for (uint32_t b = blockIdx.x; b < ntasks; b += gridDim.x) {
+        if (b != blockIdx.x)
+            __syncthreads();
+        uint64_t ub, ue;
+        const Item *it = locate_task(items, nitems, b, ub, ue);
+        if (!run_dense<DIR>(it, bs, uint32_t(ub), uint32_t(ue)))
+            run_units_light<DIR>(it, bs, uint32_t(ub), uint32_t(ue));
+    }
+}
+
+template <int DIR>
+__global__ __launch_bounds__(THREADS) void ddt_dense_kernel(const Item *__restrict__ items, uint32_t nitems,
+                                                            uint64_t ubase, uint64_t pbase, uint32_t ntasks)
+{
+    dense_body<DIR>(items, nitems, Bases{ubase, pbase}, ntasks);
+}
+
+template <int DIR, uint32_t NI>
+__global__ __launch_bounds__(THREADS) void ddt_dense_inline_kernel(ItemBlockN<NI> blk)
+{
+    const ItemBlockN<NI> *kb = reinterpret_cast<const ItemBlockN<NI> *>(
+        (const void *) __builtin_amdgcn_kernarg_segment_ptr());
+    dense_body<DIR>(kb->items, kb->n, Bases{kb->ubase, kb->pbase}, kb->ntasks);
+}
+
 // One workgroup per task, or -- when the launch is capped below the task count (a window
 // in pinned host memory, where PCIe and not the CU count is the limit: a few hundred
 // workgroups keep it full, thousands of them contend for it, scripts/ubench_pcie.hip) --
@@ -531,6 +725,20 @@ static void launch_inline_n(const ItemBlock &blk, uint32_t ntasks, uint32_t grid
                        stream, b);
 }
 
+template <int DIR, uint32_t NI>
+static void launch_dense_inline_n(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, uint64_t ubase,
+                                  uint64_t pbase, hipStream_t stream)
+{
+    ItemBlockN<NI> b;
+    b.n = blk.n;
+    b.ntasks = ntasks;
+    b.ubase = ubase;
+    b.pbase = pbase;
+    for (uint32_t i = 0; i < blk.n; ++i)
+        b.items[i] = blk.items[i];
+    hipLaunchKernelGGL((ddt_dense_inline_kernel<DIR, NI>), dim3(grid), dim3(THREADS), 0, stream, b);
+}
+
 template <int DIR, bool LISTS>
 static void launch_inline(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, uint64_t ubase, uint64_t pbase,
                           hipStream_t stream)
@@ -540,6 +748,24 @@ static void launch_inline(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, 
     else if (blk.n <= 4) launch_inline_n<DIR, LISTS, 4>(blk, ntasks, grid, ubase, pbase, stream);
     else launch_inline_n<DIR, LISTS, INLINE_ITEMS>(blk, ntasks, grid, ubase, pbase, stream);
 }
+
+// The line-dense launchers of one direction (instantiated with the LISTS = false units).
+#define DDT_DENSE_INSTANCE(DIRV, TAG)                                                                   \
+    hipError_t launch_dense_inline_##TAG(const ItemBlock &blk, uint32_t ntasks, uint32_t grid,          \
+                                         uint64_t ubase, uint64_t pbase, hipStream_t stream)            \
+    {                                                                                                   \
+        if (blk.n == 1) launch_dense_inline_n<DIRV, 1>(blk, ntasks, grid, ubase, pbase, stream);        \
+        else if (blk.n == 2) launch_dense_inline_n<DIRV, 2>(blk, ntasks, grid, ubase, pbase, stream);   \
+        else launch_dense_inline_n<DIRV, INLINE_ITEMS>(blk, ntasks, grid, ubase, pbase, stream);        \
+        return hipGetLastError();                                                                       \
+    }                                                                                                   \
+    hipError_t launch_dense_##TAG(const Item *d_items, uint32_t nitems, uint32_t ntasks, uint32_t grid, \
+                                  uint64_t ubase, uint64_t pbase, hipStream_t stream)                   \
+    {                                                                                                   \
+        hipLaunchKernelGGL((ddt_dense_kernel<DIRV>), dim3(grid), dim3(THREADS), 0, stream, d_items,     \
+                           nitems, ubase, pbase, ntasks);                                               \
+        return hipGetLastError();                                                                       \
+    }
 
 // One (direction, lists) instance of the launchers: ddt_kernels.hip dispatches to them.
 #define DDT_MOVE_INSTANCE(DIRV, LISTSV, TAG)                                                           \

@@ -533,6 +533,41 @@ uint32_t use_snt(uint32_t U, uint64_t blen)   // Item::nt of a streaming leaf, 0
     return blen >= 256 ? 3u : 0u;
 }
 
+// Records per task of the LDS-staged line-dense path (run_dense in ddt_move.hip.h), 0 = the
+// unit loop: affine blocks of blen >= 8 bytes (4-byte aligned) at an innermost user stride S
+// with blen < S <= 4 blen (at least a quarter of every line the records touch is theirs) and
+// S <= 512, packed contiguously.  R = DENSE_LDS / S records (128 for config 5's 32-byte
+// records, the microbenchmark's best, profiles/r3_ubench_dense2.log).  ddt_tune("dense"): 0 off.
+uint64_t dense_records(uint32_t U, uint64_t blen, const std::vector<LeafDim> &dims)
+{
+    if (tuning().dense == 0 || U < 4 || dims.empty() || blen < 8)
+        return 0;
+    const LeafDim &in = dims.back();
+    const int64_t S = in.sstr;
+    if (in.cnt < 2 || S <= int64_t(blen) || S > int64_t(4 * blen) || S > 512 || in.dstr != int64_t(blen)
+        || S % 4 != 0)
+        return 0;
+    const uint64_t R = DENSE_LDS / uint64_t(S);
+    return R >= 2 ? R : 0;
+}
+
+// A line-dense task: whole LDS chunks of R records, about 16 KiB of packed stream (the
+// unit loop's task size), so the workgroup prologue is paid per 16 KiB, not per chunk.
+// Tasks start at multiples of their size from the item's first block, so a task size that
+// divides the innermost count (and an item starting on an inner-run boundary) keeps every task
+// inside one run; otherwise the crossing tasks fall back to the unit loop.
+uint64_t dense_task_records(const Item &it)
+{
+    const uint64_t R = it.nbytes, chunk = R * it.upb * it.U;
+    uint64_t g = chunk >= (16u << 10) ? 1 : (16u << 10) / chunk;
+    if (tuning().dense > 0)
+        g = uint64_t(tuning().dense);   // A/B: chunks per task
+    const uint64_t cin = it.cnt[it.ndim - 1];
+    while (g > 1 && cin % (R * g) != 0)
+        --g;
+    return R * g;
+}
+
 uint64_t units_per_task(uint32_t U)
 {
     uint64_t u = (32u << 10) / U;   // provisional; assign_tasks() sets the final size
@@ -638,6 +673,10 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
                 throw std::runtime_error("plan: affine unit range outside its leaf");
             it.nt = use_snt(U, blen) ? use_snt(U, blen) : (use_nt(U, blen, sd) ? 1 : 0);
             it.wt = use_wt(U, blen, &sd);
+            it.nbytes = (!same_layout && !it.idx64 && u0 % it.upb == 0 && u1 % it.upb == 0)
+                            ? dense_records(U, blen, sd) : 0;
+            if (it.nbytes)
+                it.fd_nblk = make_fastdiv(uint32_t(blen / 4));   // run_dense: words per record
             it.u0 = u0;
             it.u1 = u1;
             it.units_per_task = units_per_task(U);
@@ -767,7 +806,9 @@ void assign_tasks(std::vector<Item> &items)
                 tb *= 2;
         }
         for (Item &it : items)
-            if (it.kind == ITEM_AFFINE || it.kind == ITEM_LIST_UNI) {
+            if (it.kind == ITEM_AFFINE && it.nbytes) {   // line-dense: whole LDS chunks per task
+                it.units_per_task = dense_task_records(it) * it.upb;
+            } else if (it.kind == ITEM_AFFINE || it.kind == ITEM_LIST_UNI) {
                 uint64_t u = tb / it.U;
                 it.units_per_task = u < THREADS ? THREADS : u;
             }
@@ -784,6 +825,10 @@ void assign_tasks(std::vector<Item> &items)
         for (Item &it : items) {
             if (it.kind != ITEM_AFFINE && it.kind != ITEM_LIST_UNI)
                 continue;
+            if (it.kind == ITEM_AFFINE && it.nbytes) {   // line-dense: whole records per task
+                it.units_per_task = dense_task_records(it) * it.upb;
+                continue;
+            }
             uint64_t cap = tb;
             if (it.kind == ITEM_AFFINE) {
                 const uint64_t pass = uint64_t(THREADS) * unroll_of(it.U) * it.U;

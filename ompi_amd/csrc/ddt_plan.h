@@ -28,6 +28,7 @@ struct Tuning {
                           // stores; -1 auto (blocks >= 64 KiB), 0 off, 1 on
     long spass = 1;       // task of a streaming leaf: this many unrolled workgroup passes
     long stask = 0;       // task of a streaming leaf in bytes (overrides spass; 0 = spass passes)
+    int dense = -1;       // line-dense records through LDS (run_dense): -1 auto, 0 off, n > 0 n chunks per task
     int hostdirect = 3;   // pinned host iovecs moved by the kernel itself over PCIe (no HBM
                           // staging): bit 0 unpack, bit 1 pack (end to end)
     long stage_mb = 256;  // HBM staging buffer (one per convertor) for pageable host iovecs: the
@@ -57,11 +58,13 @@ bool use_slab(const Item &it);
 uint32_t total_tasks(const std::vector<Item> &items);
 
 // ddt_kernels.hip: dir 0 = pack / typed copy (user side -> packed side), 1 = unpack.
-// grid_cap > 0: at most that many workgroups, looping over the tasks (host-direct windows)
+// grid_cap > 0: at most that many workgroups, looping over the tasks (host-direct windows);
+// dense: every item is line-dense (Item::nbytes), run by the dedicated dense kernel
 hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, uint64_t ubase,
-                              uint64_t pbase, hipStream_t stream, uint32_t grid_cap = 0);
+                              uint64_t pbase, hipStream_t stream, uint32_t grid_cap = 0, bool dense = false);
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
-                       uint64_t ubase, uint64_t pbase, hipStream_t stream, uint32_t grid_cap = 0);
+                       uint64_t ubase, uint64_t pbase, hipStream_t stream, uint32_t grid_cap = 0,
+                       bool dense = false);
 
 // external32 conversion between a native packed stream and its big-endian form.
 // uniform = C in {1,2,4,8,16}: every element is a C-byte word swap (C = 1: a copy) with identical native

@@ -45,6 +45,12 @@ def main():
     print(json.dumps({"floor": "one tiny torch kernel between events",
                       "us": round(float(np.median([a.elapsed_time(b) for a, b in evs])) * 1e3, 2)}), flush=True)
     faces = sys.argv[2].split(",") if len(sys.argv) > 2 else ("x", "y", "z")
+    # round 3: "read" = bench.face_throughput's cold-clean protocol (a 1 GiB read before each
+    # operation, outside the events), so a pack does not pay the previous unpack's write-backs
+    flush = sys.argv[3] if len(sys.argv) > 3 else "none"
+    scribble = torch.full((1 << 27,), 3, dtype=torch.int64, device=dev) if flush == "read" else None
+    print(json.dumps({"protocol": "pack+unpack loop" if scribble is None else
+                      "cold-clean: 1 GiB read before every operation, outside the events"}), flush=True)
     for k in faces:
         ft = ER.build_committed(recs[k])
         rows = []
@@ -61,20 +67,29 @@ def main():
             torch.cuda.synchronize()
             evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(steps)]
             torch.cuda._sleep(int(2e8))   # hold the stream while the host enqueues
-            for a, b, e in evs:
+            ev2 = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+            for (a, b, e), b2 in zip(evs, ev2):
+                if scribble is not None:
+                    scribble.sum()
                 a.record(stream)
                 c.prepare_for_send(ft, F, user.data_ptr())
                 c.pack([(fp, fS)])
                 b.record(stream)
+                if scribble is not None:
+                    scribble.sum()
+                b2.record(stream)
                 c.prepare_for_recv(ft, F, user.data_ptr())
                 c.unpack([(fp, fS)])
                 e.record(stream)
             torch.cuda.synchronize()
             tp = float(np.median([a.elapsed_time(b) for a, b, _ in evs])) * 1e3
-            tu = float(np.median([b.elapsed_time(e) for _, b, e in evs])) * 1e3
+            tu = float(np.median([b2.elapsed_time(e) for (_, _, e), b2 in zip(evs, ev2)])) * 1e3
             rows.append((F, tp, tu))
+            lines = ft.info()["size"] * F // 8 if k == "x" else None
             print(json.dumps({"face": k, "fields": F, "packed_MiB": fS / 2**20, "pack_us": round(tp, 2),
                               "unpack_us": round(tu, 2),
+                              **({"pack_G_lines_per_s": round(lines / tp / 1e3, 1),
+                                  "unpack_G_lines_per_s": round(lines / tu / 1e3, 1)} if lines else {}),
                               "frac": round(4 * fS / ((tp + tu) * 1e-6) / 8e12, 4)}), flush=True)
             del fp
         F = np.array([r[0] for r in rows], dtype=float)

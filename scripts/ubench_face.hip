@@ -34,6 +34,14 @@ template <int NT> __device__ __forceinline__ void st(u32x4 *p, u32x4 v)
     else *p = v;
 }
 
+__global__ __launch_bounds__(256) void flush_write(u32x4 *__restrict__ a, size_t nv, uint32_t v)
+{
+    for (size_t i = size_t(blockIdx.x) * 256 + threadIdx.x; i < nv; i += size_t(gridDim.x) * 256)
+        a[i] = u32x4{v, v, v, v};
+}
+
+static bool g_write_flush = false;
+
 __global__ __launch_bounds__(256) void flush_read(const u32x4 *__restrict__ a, u32x4 *__restrict__ sink, size_t nv)
 {
     u32x4 acc = {0, 0, 0, 0};
@@ -96,7 +104,10 @@ float cold(L launch, int reps)
     CHK(hipEventCreate(&b));
     std::vector<float> ts;
     for (int i = 0; i < reps + 2; ++i) {
-        hipLaunchKernelGGL(flush_read, dim3(4096), dim3(256), 0, 0, F, SINK, FV);
+        if (g_write_flush)
+            hipLaunchKernelGGL(flush_write, dim3(4096), dim3(256), 0, 0, F, FV, uint32_t(i));
+        else
+            hipLaunchKernelGGL(flush_read, dim3(4096), dim3(256), 0, 0, F, SINK, FV);
         CHK(hipEventRecord(a));
         launch();
         CHK(hipEventRecord(b));
@@ -111,8 +122,9 @@ float cold(L launch, int reps)
     return ts[ts.size() / 2];
 }
 
-int main()
+int main(int argc, char **argv)
 {
+    g_write_flush = argc > 1 && argv[1][0] == 'w';   // "write": the flush writes its 1 GiB instead
     const size_t bytes = 256ull << 20, NV = bytes / 16;
     u32x4 *A, *B, *G;
     CHK(hipMalloc(&F, FV * 16));
@@ -124,7 +136,8 @@ int main()
     CHK(hipMemset(B, 2, bytes));
     const int reps = 15;
     auto rate = [&](float us) { return 2.0 * bytes / us / 1e6; };   // TB/s read + write
-    printf("cold 256 MiB moves after a 1 GiB read flush (median of %d), TB/s r+w and frac of 8 TB/s\n", reps);
+    printf("cold 256 MiB moves after a 1 GiB %s flush (median of %d), TB/s r+w and frac of 8 TB/s\n",
+           g_write_flush ? "WRITE" : "read", reps);
 #define Z(K, NTL, NTS, PERB)                                                                                \
     {                                                                                                       \
         const uint32_t per = PERB / 16;                                                                     \
