@@ -534,13 +534,16 @@ uint32_t use_snt(uint32_t U, uint64_t blen)   // Item::nt of a streaming leaf, 0
 }
 
 // Records per task of the LDS-staged line-dense path (run_dense in ddt_move.hip.h), 0 = the
-// unit loop: affine blocks of blen >= 8 bytes (4-byte aligned) at an innermost user stride S
+// unit loop: affine blocks of blen >= 8 bytes (4-byte aligned, at least two units) at an innermost user stride S
 // with blen < S <= 4 blen (at least a quarter of every line the records touch is theirs) and
 // S <= 512, packed contiguously.  R = DENSE_LDS / S records (128 for config 5's 32-byte
 // records, the microbenchmark's best, profiles/r3_ubench_dense2.log).  ddt_tune("dense"): 0 off.
 uint64_t dense_records(uint32_t U, uint64_t blen, const std::vector<LeafDim> &dims)
 {
-    if (tuning().dense == 0 || U < 4 || dims.empty() || blen < 8)
+    // a record of one unit is already one load and one store per lane in the unit loop (cfg1's
+    // 8-byte elements: 11.9 / 13.1 us there against 14.2 / 15.8 through LDS,
+    // profiles/r3_ab_dense_final.jsonl); the LDS path pays off for records of several units
+    if (tuning().dense == 0 || U < 4 || dims.empty() || blen < 8 || blen / U < 2)
         return 0;
     const LeafDim &in = dims.back();
     const int64_t S = in.sstr;
@@ -551,17 +554,17 @@ uint64_t dense_records(uint32_t U, uint64_t blen, const std::vector<LeafDim> &di
     return R >= 2 ? R : 0;
 }
 
-// A line-dense task: whole LDS chunks of R records, about 16 KiB of packed stream (the
-// unit loop's task size), so the workgroup prologue is paid per 16 KiB, not per chunk.
+// A line-dense task: TWO LDS chunks of R records.  One chunk per workgroup pays the task
+// prologue (the item's fields are scalar loads from HBM) for every 4 KiB; more chunks run in
+// sequence inside the workgroup.  cfg5, pack / unpack us (profiles/r3_ab_dense_chunks.jsonl):
+// 1 chunk 1483 / 1950, 2 chunks 1183 / 2043, 4 chunks 1237 / 2110, unit loop 1257 / 2071.
 // Tasks start at multiples of their size from the item's first block, so a task size that
 // divides the innermost count (and an item starting on an inner-run boundary) keeps every task
 // inside one run; otherwise the crossing tasks fall back to the unit loop.
 uint64_t dense_task_records(const Item &it)
 {
-    const uint64_t R = it.nbytes, chunk = R * it.upb * it.U;
-    uint64_t g = chunk >= (16u << 10) ? 1 : (16u << 10) / chunk;
-    if (tuning().dense > 0)
-        g = uint64_t(tuning().dense);   // A/B: chunks per task
+    const uint64_t R = it.nbytes;
+    uint64_t g = tuning().dense > 0 ? uint64_t(tuning().dense) : 2;   // ddt_tune("dense", n): n chunks
     const uint64_t cin = it.cnt[it.ndim - 1];
     while (g > 1 && cin % (R * g) != 0)
         --g;
