@@ -1638,6 +1638,8 @@ int ddt_tune(const char *key, long value)
         tuning().hd_grid_pack = value < 0 ? 0 : value;
     else if (k == "s2unroll")
         tuning().s2unroll = value >= 16 ? 16 : (value >= 8 ? 8 : 4);
+    else if (k == "dsplit")
+        tuning().dsplit = value ? 1 : 0;
     else if (k == "sunroll")
         tuning().sunroll = value >= 16 ? 16 : (value >= 8 ? 8 : 4);
     else if (k == "sseg")

@@ -36,10 +36,22 @@ DDT_MOVE_DECLARE(p1)
 DDT_MOVE_DECLARE(u0)
 DDT_MOVE_DECLARE(u1)
 #undef DDT_MOVE_DECLARE
-hipError_t launch_dense_inline_p0(const ItemBlock &, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t);
-hipError_t launch_dense_inline_u0(const ItemBlock &, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t);
-hipError_t launch_dense_p0(const Item *, uint32_t, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t);
-hipError_t launch_dense_u0(const Item *, uint32_t, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t);
+hipError_t launch_dense_inline_p0(const ItemBlock &, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t, bool);
+hipError_t launch_dense_inline_u0(const ItemBlock &, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t, bool);
+hipError_t launch_dense_p0(const Item *, uint32_t, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t, bool);
+hipError_t launch_dense_u0(const Item *, uint32_t, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t, bool);
+
+// The line-dense unpack runs each task as two workgroups (ddt_tune "dsplit", dense_body):
+// 16 workgroups per 8 tasks.
+static bool dense_split(int dir, uint32_t ntasks)
+{
+    return dir == 1 && tuning().dsplit != 0 && ntasks < 0x70000000u;
+}
+static uint32_t dense_grid(bool split, uint32_t ntasks, uint32_t grid_cap)
+{
+    const uint32_t nv = split ? (ntasks + 7) / 8 * 16 : ntasks;
+    return grid_cap && grid_cap < nv ? grid_cap : nv;
+}
 
 hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, uint64_t ubase,
                               uint64_t pbase, hipStream_t stream, uint32_t grid_cap, bool dense)
@@ -47,9 +59,12 @@ hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bo
     if (ntasks == 0 || blk.n == 0)
         return hipSuccess;
     const uint32_t g = grid_cap && grid_cap < ntasks ? grid_cap : ntasks;
-    if (dense && !lists)
-        return dir == 0 ? launch_dense_inline_p0(blk, ntasks, g, ubase, pbase, stream)
-                        : launch_dense_inline_u0(blk, ntasks, g, ubase, pbase, stream);
+    if (dense && !lists) {
+        const bool sp = dense_split(dir, ntasks);
+        const uint32_t gs = dense_grid(sp, ntasks, grid_cap);
+        return dir == 0 ? launch_dense_inline_p0(blk, ntasks, gs, ubase, pbase, stream, false)
+                        : launch_dense_inline_u0(blk, ntasks, gs, ubase, pbase, stream, sp);
+    }
     if (dir == 0)
         return lists ? launch_move_inline_p1(blk, ntasks, g, ubase, pbase, stream)
                      : launch_move_inline_p0(blk, ntasks, g, ubase, pbase, stream);
@@ -63,9 +78,12 @@ hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, in
     if (ntasks == 0 || nitems == 0)
         return hipSuccess;
     const uint32_t g = grid_cap && grid_cap < ntasks ? grid_cap : ntasks;
-    if (dense && !lists)
-        return dir == 0 ? launch_dense_p0(d_items, nitems, ntasks, g, ubase, pbase, stream)
-                        : launch_dense_u0(d_items, nitems, ntasks, g, ubase, pbase, stream);
+    if (dense && !lists) {
+        const bool sp = dense_split(dir, ntasks);
+        const uint32_t gs = dense_grid(sp, ntasks, grid_cap);
+        return dir == 0 ? launch_dense_p0(d_items, nitems, ntasks, gs, ubase, pbase, stream, false)
+                        : launch_dense_u0(d_items, nitems, ntasks, gs, ubase, pbase, stream, sp);
+    }
     if (dir == 0)
         return lists ? launch_move_p1(d_items, nitems, ntasks, g, ubase, pbase, stream)
                      : launch_move_p0(d_items, nitems, ntasks, g, ubase, pbase, stream);

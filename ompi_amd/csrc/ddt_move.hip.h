@@ -648,32 +648,52 @@ __device__ __forceinline__ void run_units_light(const Item *it, Bases bs, uint32
 // in a launch that mixes them with other items they take the unit loop of the general kernel.
 // Kept apart so neither kernel pays the other's registers or LDS (the general kernel stays at
 // 56-58 VGPRs, 8 waves per SIMD, for pack and unpack; this one needs 28).
-template <int DIR>
+// SPLIT (the unpack): each task runs as two workgroups, the first taking the first half of its
+// chunks; 16 workgroups per 8 tasks, workgroup b takes task (b / 16) * 8 + b % 8, so it stays
+// on the XCD the task's slab was meant for (dense_grid on the host sizes the launch).  The
+// unpack moves one chunk per workgroup that way (cfg5: 2043 -> 1949 us against two chunks,
+// profiles/r3_ab_dense_chunks.jsonl) while the pack keeps two, its load of the next chunk in
+// flight (1183 against 1483 us with one).
+template <int DIR, bool SPLIT>
 __device__ __forceinline__ void dense_body(const Item *__restrict__ items, uint32_t nitems, Bases bs, uint32_t ntasks)
 {
-    for (uint32_t b = blockIdx.x; b < ntasks; b += gridDim.x) {
+    const uint32_t nv = SPLIT ? (ntasks + 7) / 8 * 16 : ntasks;
+    for (uint32_t b = blockIdx.x; b < nv; b += gridDim.x) {
         if (b != blockIdx.x)
             __syncthreads();
         uint64_t ub, ue;
-        const Item *it = locate_task(items, nitems, b, ub, ue);
+        const uint32_t task = SPLIT ? (b >> 4) * 8 + (b & 7) : b;
+        if (SPLIT && task >= ntasks)
+            continue;
+        const Item *it = locate_task(items, nitems, task, ub, ue);
+        if (SPLIT) {
+            const uint64_t upb = it->upb, R = it->nbytes;
+            const uint64_t nch = ((ue - ub) / upb + R - 1) / R, mid = ub + (nch + 1) / 2 * R * upb;
+            if (b & 8)
+                ub = mid < ue ? mid : ue;
+            else
+                ue = mid < ue ? mid : ue;
+            if (ub >= ue)
+                continue;
+        }
         if (!run_dense<DIR>(it, bs, uint32_t(ub), uint32_t(ue)))
             run_units_light<DIR>(it, bs, uint32_t(ub), uint32_t(ue));
     }
 }
 
-template <int DIR>
+template <int DIR, bool SPLIT>
 __global__ __launch_bounds__(THREADS) void ddt_dense_kernel(const Item *__restrict__ items, uint32_t nitems,
                                                             uint64_t ubase, uint64_t pbase, uint32_t ntasks)
 {
-    dense_body<DIR>(items, nitems, Bases{ubase, pbase}, ntasks);
+    dense_body<DIR, SPLIT>(items, nitems, Bases{ubase, pbase}, ntasks);
 }
 
-template <int DIR, uint32_t NI>
+template <int DIR, bool SPLIT, uint32_t NI>
 __global__ __launch_bounds__(THREADS) void ddt_dense_inline_kernel(ItemBlockN<NI> blk)
 {
     const ItemBlockN<NI> *kb = reinterpret_cast<const ItemBlockN<NI> *>(
         (const void *) __builtin_amdgcn_kernarg_segment_ptr());
-    dense_body<DIR>(kb->items, kb->n, Bases{kb->ubase, kb->pbase}, kb->ntasks);
+    dense_body<DIR, SPLIT>(kb->items, kb->n, Bases{kb->ubase, kb->pbase}, kb->ntasks);
 }
 
 // One workgroup per task, or -- when the launch is capped below the task count (a window
@@ -727,7 +747,7 @@ static void launch_inline_n(const ItemBlock &blk, uint32_t ntasks, uint32_t grid
 
 template <int DIR, uint32_t NI>
 static void launch_dense_inline_n(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, uint64_t ubase,
-                                  uint64_t pbase, hipStream_t stream)
+                                  uint64_t pbase, hipStream_t stream, bool split)
 {
     ItemBlockN<NI> b;
     b.n = blk.n;
@@ -736,7 +756,10 @@ static void launch_dense_inline_n(const ItemBlock &blk, uint32_t ntasks, uint32_
     b.pbase = pbase;
     for (uint32_t i = 0; i < blk.n; ++i)
         b.items[i] = blk.items[i];
-    hipLaunchKernelGGL((ddt_dense_inline_kernel<DIR, NI>), dim3(grid), dim3(THREADS), 0, stream, b);
+    if (split)
+        hipLaunchKernelGGL((ddt_dense_inline_kernel<DIR, true, NI>), dim3(grid), dim3(THREADS), 0, stream, b);
+    else
+        hipLaunchKernelGGL((ddt_dense_inline_kernel<DIR, false, NI>), dim3(grid), dim3(THREADS), 0, stream, b);
 }
 
 template <int DIR, bool LISTS>
@@ -752,18 +775,22 @@ static void launch_inline(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, 
 // The line-dense launchers of one direction (instantiated with the LISTS = false units).
 #define DDT_DENSE_INSTANCE(DIRV, TAG)                                                                   \
     hipError_t launch_dense_inline_##TAG(const ItemBlock &blk, uint32_t ntasks, uint32_t grid,          \
-                                         uint64_t ubase, uint64_t pbase, hipStream_t stream)            \
+                                         uint64_t ubase, uint64_t pbase, hipStream_t stream, bool split) \
     {                                                                                                   \
-        if (blk.n == 1) launch_dense_inline_n<DIRV, 1>(blk, ntasks, grid, ubase, pbase, stream);        \
-        else if (blk.n == 2) launch_dense_inline_n<DIRV, 2>(blk, ntasks, grid, ubase, pbase, stream);   \
-        else launch_dense_inline_n<DIRV, INLINE_ITEMS>(blk, ntasks, grid, ubase, pbase, stream);        \
+        if (blk.n == 1) launch_dense_inline_n<DIRV, 1>(blk, ntasks, grid, ubase, pbase, stream, split); \
+        else if (blk.n == 2) launch_dense_inline_n<DIRV, 2>(blk, ntasks, grid, ubase, pbase, stream, split); \
+        else launch_dense_inline_n<DIRV, INLINE_ITEMS>(blk, ntasks, grid, ubase, pbase, stream, split); \
         return hipGetLastError();                                                                       \
     }                                                                                                   \
     hipError_t launch_dense_##TAG(const Item *d_items, uint32_t nitems, uint32_t ntasks, uint32_t grid, \
-                                  uint64_t ubase, uint64_t pbase, hipStream_t stream)                   \
+                                  uint64_t ubase, uint64_t pbase, hipStream_t stream, bool split)       \
     {                                                                                                   \
-        hipLaunchKernelGGL((ddt_dense_kernel<DIRV>), dim3(grid), dim3(THREADS), 0, stream, d_items,     \
-                           nitems, ubase, pbase, ntasks);                                               \
+        if (split)                                                                                      \
+            hipLaunchKernelGGL((ddt_dense_kernel<DIRV, true>), dim3(grid), dim3(THREADS), 0, stream,    \
+                               d_items, nitems, ubase, pbase, ntasks);                                  \
+        else                                                                                            \
+            hipLaunchKernelGGL((ddt_dense_kernel<DIRV, false>), dim3(grid), dim3(THREADS), 0, stream,   \
+                               d_items, nitems, ubase, pbase, ntasks);                                  \
         return hipGetLastError();                                                                       \
     }
 

@@ -29,6 +29,7 @@ struct Tuning {
     long spass = 1;       // task of a streaming leaf: this many unrolled workgroup passes
     long stask = 0;       // task of a streaming leaf in bytes (overrides spass; 0 = spass passes)
     int dense = -1;       // line-dense records through LDS (run_dense): -1 auto, 0 off, n > 0 n chunks per task
+    int dsplit = 1;       // line-dense unpack: each task as two workgroups (dense_body SPLIT)
     int hostdirect = 3;   // pinned host iovecs moved by the kernel itself over PCIe (no HBM
                           // staging): bit 0 unpack, bit 1 pack (end to end)
     long stage_mb = 256;  // HBM staging buffer (one per convertor) for pageable host iovecs: the
