@@ -104,7 +104,20 @@ void *pool_alloc(size_t bytes)
     void *p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) {
         (void) hipGetLastError();
-        return nullptr;
+        // out of device memory: hand this device's cached blocks of other sizes back to HIP
+        // (hipFree waits for the device: the exceptional path only) and try once more
+        auto &fl = P.free[dev];
+        if (fl.empty())
+            return nullptr;
+        for (auto &sb : fl) {
+            (void) hipFree(sb.second);
+            P.blocks.erase(sb.second);
+        }
+        fl.clear();
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            (void) hipGetLastError();
+            return nullptr;
+        }
     }
     P.blocks[p] = Block{bytes, dev, 0};
     return p;

@@ -20,7 +20,8 @@
 namespace ddt {
 
 // `bytes` of device memory on the current device: a cached block of at least that size (at
-// most twice it), else hipMalloc.  nullptr when HIP is out of memory.
+// most twice it; released blocks whose fences have passed count as cached), else hipMalloc; when that fails, the device's cached blocks go back to HIP and hipMalloc is tried
+// once more.  nullptr when HIP is out of memory.
 void *pool_alloc(size_t bytes);
 // A block no queued work reads any more: reusable at once.
 void pool_free(void *p);
