@@ -577,7 +577,10 @@ def main():
     # xGMI); every rank checks that its slice of the gathered stream is its own shard.
     rccl = None
     if world > 1 and not args.no_gather:
-        rccl = gather_check(packed, S, world, rank, dev, backend)
+        try:
+            rccl = gather_check(packed, S, world, rank, dev, backend)
+        except Exception as ex:   # the timed line stands on its own; report the failed check in it
+            rccl = {"backend": backend, "ok": False, "error": f"{type(ex).__name__}: {ex}"[:300]}
 
     result = None
     if rank == 0:
