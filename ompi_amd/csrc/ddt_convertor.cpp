@@ -402,6 +402,14 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     } hold{P, S, stream};
     if (S->items.empty())
         return DDT_SUCCESS;
+    if (S->all_dense && S->items.size() == 1 && grid_cap == 0) {
+        // a large single-item line-dense launch carries its fields by value (no descriptor)
+        hipError_t e = hipSuccess;
+        if (launch_dense_by_value(S->items[0], dir, ubase, pbase, stream, &e)) {
+            HIPCHK(e);
+            return DDT_SUCCESS;
+        }
+    }
     // A descriptor set travels in the kernel-argument segment on its first launch (no upload
     // for one-off windows).  From its second launch on it is launched by pointer from HBM:
     // with device-resident kernel arguments every 64-byte line of arguments is a host write
@@ -1648,6 +1656,8 @@ int ddt_tune(const char *key, long value)
         tuning().stage_mb = value < 1 ? 1 : value;
     else if (k == "snt")
         tuning().snt = value < -1 ? -2 : (value < 0 ? -1 : (value >= 3 && value <= 5 ? int(value) : (value ? 1 : 0)));
+    else if (k == "dfast")
+        tuning().dfast = int(value & 3);
     else if (k == "dense")
         tuning().dense = value < 0 ? -1 : int(value);
     else if (k == "stask")

@@ -40,6 +40,8 @@ hipError_t launch_dense_inline_p0(const ItemBlock &, uint32_t, uint32_t, uint64_
 hipError_t launch_dense_inline_u0(const ItemBlock &, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t, bool);
 hipError_t launch_dense_p0(const Item *, uint32_t, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t, bool);
 hipError_t launch_dense_u0(const Item *, uint32_t, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t, bool);
+hipError_t launch_dense1_p0(const DenseArgs &, uint32_t, hipStream_t);
+hipError_t launch_dense1_u0(const DenseArgs &, uint32_t, hipStream_t);
 
 // The line-dense unpack runs each task as two workgroups (ddt_tune "dsplit", dense_body):
 // 16 workgroups per 8 tasks.
@@ -51,6 +53,47 @@ static uint32_t dense_grid(bool split, uint32_t ntasks, uint32_t grid_cap)
 {
     const uint32_t nv = split ? (ntasks + 7) / 8 * 16 : ntasks;
     return grid_cap && grid_cap < nv ? grid_cap : nv;
+}
+
+// The by-value single-item line-dense launch (ddt_dense1_kernel): a large launch of one dense
+// item whose chunks all lie inside one run of the innermost dim.  Returns false when the item
+// does not qualify (the caller launches the descriptor set as usual).  Small launches keep the
+// descriptor path: ~170 bytes of kernel arguments cost ~1 us more host time per launch than a
+// descriptor pointer (device-resident kernel arguments, profiles/r1_hostbench.log).
+bool launch_dense_by_value(const Item &it, int dir, uint64_t ubase, uint64_t pbase, hipStream_t stream,
+                           hipError_t *err)
+{
+    if (!(tuning().dfast & (dir == 0 ? 1 : 2)))
+        return false;
+    if (it.kind != ITEM_AFFINE || !it.nbytes || it.idx64 || it.ndim < 1 || it.ndim > DENSE_ARG_DIMS || it.upb == 0)
+        return false;
+    const uint64_t R = it.nbytes, cu = R * it.upb;
+    const uint64_t cin = it.cnt[it.ndim - 1];
+    if (it.u0 % it.upb != 0)
+        return false;
+    if (it.ndim > 1 && (cin % R != 0 || ((it.u0 / it.upb) % cin) % R != 0))
+        return false;   // a chunk could cross an inner run
+    const uint64_t nch = (it.u1 - it.u0 + cu - 1) / cu;
+    if (nch < 1024 || nch >= 0x7fffffffull || cu >= 0xffffffffull)
+        return false;
+    DenseArgs a{};
+    a.ubase = ubase + it.user;
+    a.pbase = pbase + it.packed;
+    a.u0 = uint32_t(it.u0);
+    a.u1 = uint32_t(it.u1);
+    a.cu = uint32_t(cu);
+    a.nd = it.ndim;
+    a.fdu = it.fd_upb;
+    a.fw = it.fd_nblk;
+    a.nt = it.nt;
+    for (uint32_t j = 0; j < it.ndim; ++j) {
+        a.cnt[j] = uint32_t(it.cnt[j]);
+        a.fd[j] = it.fd[j];
+        a.ustr[j] = it.ustr[j];
+        a.pstr[j] = it.pstr[j];
+    }
+    *err = dir == 0 ? launch_dense1_p0(a, uint32_t(nch), stream) : launch_dense1_u0(a, uint32_t(nch), stream);
+    return true;
 }
 
 hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, uint64_t ubase,

@@ -186,15 +186,118 @@ __device__ __forceinline__ void run_affine(const Item *it, Bases bs, uint32_t ub
 // pack loads a chunk's user span with whole 16-byte loads (gap bytes included: they sit on lines
 // the records touch anyway) and writes the packed stream with 16-byte stores when it is 16-byte
 // aligned; unpack loads the packed span with 16-byte loads and writes each record with the widest
-// aligned stores (gap bytes untouched).  The next chunk's loads are issued before the current
-// chunk is written out.  A task is several chunks (Item::nbytes = R, the planner sizes tasks to
-// ~16 KiB of packed stream), so the per-workgroup prologue is paid once per 16 KiB
-// (scripts/ubench_dense2.hip, profiles/r3_ubench_dense2.log).  Returns false (nothing moved)
-// when the task's records cross a run of the innermost dim; the caller runs the unit loop.
+// aligned stores (gap bytes untouched).
+//
+// dense_write: the chunk of n records staged in LDS (its span starting `head` bytes into the LDS
+// image) out to the destination: pstart = packed address of the chunk, urec = user address of its
+// first record.
 template <int DIR>
-__device__ __forceinline__ bool run_dense(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
+__device__ __forceinline__ void dense_write(const uint32_t *lds, uint32_t head, uint32_t n, uint32_t blen, uint32_t S,
+                                            FastDiv fw, uint64_t pstart, uint64_t urec)
 {
-    __shared__ u32x4 buf[DENSE_LDS / 16 + 2];
+    if (DIR == 0) {
+        const uint32_t pbytes = n * blen;
+        if ((pstart & 15) == 0 && (pbytes & 15) == 0) {
+            u32x4 *dst = reinterpret_cast<u32x4 *>(pstart);
+            for (uint32_t c = threadIdx.x; c < pbytes / 16; c += THREADS) {
+                uint32_t w[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t q = 4 * c + uint32_t(i), r = fastdiv(q, fw);
+                    w[i] = lds[(head + r * S) / 4 + (q - r * fw.d)];
+                }
+                dst[c] = u32x4{w[0], w[1], w[2], w[3]};
+            }
+        } else {
+            uint32_t *dst = reinterpret_cast<uint32_t *>(pstart);
+            for (uint32_t q = threadIdx.x; q < pbytes / 4; q += THREADS) {
+                const uint32_t r = fastdiv(q, fw);
+                dst[q] = lds[(head + r * S) / 4 + (q - r * fw.d)];
+            }
+        }
+    } else {
+        for (uint32_t r = threadIdx.x; r < n; r += THREADS) {
+            uint8_t *d = reinterpret_cast<uint8_t *>(urec + uint64_t(r) * S);
+            const uint32_t l0 = (head + r * blen) / 4;
+            uint32_t o = 0;
+            // widest stores the record's alignment allows (every record is 4-byte aligned)
+            while (o < blen) {
+                const uint64_t a = uint64_t(uintptr_t(d + o));
+                const uint32_t w = l0 + o / 4;
+                if ((a & 15) == 0 && blen - o >= 16) {
+                    *reinterpret_cast<u32x4 *>(d + o) = u32x4{lds[w], lds[w + 1], lds[w + 2], lds[w + 3]};
+                    o += 16;
+                } else if ((a & 7) == 0 && blen - o >= 8) {
+                    *reinterpret_cast<u32x2 *>(d + o) = u32x2{lds[w], lds[w + 1]};
+                    o += 8;
+                } else {
+                    *reinterpret_cast<uint32_t *>(d + o) = lds[w];
+                    o += 4;
+                }
+            }
+        }
+    }
+}
+
+// One chunk of nrec records whose first record sits at user address urec and packed address
+// pstart: load its source span (16-byte loads, two per lane at most), stage it, write it out.
+template <int DIR>
+__device__ __forceinline__ void dense_chunk(u32x4 *buf, uint64_t urec, uint64_t pstart, uint32_t nrec, uint32_t S,
+                                            FastDiv fw, bool ntl)
+{
+    const uint32_t blen = 4 * fw.d;
+    const uint64_t a = DIR == 0 ? urec : pstart, a16 = a & ~uint64_t(15);
+    const uint32_t head = uint32_t(a - a16);
+    const uint32_t nvec = (head + (DIR == 0 ? (nrec - 1) * S + blen : nrec * blen) + 15) / 16;
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(a16);
+    const uint32_t i0 = threadIdx.x, i1 = threadIdx.x + THREADS;
+    u32x4 v0, v1;
+    if (ntl) {
+        if (i0 < nvec) v0 = __builtin_nontemporal_load(src + i0);
+        if (i1 < nvec) v1 = __builtin_nontemporal_load(src + i1);
+    } else {
+        if (i0 < nvec) v0 = src[i0];
+        if (i1 < nvec) v1 = src[i1];
+    }
+    if (i0 < nvec) buf[i0] = v0;
+    if (i1 < nvec) buf[i1] = v1;
+    __syncthreads();
+    dense_write<DIR>(reinterpret_cast<const uint32_t *>(buf), head, nrec, blen, S, fw, pstart, urec);
+}
+
+// A task of one chunk (ddt_tune("dense", 1)): the workgroup finds its first record through the
+// item's FastDivs and the nest, then moves the chunk.  Returns false when the records cross a
+// run of the innermost dim (the caller runs the unit loop); a one-dim item never crosses (its
+// unit range lies inside its leaf).
+template <int DIR>
+__device__ __forceinline__ bool run_dense1(const Item *it, Bases bs, uint32_t ub, uint32_t ue, u32x4 *buf)
+{
+    const FastDiv fdu = it->fd_upb;
+    const uint32_t b0 = fastdiv(ub, fdu), nrec = fastdiv(ue - ub, fdu);
+    const uint32_t nd = it->ndim;
+    int64_t uo = 0, po = 0;
+    uint32_t blk = b0;
+    for (int j = int(nd) - 1; j > 0; --j) {
+        const uint32_t q = fastdiv(blk, it->fd[j]);
+        const uint32_t idx = blk - q * uint32_t(it->cnt[j]);
+        if (j == int(nd) - 1 && idx + nrec > uint32_t(it->cnt[j]))
+            return false;
+        blk = q;
+        uo += int64_t(idx) * it->ustr[j];
+        po += int64_t(idx) * it->pstr[j];
+    }
+    uo += int64_t(blk) * it->ustr[0];
+    po += int64_t(blk) * it->pstr[0];
+    dense_chunk<DIR>(buf, bs.u + it->user + uint64_t(uo), bs.p + it->packed + uint64_t(po), nrec,
+                     uint32_t(it->ustr[nd - 1]), it->fd_nblk, DIR == 1 || it->nt == 1);
+    return true;
+}
+
+// A task of several chunks: the next chunk's loads are issued before the current chunk is
+// written out (ddt_tune("dense", n) with n > 1).
+template <int DIR>
+__device__ __forceinline__ bool run_dense(const Item *it, Bases bs, uint32_t ub, uint32_t ue, u32x4 *buf)
+{
     uint32_t *lds = reinterpret_cast<uint32_t *>(buf);
     constexpr uint32_t NV = DENSE_LDS / 16 + 2, PER = (NV + THREADS - 1) / THREADS;   // 2 vectors / lane
     const uint32_t upb = uint32_t(it->upb), U = it->U;
@@ -256,49 +359,7 @@ __device__ __forceinline__ bool run_dense(const Item *it, Bases bs, uint32_t ub,
         __syncthreads();
         if (r0 + R < nrec)
             load(r0 + R, v);   // in flight while this chunk is written out
-        if (DIR == 0) {
-            const uint64_t pstart = pbase + uint64_t(r0) * blen;
-            const uint32_t pbytes = n * blen;
-            if ((pstart & 15) == 0 && (pbytes & 15) == 0) {
-                u32x4 *dst = reinterpret_cast<u32x4 *>(pstart);
-                for (uint32_t c = threadIdx.x; c < pbytes / 16; c += THREADS) {
-                    uint32_t w[4];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const uint32_t q = 4 * c + uint32_t(i), r = fastdiv(q, fw);
-                        w[i] = lds[(head + r * S) / 4 + (q - r * fw.d)];
-                    }
-                    dst[c] = u32x4{w[0], w[1], w[2], w[3]};
-                }
-            } else {
-                uint32_t *dst = reinterpret_cast<uint32_t *>(pstart);
-                for (uint32_t q = threadIdx.x; q < pbytes / 4; q += THREADS) {
-                    const uint32_t r = fastdiv(q, fw);
-                    dst[q] = lds[(head + r * S) / 4 + (q - r * fw.d)];
-                }
-            }
-        } else {
-            for (uint32_t r = threadIdx.x; r < n; r += THREADS) {
-                uint8_t *d = reinterpret_cast<uint8_t *>(ubase + uint64_t(r0 + r) * S);
-                const uint32_t l0 = (head + r * blen) / 4;
-                uint32_t o = 0;
-                // widest stores the record's alignment allows (every record is 4-byte aligned)
-                while (o < blen) {
-                    const uint64_t a = uint64_t(uintptr_t(d + o));
-                    const uint32_t w = l0 + o / 4;
-                    if ((a & 15) == 0 && blen - o >= 16) {
-                        *reinterpret_cast<u32x4 *>(d + o) = u32x4{lds[w], lds[w + 1], lds[w + 2], lds[w + 3]};
-                        o += 16;
-                    } else if ((a & 7) == 0 && blen - o >= 8) {
-                        *reinterpret_cast<u32x2 *>(d + o) = u32x2{lds[w], lds[w + 1]};
-                        o += 8;
-                    } else {
-                        *reinterpret_cast<uint32_t *>(d + o) = lds[w];
-                        o += 4;
-                    }
-                }
-            }
-        }
+        dense_write<DIR>(lds, head, n, blen, S, fw, pbase + uint64_t(r0) * blen, ubase + uint64_t(r0) * S);
     }
     return true;
 }
@@ -657,6 +718,7 @@ __device__ __forceinline__ void run_units_light(const Item *it, Bases bs, uint32
 template <int DIR, bool SPLIT>
 __device__ __forceinline__ void dense_body(const Item *__restrict__ items, uint32_t nitems, Bases bs, uint32_t ntasks)
 {
+    __shared__ u32x4 buf[DENSE_LDS / 16 + 2];   // one chunk's span (+ head alignment)
     const uint32_t nv = SPLIT ? (ntasks + 7) / 8 * 16 : ntasks;
     for (uint32_t b = blockIdx.x; b < nv; b += gridDim.x) {
         if (b != blockIdx.x)
@@ -676,7 +738,10 @@ __device__ __forceinline__ void dense_body(const Item *__restrict__ items, uint3
             if (ub >= ue)
                 continue;
         }
-        if (!run_dense<DIR>(it, bs, uint32_t(ub), uint32_t(ue)))
+        const bool moved = ue - ub <= it->nbytes * it->upb
+                               ? run_dense1<DIR>(it, bs, uint32_t(ub), uint32_t(ue), buf)
+                               : run_dense<DIR>(it, bs, uint32_t(ub), uint32_t(ue), buf);
+        if (!moved)
             run_units_light<DIR>(it, bs, uint32_t(ub), uint32_t(ue));
     }
 }
@@ -694,6 +759,44 @@ __global__ __launch_bounds__(THREADS) void ddt_dense_inline_kernel(ItemBlockN<NI
     const ItemBlockN<NI> *kb = reinterpret_cast<const ItemBlockN<NI> *>(
         (const void *) __builtin_amdgcn_kernarg_segment_ptr());
     dense_body<DIR, SPLIT>(kb->items, kb->n, Bases{kb->ubase, kb->pbase}, kb->ntasks);
+}
+
+// A single line-dense item whose chunks never cross a run of the innermost dim, launched with
+// its few fields BY VALUE (DenseArgs, ~170 bytes of kernel arguments: one batch of scalar loads)
+// and one workgroup per chunk, task structure and XCD slabs ignored.  Every cycle before a
+// workgroup's first load lengthens its ~2 us life, and at 8 workgroups per CU the chip's bytes
+// in flight shrink with it (Little's law).  On config 5's pack the engine's descriptor path --
+// kernarg -> item pointer -> item fields, the task search and slab remap, a branch between the
+// one- and multi-chunk routines, each a dependent round of scalar loads -- took 1142-1221 us
+// where the same chunk routine called with the fields at hand took 1100 and a bare kernel with
+// compile-time shape 1075 (scripts/ubench_dense4.hip, profiles/r3_ubench_dense4.log).
+// (DenseArgs: ddt_device.h)
+
+template <int DIR>
+__global__ __launch_bounds__(THREADS) void ddt_dense1_kernel(DenseArgs args)
+{
+    __shared__ u32x4 buf[DENSE_LDS / 16 + 2];
+    const DenseArgs *k = reinterpret_cast<const DenseArgs *>((const void *) __builtin_amdgcn_kernarg_segment_ptr());
+    const uint32_t ub = k->u0 + blockIdx.x * k->cu;
+    const uint32_t ue = min(ub + k->cu, k->u1);
+    const uint32_t b0 = fastdiv(ub, k->fdu), nrec = fastdiv(ue - ub, k->fdu);
+    const uint32_t nd = k->nd;
+    int64_t uo = 0, po = 0;
+    uint32_t blk = b0;
+#pragma unroll
+    for (int j = int(DENSE_ARG_DIMS) - 1; j > 0; --j) {
+        if (j < int(nd)) {
+            const uint32_t q = fastdiv(blk, k->fd[j]);
+            const uint32_t idx = blk - q * k->cnt[j];
+            blk = q;
+            uo += int64_t(idx) * k->ustr[j];
+            po += int64_t(idx) * k->pstr[j];
+        }
+    }
+    uo += int64_t(blk) * k->ustr[0];
+    po += int64_t(blk) * k->pstr[0];
+    dense_chunk<DIR>(buf, k->ubase + uint64_t(uo), k->pbase + uint64_t(po), nrec, uint32_t(k->ustr[nd - 1]), k->fw,
+                     DIR == 1 || k->nt == 1);
 }
 
 // One workgroup per task, or -- when the launch is capped below the task count (a window
@@ -780,6 +883,11 @@ static void launch_inline(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, 
         if (blk.n == 1) launch_dense_inline_n<DIRV, 1>(blk, ntasks, grid, ubase, pbase, stream, split); \
         else if (blk.n == 2) launch_dense_inline_n<DIRV, 2>(blk, ntasks, grid, ubase, pbase, stream, split); \
         else launch_dense_inline_n<DIRV, INLINE_ITEMS>(blk, ntasks, grid, ubase, pbase, stream, split); \
+        return hipGetLastError();                                                                       \
+    }                                                                                                   \
+    hipError_t launch_dense1_##TAG(const DenseArgs &a, uint32_t nchunks, hipStream_t stream)           \
+    {                                                                                                   \
+        hipLaunchKernelGGL((ddt_dense1_kernel<DIRV>), dim3(nchunks), dim3(THREADS), 0, stream, a);      \
         return hipGetLastError();                                                                       \
     }                                                                                                   \
     hipError_t launch_dense_##TAG(const Item *d_items, uint32_t nitems, uint32_t ntasks, uint32_t grid, \

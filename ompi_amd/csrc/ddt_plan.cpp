@@ -557,7 +557,9 @@ uint64_t dense_records(uint32_t U, uint64_t blen, const std::vector<LeafDim> &di
 // A line-dense task: TWO LDS chunks of R records.  One chunk per workgroup pays the task
 // prologue (the item's fields are scalar loads from HBM) for every 4 KiB; more chunks run in
 // sequence inside the workgroup.  cfg5, pack / unpack us (profiles/r3_ab_dense_chunks.jsonl):
-// 1 chunk 1483 / 1950, 2 chunks 1183 / 2043, 4 chunks 1237 / 2110, unit loop 1257 / 2071.
+// 1 chunk 1483 / 1950, 2 chunks 1183 / 2043, 4 chunks 1237 / 2110, unit loop 1257 / 2071 (the
+// unpack runs each task as two workgroups, dsplit: 1919).  A large single-item pack skips the
+// task structure altogether (launch_dense_by_value: a workgroup per chunk, fields by value).
 // Tasks start at multiples of their size from the item's first block, so a task size that
 // divides the innermost count (and an item starting on an inner-run boundary) keeps every task
 // inside one run; otherwise the crossing tasks fall back to the unit loop.

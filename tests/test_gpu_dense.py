@@ -10,7 +10,9 @@ opal_pack_homogeneous_contig_with_gaps_function), and the bytes must be identica
 Every shape here qualifies (ddt_plan.cpp dense_records), at record sizes 12..240 bytes,
 records 4- but not 16-byte aligned, counts whose instances break the record runs inside a
 task (the unit-loop fallback), fragment pipelines (the inline-descriptor kernel), both task
-mappings of the unpack (ddt_tune dsplit) and a capped grid over pinned host memory.
+mappings of the unpack (ddt_tune dsplit) and a capped grid over pinned host memory, and the
+by-value launch of a large single dense item (ddt_dense1_kernel, >= 1024 chunks: a workgroup per
+chunk, ddt_tune dfast) on one- and two-dim nests, 16- and 4-byte phases, both directions.
 """
 from __future__ import annotations
 
@@ -43,7 +45,7 @@ def knobs():
         for k, v in kv.items():
             L.ddt_tune(k.encode(), v)
     yield set_
-    set_(dense=-1, dsplit=1, hd_grid=256, hd_grid_pack=0)   # ddt_plan.h Tuning defaults
+    set_(dense=-1, dsplit=1, dfast=1, hd_grid=256, hd_grid_pack=0)   # ddt_plan.h Tuning defaults
 
 
 @pytest.mark.parametrize("dsplit", [1, 0])
@@ -124,3 +126,27 @@ def test_dense_records_pinned_capped_grid(device, knobs, dsplit):
     b.o.unpack(1, exp, origin, 0, ref.tobytes())
     assert ompi_amd.unpack(pk.data_ptr(), size, 0, out.data_ptr() + origin, 1, e) == size
     np.testing.assert_array_equal(out.cpu().numpy(), exp)
+
+
+BIG = {
+    # one dim: 1563 chunks of 128 records
+    "cfg5_rec_1d": (("hvector", 200_000, 1, 32, REC20), 1),
+    # two dims (instances of 131072 records, a multiple of the 128-record chunk): 2048 chunks
+    "cfg5_rec_2d": (("resized", ("hvector", 131_072, 1, 32, REC20), 0, 131_072 * 32 + 64), 2),
+    # 28-byte records every 36 bytes (113 per chunk, 4-byte phases): 2655 chunks
+    "f7_of_9_1d": (("vector", 300_000, 7, 9, ("basic", FLOAT4)), 1),
+    # two dims whose inner count is NOT a multiple of the chunk: the descriptor path instead
+    "cfg5_rec_2d_ragged": (("resized", ("hvector", 150_000, 1, 32, REC20), 0, 150_000 * 32 + 64), 2),
+}
+
+
+@pytest.mark.parametrize("dfast", [1, 3, 0])
+@pytest.mark.parametrize("name", sorted(BIG))
+def test_dense_by_value_launch(device, knobs, name, dfast):
+    """Large single-item dense launches: the by-value kernel for the pack (dfast 1, default),
+    both directions (3) or neither (0), aligned and 4 bytes off, bit-exact vs the oracle."""
+    knobs(dfast=dfast)
+    rec, count = BIG[name]
+    b = R.Built(rec)
+    _roundtrip(b, count, device, 61)
+    _roundtrip(b, count, device, 62, shift=4)
