@@ -17,7 +17,6 @@ struct SortedList {
     uint32_t seg = 0;        // elements per segment of U
     uint32_t segb = 64;      // segment bytes: 64 or 128
     uint32_t nc = 0, nb = 0; // chunks, buckets
-    uint32_t ncu = 256;      // CUs of the plan's device: the pipelined pack 1's grid
     uint64_t slots = 0;      // U slots, runs padded to whole segments
     uint64_t dev_bytes = 0;  // device bytes held (tables + U)
     uint32_t *A = nullptr;       // [n] element offset (units of esz) of the j-th block in address order

@@ -65,8 +65,6 @@ constexpr uint32_t POL_USER_NTL = 8;   // pack 1: user-side loads non-temporal
 // of pass 1 / 1' (the address-ordered gather or scatter), or its run phase (emit or load runs)
 constexpr uint32_t POL_SKIP_USER = 16;
 constexpr uint32_t POL_SKIP_RUNS = 32;
-// pack 1 in its one-workgroup-per-chunk form instead of the pipelined persistent one (k_pack1p)
-constexpr uint32_t POL_NO_PIPE = 64;
 
 template <typename T> __device__ __forceinline__ T ldp(const T *p, bool nt)
 {
@@ -310,100 +308,6 @@ __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, 
     emit_runs<E, SEGB>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, nts);
 }
 
-// pack pass 1, pipelined (the default; POL_NO_PIPE for the form above): one persistent
-// workgroup per CU loops over chunks c = blockIdx.x, + gridDim.x, ...  The chunk image fills the
-// CU's LDS, so in the one-workgroup-per-chunk form a CU runs its chunks strictly one after
-// another: the run emission of chunk c (stores only) and the gather of chunk c + 1 (dependent
-// load pairs) never overlap.  Here the next chunk's run tables and the first PF elements per
-// thread of its gather (slots and user elements, in registers: CH / PT = 32 / 16 / 8 elements
-// per thread for 4- / 8- / 16-byte elements, PF = min(that, 16)) are issued before the current
-// chunk's runs are emitted, so their latency is spent under the emission; the rest of the
-// gather (4-byte elements: the second half) runs in K-element rounds as in k_pack1.
-template <int E, int SEGB, int K>
-__global__ __launch_bounds__(PT) void k_pack1p(const uint8_t *__restrict__ user, const AddrList al,
-                                               const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
-                                               const uint32_t *__restrict__ ub, uint8_t *__restrict__ U, uint32_t n,
-                                               uint32_t nb, uint32_t nc, uint32_t pol)
-{
-    using T = typename Elem<E>::T;
-    constexpr uint32_t CH = LDS_BYTES / E, SEG = SEGB / E;
-    constexpr uint32_t PF = CH / PT < 16 ? CH / PT : 16;   // prefetched elements per thread
-    constexpr uint32_t NTAB = (MAXNB + PT - 1) / PT;       // run-table entries per thread
-    const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS, ntu = pol & POL_USER_NTL;
-    const bool gather = !(pol & POL_SKIP_USER);
-    __shared__ T lds[CH + SEG];
-    __shared__ uint16_t toff[MAXNB + 1];
-    __shared__ uint32_t tub[MAXNB];
-    const T *src = reinterpret_cast<const T *>(user);
-    T v[PF];
-    uint32_t s[PF];
-    uint32_t o16[NTAB], u32[NTAB];
-    auto fetch = [&](uint32_t c) {
-        const uint32_t j0 = c * CH, m = min(CH, n - j0);
-#pragma unroll
-        for (uint32_t i = 0; i < NTAB; ++i) {
-            const uint32_t k = threadIdx.x + i * PT;
-            if (k < nb) {
-                o16[i] = off16[size_t(c) * nb + k];
-                u32[i] = ub[size_t(c) * nb + k];
-            }
-        }
-        if (!gather)
-            return;
-#pragma unroll
-        for (uint32_t q = 0; q < PF; ++q) {
-            const uint32_t t = threadIdx.x + q * PT;
-            if (t < m) {
-                s[q] = ldp(&SL[j0 + t], ntl);
-                v[q] = ldp(&src[addr_at(al, j0 + t, ntl)], ntu);
-            }
-        }
-    };
-    uint32_t c = blockIdx.x;
-    if (c < nc)
-        fetch(c);
-    for (; c < nc; c += gridDim.x) {
-        const uint32_t j0 = c * CH, m = min(CH, n - j0);
-#pragma unroll
-        for (uint32_t i = 0; i < NTAB; ++i) {
-            const uint32_t k = threadIdx.x + i * PT;
-            if (k < nb) {
-                toff[k] = uint16_t(o16[i]);
-                tub[k] = u32[i];
-            }
-        }
-        if (threadIdx.x == 0)
-            toff[nb] = uint16_t(m);
-        if (gather) {
-#pragma unroll
-            for (uint32_t q = 0; q < PF; ++q)
-                if (threadIdx.x + q * PT < m)
-                    lds[s[q]] = v[q];
-            for (uint32_t t0 = threadIdx.x + PF * PT; t0 < m; t0 += PT * K) {
-                T w[K];
-                uint32_t r[K];
-#pragma unroll
-                for (int q = 0; q < K; ++q) {
-                    const uint32_t t = t0 + q * PT;
-                    if (t < m) {
-                        r[q] = ldp(&SL[j0 + t], ntl);
-                        w[q] = ldp(&src[addr_at(al, j0 + t, ntl)], ntu);
-                    }
-                }
-#pragma unroll
-                for (int q = 0; q < K; ++q)
-                    if (t0 + q * PT < m)
-                        lds[r[q]] = w[q];
-            }
-        }
-        __syncthreads();
-        if (c + gridDim.x < nc)
-            fetch(c + gridDim.x);   // in flight while this chunk's runs go out
-        emit_runs<E, SEGB>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, nts);
-        __syncthreads();   // the image and tables are free for the next chunk
-    }
-}
-
 // pack pass 2: the bucket's runs scatter into LDS by destination, then stream out
 template <int E, int K>
 __global__ __launch_bounds__(PT) void k_pack2(const uint8_t *__restrict__ U, const uint16_t *__restrict__ upos,
@@ -644,12 +548,6 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
     seg = segb / esz;
     nc = (n + ch - 1) / ch;
     nb = nc;   // RG == CH
-    {   // persistent pack-1 workgroups: one per CU (the chunk image fills a CU's LDS)
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) == hipSuccess
-            && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-            ncu = uint32_t(cus);
-    }
     uint32_t shift = 0;
     while ((1u << shift) < esz)
         ++shift;
@@ -764,16 +662,12 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol
         if (e != hipSuccess)
             return e;
     }
-    const dim3 gc(nc), gb(nb), blk(PT), gp(std::min(nc, ncu));
+    const dim3 gc(nc), gb(nb), blk(PT);
     const AddrList al{A, A16, Abase};
     uint8_t *u8 = static_cast<uint8_t *>(U);
 #define DDT_SORTED_LAUNCH_K(E, SB, K)                                                                           \
     if (dir == 0) {                                                                                             \
-        if (pol & POL_NO_PIPE)                                                                                  \
-            hipLaunchKernelGGL((k_pack1<E, SB, K>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol); \
-        else                                                                                                    \
-            hipLaunchKernelGGL((k_pack1p<E, SB, K>), gp, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, nc, \
-                               pol);                                                                            \
+        hipLaunchKernelGGL((k_pack1<E, SB, K>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);  \
         launch_pass2<E, 0>(gb, blk, stream, u8, upos, bstart, packed, n, pol, k2);                             \
     } else {                                                                                                    \
         launch_pass2<E, 1>(gb, blk, stream, packed, upos, bstart, u8, n, pol, k2);                             \
