@@ -40,8 +40,10 @@ hipError_t launch_dense_inline_p0(const ItemBlock &, uint32_t, uint32_t, uint64_
 hipError_t launch_dense_inline_u0(const ItemBlock &, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t, bool);
 hipError_t launch_dense_p0(const Item *, uint32_t, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t, bool);
 hipError_t launch_dense_u0(const Item *, uint32_t, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t, bool);
-hipError_t launch_dense1_p0(const DenseArgs &, uint32_t, hipStream_t);
-hipError_t launch_dense1_u0(const DenseArgs &, uint32_t, hipStream_t);
+hipError_t launch_dense1_p0(const ItemArgs &, uint32_t, hipStream_t);
+hipError_t launch_dense1_u0(const ItemArgs &, uint32_t, hipStream_t);
+hipError_t launch_affine1_p0(const ItemArgs &, uint32_t, int, hipStream_t);
+hipError_t launch_affine1_u0(const ItemArgs &, uint32_t, int, hipStream_t);
 
 // The line-dense unpack runs each task as two workgroups (ddt_tune "dsplit", dense_body):
 // 16 workgroups per 8 tasks.
@@ -55,28 +57,23 @@ static uint32_t dense_grid(bool split, uint32_t ntasks, uint32_t grid_cap)
     return grid_cap && grid_cap < nv ? grid_cap : nv;
 }
 
-// The by-value single-item line-dense launch (ddt_dense1_kernel): a large launch of one dense
-// item whose chunks all lie inside one run of the innermost dim.  Returns false when the item
-// does not qualify (the caller launches the descriptor set as usual).  Small launches keep the
-// descriptor path: ~170 bytes of kernel arguments cost ~1 us more host time per launch than a
-// descriptor pointer (device-resident kernel arguments, profiles/r1_hostbench.log).
-bool launch_dense_by_value(const Item &it, int dir, uint64_t ubase, uint64_t pbase, hipStream_t stream,
-                           hipError_t *err)
+// The by-value single-item launches: a large launch of ONE affine item whose fields travel in the
+// kernel arguments (ItemArgs) instead of a descriptor in memory, one workgroup per chunk or task:
+//   * a line-dense item whose chunks all lie inside one run of the innermost dim
+//     (ddt_dense1_kernel; ddt_tune "dfast", default: pack);
+//   * a streaming item of 16-byte units with plain stores (ddt_affine1_kernel; "afast").
+// Returns false when the item does not qualify (the caller launches the descriptor set as
+// usual).  Small launches keep the descriptor path: ~170 bytes of kernel arguments cost ~1 us
+// more host time per launch than a descriptor pointer (device-resident kernel arguments,
+// profiles/r1_hostbench.log).
+static bool fill_args(const Item &it, uint64_t ubase, uint64_t pbase, uint64_t cu, ItemArgs &a)
 {
-    if (!(tuning().dfast & (dir == 0 ? 1 : 2)))
+    if (it.kind != ITEM_AFFINE || it.idx64 || it.ndim < 1 || it.ndim > ITEM_ARG_DIMS || it.upb == 0 || cu == 0)
         return false;
-    if (it.kind != ITEM_AFFINE || !it.nbytes || it.idx64 || it.ndim < 1 || it.ndim > DENSE_ARG_DIMS || it.upb == 0)
+    const uint64_t n = (it.u1 - it.u0 + cu - 1) / cu;
+    if (n < 1024 || n >= 0x7fffffffull || cu >= 0xffffffffull)
         return false;
-    const uint64_t R = it.nbytes, cu = R * it.upb;
-    const uint64_t cin = it.cnt[it.ndim - 1];
-    if (it.u0 % it.upb != 0)
-        return false;
-    if (it.ndim > 1 && (cin % R != 0 || ((it.u0 / it.upb) % cin) % R != 0))
-        return false;   // a chunk could cross an inner run
-    const uint64_t nch = (it.u1 - it.u0 + cu - 1) / cu;
-    if (nch < 1024 || nch >= 0x7fffffffull || cu >= 0xffffffffull)
-        return false;
-    DenseArgs a{};
+    a = ItemArgs{};
     a.ubase = ubase + it.user;
     a.pbase = pbase + it.packed;
     a.u0 = uint32_t(it.u0);
@@ -92,7 +89,36 @@ bool launch_dense_by_value(const Item &it, int dir, uint64_t ubase, uint64_t pba
         a.ustr[j] = it.ustr[j];
         a.pstr[j] = it.pstr[j];
     }
-    *err = dir == 0 ? launch_dense1_p0(a, uint32_t(nch), stream) : launch_dense1_u0(a, uint32_t(nch), stream);
+    return true;
+}
+
+bool launch_single_item(const Item &it, int dir, uint64_t ubase, uint64_t pbase, hipStream_t stream,
+                        hipError_t *err)
+{
+    const int bit = dir == 0 ? 1 : 2;
+    ItemArgs a;
+    if (it.kind != ITEM_AFFINE || it.upb == 0)
+        return false;
+    if (it.nbytes) {   // line-dense (Item::nbytes = records per chunk)
+        if (!(tuning().dfast & bit) || it.u0 % it.upb != 0)
+            return false;
+        const uint64_t R = it.nbytes, cin = it.cnt[it.ndim ? it.ndim - 1 : 0];
+        if (it.ndim > 1 && (cin % R != 0 || ((it.u0 / it.upb) % cin) % R != 0))
+            return false;   // a chunk could cross an inner run
+        if (!fill_args(it, ubase, pbase, R * it.upb, a))
+            return false;
+        const uint32_t n = uint32_t((it.u1 - it.u0 + a.cu - 1) / a.cu);
+        *err = dir == 0 ? launch_dense1_p0(a, n, stream) : launch_dense1_u0(a, n, stream);
+        return true;
+    }
+    if (!(tuning().afast & bit) || it.U != 16 || it.wt != 0 || (it.nt != 0 && it.nt != 3)
+        || (it.slab != 0 && it.slab != SLAB_FULL))
+        return false;
+    if (!fill_args(it, ubase, pbase, it.units_per_task, a))
+        return false;
+    a.slab = it.slab;
+    const uint32_t n = uint32_t((it.u1 - it.u0 + a.cu - 1) / a.cu);
+    *err = dir == 0 ? launch_affine1_p0(a, n, int(it.nt), stream) : launch_affine1_u0(a, n, int(it.nt), stream);
     return true;
 }
 

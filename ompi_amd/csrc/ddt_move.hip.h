@@ -762,7 +762,7 @@ __global__ __launch_bounds__(THREADS) void ddt_dense_inline_kernel(ItemBlockN<NI
 }
 
 // A single line-dense item whose chunks never cross a run of the innermost dim, launched with
-// its few fields BY VALUE (DenseArgs, ~170 bytes of kernel arguments: one batch of scalar loads)
+// its few fields BY VALUE (ItemArgs, ~170 bytes of kernel arguments: one batch of scalar loads)
 // and one workgroup per chunk, task structure and XCD slabs ignored.  Every cycle before a
 // workgroup's first load lengthens its ~2 us life, and at 8 workgroups per CU the chip's bytes
 // in flight shrink with it (Little's law).  On config 5's pack the engine's descriptor path --
@@ -770,13 +770,13 @@ __global__ __launch_bounds__(THREADS) void ddt_dense_inline_kernel(ItemBlockN<NI
 // one- and multi-chunk routines, each a dependent round of scalar loads -- took 1142-1221 us
 // where the same chunk routine called with the fields at hand took 1100 and a bare kernel with
 // compile-time shape 1075 (scripts/ubench_dense4.hip, profiles/r3_ubench_dense4.log).
-// (DenseArgs: ddt_device.h)
+// (ItemArgs: ddt_device.h)
 
 template <int DIR>
-__global__ __launch_bounds__(THREADS) void ddt_dense1_kernel(DenseArgs args)
+__global__ __launch_bounds__(THREADS) void ddt_dense1_kernel(ItemArgs args)
 {
     __shared__ u32x4 buf[DENSE_LDS / 16 + 2];
-    const DenseArgs *k = reinterpret_cast<const DenseArgs *>((const void *) __builtin_amdgcn_kernarg_segment_ptr());
+    const ItemArgs *k = reinterpret_cast<const ItemArgs *>((const void *) __builtin_amdgcn_kernarg_segment_ptr());
     const uint32_t ub = k->u0 + blockIdx.x * k->cu;
     const uint32_t ue = min(ub + k->cu, k->u1);
     const uint32_t b0 = fastdiv(ub, k->fdu), nrec = fastdiv(ue - ub, k->fdu);
@@ -784,7 +784,7 @@ __global__ __launch_bounds__(THREADS) void ddt_dense1_kernel(DenseArgs args)
     int64_t uo = 0, po = 0;
     uint32_t blk = b0;
 #pragma unroll
-    for (int j = int(DENSE_ARG_DIMS) - 1; j > 0; --j) {
+    for (int j = int(ITEM_ARG_DIMS) - 1; j > 0; --j) {
         if (j < int(nd)) {
             const uint32_t q = fastdiv(blk, k->fd[j]);
             const uint32_t idx = blk - q * k->cnt[j];
@@ -797,6 +797,61 @@ __global__ __launch_bounds__(THREADS) void ddt_dense1_kernel(DenseArgs args)
     po += int64_t(blk) * k->pstr[0];
     dense_chunk<DIR>(buf, k->ubase + uint64_t(uo), k->pbase + uint64_t(po), nrec, uint32_t(k->ustr[nd - 1]), k->fw,
                      DIR == 1 || k->nt == 1);
+}
+
+// A single affine item of 16-byte units (the streaming leaves: a y or z face over many fields,
+// runs of >= 256 B) launched with its fields by value, one workgroup per task: the same unit loop
+// as run_affine, without the descriptor chase (kernarg -> item pointer -> item fields -> task
+// search) ahead of the first load; the XCD slab remap is arithmetic on the workgroup index.  NT as
+// run_affine (0 plain, 3 non-temporal loads).
+template <int DIR, int NT>
+__global__ __launch_bounds__(THREADS) void ddt_affine1_kernel(ItemArgs args)
+{
+    using T = u32x4;
+    constexpr int U = 16, K = unroll_of(16);
+    const ItemArgs *k = reinterpret_cast<const ItemArgs *>((const void *) __builtin_amdgcn_kernarg_segment_ptr());
+    uint32_t t = blockIdx.x;
+    if (k->slab) {   // one contiguous slab of tasks per XCD, as locate_task (arithmetic only)
+        const uint32_t T = gridDim.x, x = t & 7u, i = t >> 3, per = T >> 3, rem = T & 7u;
+        t = x * per + (x < rem ? x : rem) + i;
+    }
+    const uint32_t ub = k->u0 + t * k->cu;
+    const uint32_t ue = min(ub + k->cu, k->u1);
+    const FastDiv fdu = k->fdu;
+    const uint32_t upb = fdu.d, nd = k->nd;
+    for (uint32_t base = ub + threadIdx.x; base < ue; base += THREADS * K) {
+        T v[K];
+        T *dst[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const uint32_t u = base + uint32_t(q) * THREADS;
+            dst[q] = nullptr;
+            if (u < ue) {
+                uint32_t blk = fastdiv(u, fdu);
+                const uint32_t within = u - blk * upb;
+                int64_t uo = int64_t(within) * U, po = uo;
+#pragma unroll
+                for (int j = int(ITEM_ARG_DIMS) - 1; j > 0; --j) {
+                    if (j < int(nd)) {
+                        const uint32_t qq = fastdiv(blk, k->fd[j]);
+                        const uint32_t idx = blk - qq * k->cnt[j];
+                        blk = qq;
+                        uo += int64_t(idx) * k->ustr[j];
+                        po += int64_t(idx) * k->pstr[j];
+                    }
+                }
+                uo += int64_t(blk) * k->ustr[0];
+                po += int64_t(blk) * k->pstr[0];
+                const T *src = reinterpret_cast<const T *>(DIR == 0 ? k->ubase + uo : k->pbase + po);
+                dst[q] = reinterpret_cast<T *>(DIR == 0 ? k->pbase + po : k->ubase + uo);
+                v[q] = ld<T, NT == 3>(src);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            if (dst[q])
+                *dst[q] = v[q];
+    }
 }
 
 // One workgroup per task, or -- when the launch is capped below the task count (a window
@@ -885,9 +940,17 @@ static void launch_inline(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, 
         else launch_dense_inline_n<DIRV, INLINE_ITEMS>(blk, ntasks, grid, ubase, pbase, stream, split); \
         return hipGetLastError();                                                                       \
     }                                                                                                   \
-    hipError_t launch_dense1_##TAG(const DenseArgs &a, uint32_t nchunks, hipStream_t stream)           \
+    hipError_t launch_dense1_##TAG(const ItemArgs &a, uint32_t nchunks, hipStream_t stream)            \
     {                                                                                                   \
         hipLaunchKernelGGL((ddt_dense1_kernel<DIRV>), dim3(nchunks), dim3(THREADS), 0, stream, a);      \
+        return hipGetLastError();                                                                       \
+    }                                                                                                   \
+    hipError_t launch_affine1_##TAG(const ItemArgs &a, uint32_t ntasks, int nt, hipStream_t stream)     \
+    {                                                                                                   \
+        if (nt == 3)                                                                                    \
+            hipLaunchKernelGGL((ddt_affine1_kernel<DIRV, 3>), dim3(ntasks), dim3(THREADS), 0, stream, a); \
+        else                                                                                            \
+            hipLaunchKernelGGL((ddt_affine1_kernel<DIRV, 0>), dim3(ntasks), dim3(THREADS), 0, stream, a); \
         return hipGetLastError();                                                                       \
     }                                                                                                   \
     hipError_t launch_dense_##TAG(const Item *d_items, uint32_t nitems, uint32_t ntasks, uint32_t grid, \

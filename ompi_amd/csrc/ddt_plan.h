@@ -32,6 +32,7 @@ struct Tuning {
     int dsplit = 1;       // line-dense unpack: each task as two workgroups (dense_body SPLIT)
     int dfast = 1;        // single-item line-dense launches by value, a workgroup per chunk
                           // (ddt_dense1_kernel): bit 0 pack, bit 1 unpack
+    int afast = 0;        // single-item streaming launches by value (ddt_affine1_kernel): bits as dfast
     int hostdirect = 3;   // pinned host iovecs moved by the kernel itself over PCIe (no HBM
                           // staging): bit 0 unpack, bit 1 pack (end to end)
     long stage_mb = 256;  // HBM staging buffer (one per convertor) for pageable host iovecs: the
@@ -65,8 +66,8 @@ uint32_t total_tasks(const std::vector<Item> &items);
 // dense: every item is line-dense (Item::nbytes), run by the dedicated dense kernel
 hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, uint64_t ubase,
                               uint64_t pbase, hipStream_t stream, uint32_t grid_cap = 0, bool dense = false);
-bool launch_dense_by_value(const Item &it, int dir, uint64_t ubase, uint64_t pbase, hipStream_t stream,
-                           hipError_t *err);
+bool launch_single_item(const Item &it, int dir, uint64_t ubase, uint64_t pbase, hipStream_t stream,
+                        hipError_t *err);
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
                        uint64_t ubase, uint64_t pbase, hipStream_t stream, uint32_t grid_cap = 0,
                        bool dense = false);

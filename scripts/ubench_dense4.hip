@@ -212,7 +212,7 @@ int main(int argc, char **argv)
         if (!round) check("r1");
         printf("R1  engine run_dense1 from a minimal kernel   : %7.1f us (%4.0f GB/s)\n", t, gbs(t));
         {
-            DenseArgs da{};
+            ItemArgs da{};
             da.ubase = ub; da.pbase = pb; da.u0 = uint32_t(base.u0); da.u1 = uint32_t(base.u1);
             da.cu = uint32_t(R * base.upb); da.nd = base.ndim; da.fdu = base.fd_upb; da.fw = base.fd_nblk;
             da.nt = base.nt;
