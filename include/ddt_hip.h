@@ -330,8 +330,7 @@ int ddt_debug_host_window(const void *p, size_t n, uint64_t *device_addr);
  * streaming task (0, default: spass passes); "dense" = line-dense records moved through LDS
  * with whole-line accesses (-1 auto, 0 off, n chunks per task); "dsplit" = such an unpack runs
  * each task as two workgroups (1 default, 0 off); "dfast" = a large single-item line-dense launch
- * passes its fields by value, one workgroup per chunk (bit 0 pack, default; bit 1 unpack); "afast" =
- * the same for a large single streaming item of 16-byte units (bits as dfast); "hostdirect" =
+ * passes its fields by value, one workgroup per chunk (bit 0 pack, default; bit 1 unpack); "hostdirect" =
  * pinned host iovecs moved by the kernel over PCIe (bit 0 unpack, bit 1 pack; 3 default, 0 =
  * HBM staging); "hd_grid" / "hd_grid_pack" = workgroup cap of such an unpack / pack launch (256 / 0 default,
  * 0 none); "stage_mb" =

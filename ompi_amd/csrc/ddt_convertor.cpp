@@ -403,7 +403,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     if (S->items.empty())
         return DDT_SUCCESS;
     if (S->items.size() == 1 && grid_cap == 0) {
-        // a large single-item launch carries the item's fields by value (no descriptor)
+        // a large single-item line-dense launch carries the item's fields by value
         hipError_t e = hipSuccess;
         if (launch_single_item(S->items[0], dir, ubase, pbase, stream, &e)) {
             HIPCHK(e);
@@ -1658,8 +1658,6 @@ int ddt_tune(const char *key, long value)
         tuning().snt = value < -1 ? -2 : (value < 0 ? -1 : (value >= 3 && value <= 5 ? int(value) : (value ? 1 : 0)));
     else if (k == "dfast")
         tuning().dfast = int(value & 3);
-    else if (k == "afast")
-        tuning().afast = int(value & 3);
     else if (k == "dense")
         tuning().dense = value < 0 ? -1 : int(value);
     else if (k == "stask")

@@ -113,14 +113,14 @@ static_assert(sizeof(Item) == 512, "Item layout is shared with tests/plan_emu.py
 static_assert(sizeof(ItemBlock) <= 4096, "kernel argument segment limit");
 
 // One affine item's fields passed BY VALUE in the kernel arguments (~170 bytes: one batch of
-// scalar loads, no descriptor pointer to chase): the single-item launches of ddt_dense1_kernel
-// and ddt_affine1_kernel (launch_single_item, ddt_kernels.hip).
+// scalar loads, no descriptor pointer to chase): the single-item line-dense launch of
+// ddt_dense1_kernel (launch_single_item, ddt_kernels.hip).
 struct ItemArgs {
     uint64_t ubase, pbase;      // user / packed address of the item's unit 0
     uint32_t u0, u1;            // unit range of the item
     uint32_t cu, nd;            // units per workgroup (dense: one chunk of R records); dims in use
     FastDiv fdu, fw;            // units per block; (dense) 4-byte words per record
-    uint32_t nt, slab;          // Item::nt; Item::slab (0 or SLAB_FULL: one XCD slab of tasks each)
+    uint32_t nt, pad;           // Item::nt
     uint32_t cnt[4];
     FastDiv fd[4];
     int64_t ustr[4], pstr[4];

@@ -42,8 +42,6 @@ hipError_t launch_dense_p0(const Item *, uint32_t, uint32_t, uint32_t, uint64_t,
 hipError_t launch_dense_u0(const Item *, uint32_t, uint32_t, uint32_t, uint64_t, uint64_t, hipStream_t, bool);
 hipError_t launch_dense1_p0(const ItemArgs &, uint32_t, hipStream_t);
 hipError_t launch_dense1_u0(const ItemArgs &, uint32_t, hipStream_t);
-hipError_t launch_affine1_p0(const ItemArgs &, uint32_t, int, hipStream_t);
-hipError_t launch_affine1_u0(const ItemArgs &, uint32_t, int, hipStream_t);
 
 // The line-dense unpack runs each task as two workgroups (ddt_tune "dsplit", dense_body):
 // 16 workgroups per 8 tasks.
@@ -57,15 +55,17 @@ static uint32_t dense_grid(bool split, uint32_t ntasks, uint32_t grid_cap)
     return grid_cap && grid_cap < nv ? grid_cap : nv;
 }
 
-// The by-value single-item launches: a large launch of ONE affine item whose fields travel in the
-// kernel arguments (ItemArgs) instead of a descriptor in memory, one workgroup per chunk or task:
-//   * a line-dense item whose chunks all lie inside one run of the innermost dim
-//     (ddt_dense1_kernel; ddt_tune "dfast", default: pack);
-//   * a streaming item of 16-byte units with plain stores (ddt_affine1_kernel; "afast").
-// Returns false when the item does not qualify (the caller launches the descriptor set as
-// usual).  Small launches keep the descriptor path: ~170 bytes of kernel arguments cost ~1 us
-// more host time per launch than a descriptor pointer (device-resident kernel arguments,
-// profiles/r1_hostbench.log).
+// The by-value single-item launch: a large launch of ONE line-dense item whose chunks all lie
+// inside one run of the innermost dim passes the item's fields in the kernel arguments (ItemArgs)
+// instead of a descriptor in memory, one workgroup per chunk (ddt_dense1_kernel; ddt_tune
+// "dfast", default: pack).  Returns false when the item does not qualify (the caller launches the
+// descriptor set as usual).  Small launches keep the descriptor path: ~170 bytes of kernel
+// arguments cost ~1 us more host time per launch than a descriptor pointer (device-resident
+// kernel arguments, profiles/r1_hostbench.log).  The same launch form for streaming items of
+// 16-byte units (a y or z face over 512 fields) was built and measured within box noise of the
+// descriptor kernel, its unpacks slower (commit 05bf71b, profiles/r3_ubench_face1.log,
+// r3_ab_faces_afast.jsonl), and dropped: a 16 KiB streaming task hides its prologue, a 4 KiB
+// dense chunk does not.
 static bool fill_args(const Item &it, uint64_t ubase, uint64_t pbase, uint64_t cu, ItemArgs &a)
 {
     if (it.kind != ITEM_AFFINE || it.idx64 || it.ndim < 1 || it.ndim > ITEM_ARG_DIMS || it.upb == 0 || cu == 0)
@@ -95,30 +95,18 @@ static bool fill_args(const Item &it, uint64_t ubase, uint64_t pbase, uint64_t c
 bool launch_single_item(const Item &it, int dir, uint64_t ubase, uint64_t pbase, hipStream_t stream,
                         hipError_t *err)
 {
-    const int bit = dir == 0 ? 1 : 2;
+    // line-dense only (Item::nbytes = records per chunk)
+    if (it.kind != ITEM_AFFINE || it.upb == 0 || !it.nbytes || !(tuning().dfast & (dir == 0 ? 1 : 2))
+        || it.u0 % it.upb != 0)
+        return false;
+    const uint64_t R = it.nbytes, cin = it.cnt[it.ndim ? it.ndim - 1 : 0];
+    if (it.ndim > 1 && (cin % R != 0 || ((it.u0 / it.upb) % cin) % R != 0))
+        return false;   // a chunk could cross an inner run
     ItemArgs a;
-    if (it.kind != ITEM_AFFINE || it.upb == 0)
+    if (!fill_args(it, ubase, pbase, R * it.upb, a))
         return false;
-    if (it.nbytes) {   // line-dense (Item::nbytes = records per chunk)
-        if (!(tuning().dfast & bit) || it.u0 % it.upb != 0)
-            return false;
-        const uint64_t R = it.nbytes, cin = it.cnt[it.ndim ? it.ndim - 1 : 0];
-        if (it.ndim > 1 && (cin % R != 0 || ((it.u0 / it.upb) % cin) % R != 0))
-            return false;   // a chunk could cross an inner run
-        if (!fill_args(it, ubase, pbase, R * it.upb, a))
-            return false;
-        const uint32_t n = uint32_t((it.u1 - it.u0 + a.cu - 1) / a.cu);
-        *err = dir == 0 ? launch_dense1_p0(a, n, stream) : launch_dense1_u0(a, n, stream);
-        return true;
-    }
-    if (!(tuning().afast & bit) || it.U != 16 || it.wt != 0 || (it.nt != 0 && it.nt != 3)
-        || (it.slab != 0 && it.slab != SLAB_FULL))
-        return false;
-    if (!fill_args(it, ubase, pbase, it.units_per_task, a))
-        return false;
-    a.slab = it.slab;
     const uint32_t n = uint32_t((it.u1 - it.u0 + a.cu - 1) / a.cu);
-    *err = dir == 0 ? launch_affine1_p0(a, n, int(it.nt), stream) : launch_affine1_u0(a, n, int(it.nt), stream);
+    *err = dir == 0 ? launch_dense1_p0(a, n, stream) : launch_dense1_u0(a, n, stream);
     return true;
 }
 

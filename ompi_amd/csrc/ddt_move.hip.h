@@ -799,61 +799,6 @@ __global__ __launch_bounds__(THREADS) void ddt_dense1_kernel(ItemArgs args)
                      DIR == 1 || k->nt == 1);
 }
 
-// A single affine item of 16-byte units (the streaming leaves: a y or z face over many fields,
-// runs of >= 256 B) launched with its fields by value, one workgroup per task: the same unit loop
-// as run_affine, without the descriptor chase (kernarg -> item pointer -> item fields -> task
-// search) ahead of the first load; the XCD slab remap is arithmetic on the workgroup index.  NT as
-// run_affine (0 plain, 3 non-temporal loads).
-template <int DIR, int NT>
-__global__ __launch_bounds__(THREADS) void ddt_affine1_kernel(ItemArgs args)
-{
-    using T = u32x4;
-    constexpr int U = 16, K = unroll_of(16);
-    const ItemArgs *k = reinterpret_cast<const ItemArgs *>((const void *) __builtin_amdgcn_kernarg_segment_ptr());
-    uint32_t t = blockIdx.x;
-    if (k->slab) {   // one contiguous slab of tasks per XCD, as locate_task (arithmetic only)
-        const uint32_t T = gridDim.x, x = t & 7u, i = t >> 3, per = T >> 3, rem = T & 7u;
-        t = x * per + (x < rem ? x : rem) + i;
-    }
-    const uint32_t ub = k->u0 + t * k->cu;
-    const uint32_t ue = min(ub + k->cu, k->u1);
-    const FastDiv fdu = k->fdu;
-    const uint32_t upb = fdu.d, nd = k->nd;
-    for (uint32_t base = ub + threadIdx.x; base < ue; base += THREADS * K) {
-        T v[K];
-        T *dst[K];
-#pragma unroll
-        for (int q = 0; q < K; ++q) {
-            const uint32_t u = base + uint32_t(q) * THREADS;
-            dst[q] = nullptr;
-            if (u < ue) {
-                uint32_t blk = fastdiv(u, fdu);
-                const uint32_t within = u - blk * upb;
-                int64_t uo = int64_t(within) * U, po = uo;
-#pragma unroll
-                for (int j = int(ITEM_ARG_DIMS) - 1; j > 0; --j) {
-                    if (j < int(nd)) {
-                        const uint32_t qq = fastdiv(blk, k->fd[j]);
-                        const uint32_t idx = blk - qq * k->cnt[j];
-                        blk = qq;
-                        uo += int64_t(idx) * k->ustr[j];
-                        po += int64_t(idx) * k->pstr[j];
-                    }
-                }
-                uo += int64_t(blk) * k->ustr[0];
-                po += int64_t(blk) * k->pstr[0];
-                const T *src = reinterpret_cast<const T *>(DIR == 0 ? k->ubase + uo : k->pbase + po);
-                dst[q] = reinterpret_cast<T *>(DIR == 0 ? k->pbase + po : k->ubase + uo);
-                v[q] = ld<T, NT == 3>(src);
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < K; ++q)
-            if (dst[q])
-                *dst[q] = v[q];
-    }
-}
-
 // One workgroup per task, or -- when the launch is capped below the task count (a window
 // in pinned host memory, where PCIe and not the CU count is the limit: a few hundred
 // workgroups keep it full, thousands of them contend for it, scripts/ubench_pcie.hip) --
@@ -943,14 +888,6 @@ static void launch_inline(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, 
     hipError_t launch_dense1_##TAG(const ItemArgs &a, uint32_t nchunks, hipStream_t stream)            \
     {                                                                                                   \
         hipLaunchKernelGGL((ddt_dense1_kernel<DIRV>), dim3(nchunks), dim3(THREADS), 0, stream, a);      \
-        return hipGetLastError();                                                                       \
-    }                                                                                                   \
-    hipError_t launch_affine1_##TAG(const ItemArgs &a, uint32_t ntasks, int nt, hipStream_t stream)     \
-    {                                                                                                   \
-        if (nt == 3)                                                                                    \
-            hipLaunchKernelGGL((ddt_affine1_kernel<DIRV, 3>), dim3(ntasks), dim3(THREADS), 0, stream, a); \
-        else                                                                                            \
-            hipLaunchKernelGGL((ddt_affine1_kernel<DIRV, 0>), dim3(ntasks), dim3(THREADS), 0, stream, a); \
         return hipGetLastError();                                                                       \
     }                                                                                                   \
     hipError_t launch_dense_##TAG(const Item *d_items, uint32_t nitems, uint32_t ntasks, uint32_t grid, \

@@ -32,7 +32,6 @@ struct Tuning {
     int dsplit = 1;       // line-dense unpack: each task as two workgroups (dense_body SPLIT)
     int dfast = 1;        // single-item line-dense launches by value, a workgroup per chunk
                           // (ddt_dense1_kernel): bit 0 pack, bit 1 unpack
-    int afast = 0;        // single-item streaming launches by value (ddt_affine1_kernel): bits as dfast
     int hostdirect = 3;   // pinned host iovecs moved by the kernel itself over PCIe (no HBM
                           // staging): bit 0 unpack, bit 1 pack (end to end)
     long stage_mb = 256;  // HBM staging buffer (one per convertor) for pageable host iovecs: the

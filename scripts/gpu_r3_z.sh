@@ -2,8 +2,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 120 ./scripts/ubench_face1 10 > gpurun_out/r3z_ubench_face1.log 2>&1 || exit $?
-cat gpurun_out/r3z_ubench_face1.log
 : > gpurun_out/r3z_ab_faces.jsonl
 for f in y z; do
   timeout -k 10 400 python3 scripts/ab.py --config $f --count 512 --rounds 3 --steps 6 --mode pair --flush read --variants "afast=0,afast=3,afast=1" >> gpurun_out/r3z_ab_faces.jsonl 2>>gpurun_out/r3z.err || exit $?
