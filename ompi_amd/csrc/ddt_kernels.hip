@@ -71,7 +71,8 @@ static bool fill_args(const Item &it, uint64_t ubase, uint64_t pbase, uint64_t c
     if (it.kind != ITEM_AFFINE || it.idx64 || it.ndim < 1 || it.ndim > ITEM_ARG_DIMS || it.upb == 0 || cu == 0)
         return false;
     const uint64_t n = (it.u1 - it.u0 + cu - 1) / cu;
-    if (n < 1024 || n >= 0x7fffffffull || cu >= 0xffffffffull)
+    // the kernel's 32-bit unit arithmetic: the last chunk's end (u0 + n * cu) must not wrap
+    if (n < 1024 || n >= 0x7fffffffull || it.u0 + n * cu >= 0xffffffffull)
         return false;
     a = ItemArgs{};
     a.ubase = ubase + it.user;

@@ -41,7 +41,7 @@ def main():
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"]
         if "ddt_move" in k or "ddt_dense" in k:
-            d = "pack" if "<0," in k else "unpack"
+            d = "pack" if ("<0," in k or "<0>" in k) else "unpack"
         elif "k_pack" in k or "k_unpack" in k:
             d = "pack" if "k_pack" in k else "unpack"
         else:

@@ -37,7 +37,7 @@ def per_kernel(path, counter):
         if r["Counter_Name"] != counter:
             continue
         if "ddt_move" in k or "ddt_dense" in k:
-            direction = "pack" if "<0," in k else "unpack"
+            direction = "pack" if ("<0," in k or "<0>" in k) else "unpack"
         elif "k_pack" in k or "k_unpack" in k:
             direction = "pack" if "k_pack" in k else "unpack"
         else:
