@@ -431,6 +431,13 @@ def main():
         rc = subprocess.call(self_launch_argv(args.gpus, sys.argv[1:], free_port()))
         sys.exit(rc)
 
+    # stdout carries exactly ONE line, the JSON result of rank 0: everything else the process (or
+    # a library below it: gloo reports its peer connections on stdout) writes to fd 1 goes to
+    # stderr, and the result is written to the saved descriptor at the end
+    sys.stdout.flush()
+    result_fd = os.dup(1)
+    os.dup2(2, 1)
+
     import torch
     import torch.distributed as dist
 
@@ -649,7 +656,8 @@ def main():
     elif rank == 0:
         result["cpu_baseline"] = None   # timed on rank 0 at N = 1 only
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        sys.stdout.flush()
+        os.write(result_fd, (json.dumps(result) + "\n").encode())
     if world > 1:
         dist.destroy_process_group()
 
