@@ -1,0 +1,8 @@
+# Round 3 batch ae: smoke() and the bench tests after the stdout change
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r3ae_smoke.log 2>&1 || exit $?
+tail -1 gpurun_out/r3ae_smoke.log
+timeout -k 10 600 python -u -m pytest tests/test_gpu_bench.py tests/test_gpu_shard.py -q -x --timeout 300 --timeout-method thread > gpurun_out/r3ae_pytest.log 2>&1
+rc=$?; tail -3 gpurun_out/r3ae_pytest.log; exit $rc
