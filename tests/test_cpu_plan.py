@@ -234,3 +234,20 @@ def test_get_elements_known_answers():
     v = D.create_vector(3, 2, 4, D.MPI.MPI_DOUBLE).commit()                              # size 48
     assert v.get_elements(24) == 3 and v.get_elements(48 * 5) == 30 and v.get_elements(20) is None
     assert D.MPI.MPI_INT.get_elements(12) == 3 and D.MPI.MPI_INT.get_elements(6) is None
+
+
+def test_opal_ddt_api_known_answers():
+    """test/datatype/opal_ddt_api.c: get_element_count on a vector of 3 blocks of 4 ints at a
+    stride of 6 (:233-260: the whole 48 bytes hold 12 elements, 4 bytes 1, 16 bytes 4), and the
+    bounds of its two backward constructions (:162-218: a vector of 3 ints at a stride of -2
+    spans true_lb -16 .. true_ub 4; ints added at 4 then 0 span 0 .. 8)."""
+    from ompi_amd import datatype as D
+    v = D.create_vector(3, 4, 6, D.MPI.MPI_INT).commit()
+    assert v.size == 48
+    assert v.get_elements(48) == 12 and v.get_elements(4) == 1 and v.get_elements(16) == 4
+    neg = D.create_vector(3, 1, -2, D.MPI.MPI_INT).commit()
+    i = neg.info()
+    assert (i["true_lb"], i["true_ub"]) == (-16, 4)
+    back = D.create_struct([1, 1], [4, 0], [D.MPI.MPI_INT, D.MPI.MPI_INT]).commit()
+    i = back.info()
+    assert (i["true_lb"], i["true_ub"]) == (0, 8)

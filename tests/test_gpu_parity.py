@@ -285,6 +285,24 @@ def test_copy_content_same_ddt(device):
     np.testing.assert_array_equal(_host(dst), exp)
 
 
+def test_copy_content_same_ddt_opal_ddt_api(device):
+    """test/datatype/opal_ddt_api.c:383-500 known answer: a vector of 3 blocks of 2 ints at a
+    stride of 4 ints over 40 bytes, source bytes 0..39 ascending, destination 0xCC: the blocks
+    (bytes 0..7, 16..23, 32..39) are copied and the gaps (8..15, 24..31) keep the sentinel."""
+    import torch
+    from ompi_amd import convertor as C
+    from ompi_amd import datatype as D
+    v = D.create_vector(3, 2, 4, D.MPI.MPI_INT).commit()
+    src = torch.arange(40, dtype=torch.uint8, device=device)
+    dst = torch.full((40,), 0xCC, dtype=torch.uint8, device=device)
+    C.copy_content_same_ddt(v, 1, dst.data_ptr(), src.data_ptr())
+    got = _host(dst)
+    exp = np.full(40, 0xCC, dtype=np.uint8)
+    for b0 in (0, 16, 32):
+        exp[b0:b0 + 8] = np.arange(b0, b0 + 8)
+    np.testing.assert_array_equal(got, exp)
+
+
 def test_window_api(device):
     """UCX-style random-access windows (pml_ucx_datatype.c:72-123)."""
     import torch
