@@ -251,3 +251,17 @@ def test_opal_ddt_api_known_answers():
     back = D.create_struct([1, 1], [4, 0], [D.MPI.MPI_INT, D.MPI.MPI_INT]).commit()
     i = back.info()
     assert (i["true_lb"], i["true_ub"]) == (0, 8)
+
+
+def test_opal_bigcount_large_contiguous():
+    """test/datatype/opal_datatype_bigcount.c:141-197: a contiguous run of INT_MAX + 1000 and of
+    3 x INT_MAX bytes has that size and extent (64-bit arithmetic, no truncation at 2^31 or
+    2^32); metadata only, no buffer.  The plan of the larger one is one leaf of 64-bit units."""
+    from ompi_amd import datatype as D
+    INT_MAX = 2**31 - 1
+    for n in (INT_MAX + 1000, 3 * INT_MAX):
+        t = D.create_contiguous(n, D.MPI.MPI_BYTE).commit()
+        i = t.info()
+        assert t.size == n and i["ub"] - i["lb"] == n and (i["true_lb"], i["true_ub"]) == (0, n)
+        assert t.get_elements(n) == n
+    assert t.plan_info()["leaves"] == 1
