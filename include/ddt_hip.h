@@ -315,7 +315,7 @@ int64_t ddt_type_plan_list(const ddt_datatype_t *type, size_t leaf, int64_t *dis
                            size_t cap);
 int ddt_debug_host_window(const void *p, size_t n, uint64_t *device_addr);
 /* Tuning knobs for A/B measurements (affect descriptor sets built afterwards):
- * "nt" = user-side non-temporal gathers (-1 auto, 0 off, 1 on); "task_kb" = packed KiB per
+ * "nt" = user-side non-temporal gathers (-1 auto = off since round 3, 0 off, 1 on); "task_kb" = packed KiB per
  * workgroup (0 adaptive); "policy" = task sizing (0 v0, 1 per-leaf passes); "interleave" =
  * reorder items in runs of this many tasks (0 off); "wt" = write-through stores (-1 auto,
  * 0 off, 1 every sparse leaf, 2 all); "sorted" = address-ordered list engine (-1 auto from

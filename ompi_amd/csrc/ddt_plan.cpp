@@ -463,21 +463,21 @@ uint64_t task_bytes_override()
     return uint64_t(tuning().task_kb > 0 ? tuning().task_kb : 0) << 10;
 }
 
-// Non-temporal user-side LOADS (pack) for sparse, narrow blocks spread over more than
-// the 256 MiB Infinity Cache (x-face-like gathers): the 6-face halo pack went from 112 to
-// 68 us (scripts/ubench*.hip, bench.py).  Stores stay temporal: non-temporal scattered
-// stores made the halo unpack slower (82 -> 108 us).  DDT_NT=0/1 forces it off/on.
-bool use_nt(uint32_t U, uint64_t blen, const std::vector<LeafDim> &dims)
+// Non-temporal user-side LOADS (pack) for sparse, narrow blocks (x-face-like gathers: one
+// element per 128-byte line).  Round 1 made them non-temporal when spread over more than the
+// 256 MiB Infinity Cache (halo pack 112 -> 68 us), while the unpack's partial-line writes were
+// still plain and left dirty lines for the next pack.  Since round 3 those writes are
+// non-temporal (use_wt), and a plain gather is now the better pair: the lines it reads stay in
+// the Infinity Cache, and the unpack's partial writes to the same lines merge there instead of
+// in a DRAM read-modify-write.  Pack + unpack step (profiles/r3_ab_nt_wt.jsonl, pair loop, two
+// boxes): cfg2 169.4 -> 158.0 us, cfg3 172.5 -> 157.5, both x faces 142.5 -> 128.1, cfg1
+// unchanged, cfg5 3070 -> 3053; the pack itself pays 6-8 us (non-temporal gathers run at 44
+// against 40 G lines/s), which is what a cold-clean single operation sees (cfg2 174.8 -> 181.5
+// with a 1 GiB read before each operation, profiles/r3_ab_nt.jsonl).  So the default (-1) is
+// plain, like 0; ddt_tune("nt", 1) makes every leaf's user-side loads non-temporal.
+bool use_nt(uint32_t, uint64_t, const std::vector<LeafDim> &)
 {
-    const int force = tuning().nt;
-    if (force >= 0)
-        return force == 1;
-    if (U > 8 || blen > 64)
-        return false;
-    uint64_t span = blen;
-    for (const LeafDim &d : dims)
-        span += (d.cnt - 1) * absu(d.sstr);
-    return span > (192ull << 20);
+    return tuning().nt == 1;
 }
 
 // User-side store policy of an unpack (Item::wt).  An isolated narrow block (blen <= 8, every

@@ -14,7 +14,7 @@ namespace ddt {
 
 // Tuning knobs (environment DDT_NT / DDT_TASK_KB, or ddt_tune()): for A/B sweeps.
 struct Tuning {
-    int nt = -1;       // user-side non-temporal loads: -1 auto, 0 off, 1 on
+    int nt = -1;       // user-side non-temporal loads: -1 auto (off, use_nt), 0 off, 1 on
     long task_kb = 0;  // packed KiB per workgroup task: 0 = adaptive
     long interleave = 0;  // >0: interleave items in runs of this many tasks
     int policy = 1;       // task sizing: 0 = v0 (~6 K tasks), 1 = per-leaf passes
