@@ -337,10 +337,126 @@ def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z"), flush="
         out[k] = {"packed_bytes": fS, "pack_us": round(tp * 1e6, 2), "unpack_us": round(tu * 1e6, 2),
                   "GiBs": round(2 * fS / (tp + tu) / GiB, 1), "frac": round(4 * fS / (tp + tu) / HBM_PEAK, 4),
                   "pack_frac": round(2 * fS / tp / HBM_PEAK, 4), "unpack_frac": round(2 * fS / tu / HBM_PEAK, 4)}
+        # the same protocol around the face's bare kernel (ompi_amd/csrc/ddt_floor.hip): same
+        # buffers, events, flushes; frac_of_floor = floor / engine (1.0 = the engine at the floor)
+        try:
+            import ctypes
+            L, Part = floor_lib()
+            kind, es, ls, ss, base, lw = face_floor_part(k, fields)
+            part = Part(kind, es, ls[0], ls[1], ls[2], lw, ss[0], ss[1], ss[2], base, 0)
+            fev = []
+            for i in range(warmup + steps):
+                a, b_, c_, d_ = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+                if flush:
+                    touch(2 * i)
+                a.record(stream)
+                L.ddt_floor_launch(ctypes.c_void_p(user.data_ptr()), ctypes.c_void_p(fp.data_ptr()),
+                                   ctypes.byref(part), 0, ctypes.c_void_p(stream.cuda_stream))
+                b_.record(stream)
+                if flush:
+                    touch(2 * i + 1)
+                c_.record(stream)
+                L.ddt_floor_launch(ctypes.c_void_p(user.data_ptr()), ctypes.c_void_p(fp.data_ptr()),
+                                   ctypes.byref(part), 1, ctypes.c_void_p(stream.cuda_stream))
+                d_.record(stream)
+                if i >= warmup:
+                    fev.append((a, b_, c_, d_))
+            torch.cuda.synchronize()
+            fpk = float(np.median([a.elapsed_time(b_) for a, b_, _, _ in fev])) * 1e3
+            fup = float(np.median([c_.elapsed_time(d_) for _, _, c_, d_ in fev])) * 1e3
+            out[k].update({"floor_pack_us": round(fpk, 2), "floor_unpack_us": round(fup, 2),
+                           "frac_of_floor": round((fpk + fup) / ((tp + tu) * 1e6), 4)})
+        except (OSError, AssertionError) as ex:
+            out[k]["floor_error"] = f"{type(ex).__name__}: {ex}"[:160]
         del fp
     del user, scribble
     torch.cuda.empty_cache()
     return out
+
+
+# ------------------------------------------------------------------ floor (bare kernels)
+def floor_parts(name):
+    """The workload as the access primitives of ompi_amd/csrc/ddt_floor.hip -- element gathers
+    (one 4/8-byte element per position), element scatters, block copies -- with the same user
+    offsets the engine moves: [(label, kind, esize, (l0, l1, l2), (s0, s1, s2), base, lw)].
+    Position counts are powers of two (decomposed by shifts).  None where the workload is not
+    made of these primitives (cfg4: address-ordered index list; cfg5: line-dense records)."""
+    if name == "cfg2":
+        n, F, e = 256, 16, 8
+        field, row, plane = n * n * n * e, n * e, n * n * e
+        return [("x faces", 0, 8, (16, 1, 4), (row, row - e, field), 0, 0),
+                ("y faces", 1, 0, (8, 1, 4), (plane, (n - 1) * row, field), 0, 7),
+                ("z faces", 1, 0, (1, 4, 0), ((n - 1) * plane, field, 0), 0, 15)]
+    if name == "cfg3":
+        n, F, e = 512, 8, 4
+        field, row, plane = n * n * n * e, n * e, n * n * e
+        return [("dim0 planes", 1, 0, (3, 0, 0), (field, 0, 0), (n - 1) * plane, 16),
+                ("dim1 rows", 1, 0, (9, 3, 0), (plane, field, 0), (n - 1) * row, 7),
+                ("dim2 elements", 0, 4, (18, 3, 0), (row, field, 0), (n - 1) * e, 0)]
+    if name == "cfg1":
+        return [("elements", 0, 8, (10, 11, 0), (16, 16376, 0), 0, 0)]
+    return None
+
+
+_FLOOR = None
+
+
+def floor_lib():
+    """ompi_amd/libddt_floor.so (bare kernels, measurement only) and its part structure."""
+    global _FLOOR
+    if _FLOOR is None:
+        import ctypes
+
+        class Part(ctypes.Structure):
+            _fields_ = [("kind", ctypes.c_int32), ("esize", ctypes.c_int32), ("l0", ctypes.c_uint32),
+                        ("l1", ctypes.c_uint32), ("l2", ctypes.c_uint32), ("lw", ctypes.c_uint32),
+                        ("s0", ctypes.c_int64), ("s1", ctypes.c_int64), ("s2", ctypes.c_int64),
+                        ("base", ctypes.c_int64), ("poff", ctypes.c_int64)]
+        L = ctypes.CDLL(os.path.join(ROOT, "ompi_amd", "libddt_floor.so"))
+        L.ddt_floor_run.restype = ctypes.c_int
+        L.ddt_floor_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_void_p]
+        L.ddt_floor_launch.restype = ctypes.c_int
+        L.ddt_floor_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                       ctypes.c_void_p]
+        _FLOOR = (L, Part)
+    return _FLOOR
+
+
+def face_floor_part(face, fields, n=256, e=8):
+    """One face type of the 256^3 double grid over `fields` fields (a power of two) as a floor
+    part: x = element gather/scatter, y = 2 KiB rows, z = 512 KiB planes."""
+    lf = fields.bit_length() - 1
+    assert 1 << lf == fields
+    field, row, plane = n * n * n * e, n * e, n * n * e
+    return {"x": (0, 8, (16, lf, 0), (row, field, 0), 0, 0),
+            "y": (1, 0, (8, lf, 0), (plane, field, 0), 0, 7),
+            "z": (1, 0, (lf, 0, 0), (field, 0, 0), 0, 15)}[face]
+
+
+def floor_run(name, user_ptr, packed_ptr, reps=10):
+    """Each part of the workload by its bare kernel, pack then unpack, in the same run and on
+    the same buffers as the engine; returns per-part medians (us) or None."""
+    import ctypes
+    parts = floor_parts(name)
+    if parts is None:
+        return None
+    L, Part = floor_lib()
+    arr = (Part * len(parts))()
+    poff = 0
+    for i, (_, kind, es, ls, ss, base, lw) in enumerate(parts):
+        arr[i] = Part(kind, es, ls[0], ls[1], ls[2], lw, ss[0], ss[1], ss[2], base, poff)
+        npos = 1 << sum(ls)
+        poff += npos * (es if kind == 0 else 16 << lw)
+    out = (ctypes.c_float * (2 * len(parts)))()
+    rc = L.ddt_floor_run(ctypes.c_void_p(user_ptr), ctypes.c_void_p(packed_ptr), arr, len(parts), reps, out)
+    if rc != 0:
+        return {"error": f"hip error {rc}"}
+    res = {label: {"pack_us": round(out[2 * i], 2), "unpack_us": round(out[2 * i + 1], 2)}
+           for i, (label, *_r) in enumerate(parts)}
+    return {"parts": res, "bytes": poff,
+            "pack_us": round(sum(v["pack_us"] for v in res.values()), 2),
+            "unpack_us": round(sum(v["unpack_us"] for v in res.values()), 2)}
 
 
 # ------------------------------------------------------------------ multi-rank harness
@@ -421,6 +537,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="skip the HIP-graph replay measurement")
     ap.add_argument("--event-every", type=int, default=10,
                     help="bracket every Nth timed step with HIP events (kernel durations)")
+    ap.add_argument("--no-floor", action="store_true", help="skip the bare-kernel floor of the workload")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-face latency probe (profiling runs: one workload per trace)")
     args = ap.parse_args()
@@ -579,6 +696,30 @@ def main():
         torch.cuda.synchronize()
         graph_step = g0.elapsed_time(g1) / 1e3 / args.steps
 
+    # The floor of this workload on this box, outside the timed region: each of its parts moved
+    # by a bare kernel (ompi_amd/csrc/ddt_floor.hip) on the same buffers, in the same pack-then-
+    # unpack order.  frac_of_floor = floor / the engine's own event time (1.0 = at the floor).
+    floor = None
+    if rank == 0 and world == 1 and not args.no_floor and not split:
+        try:
+            fl = floor_run(args.config, uptr, packed.data_ptr())
+        except OSError as ex:   # the measurement library is missing: report, never fail the line
+            fl = {"error": f"{type(ex).__name__}: {ex}"[:200]}
+        if fl and "error" not in fl:
+            if fl["bytes"] != S:
+                fl["error"] = f"floor parts cover {fl['bytes']} of {S} packed bytes"
+            else:
+                step_floor = fl["pack_us"] + fl["unpack_us"]
+                fl["step_us"] = round(step_floor, 2)
+                fl["frac_of_floor"] = {"pack": round(fl["pack_us"] / (tp * 1e6), 4),
+                                       "unpack": round(fl["unpack_us"] / (tu * 1e6), 4),
+                                       "step": round(step_floor / ((tp + tu) * 1e6), 4)}
+                fl["source"] = ("ompi_amd/csrc/ddt_floor.hip: element gathers (plain loads), element "
+                                "scatters (non-temporal stores), 16 KiB block copies (non-temporal loads), "
+                                "median of 10 rounds; floor = sum of the parts")
+        floor = fl
+        torch.cuda.synchronize()
+
     # The RCCL leg of SURVEY.md §8e, outside the timed region: a consumer that needs the
     # whole packed stream on one device all-gathers the shards (backend "nccl" = RCCL over
     # xGMI); every rank checks that its slice of the gathered stream is its own shard.
@@ -617,6 +758,7 @@ def main():
             "graph_replay_GiBs_per_gpu": (round(2.0 * S / graph_step / GiB, 3) if graph_step else None),
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 2), "peak": 8000.0,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": None},
+            "floor_us": floor,
         }
         # the committed PMC passes were measured on the config's default (weak) message; a
         # --strong message of another size does not inherit them
@@ -638,10 +780,12 @@ def main():
                 "frac": round(ops / (tp + tu) / rq["ceiling_requests_per_s"], 4),
                 "source": f"profiles/requests_{args.config}.json"}
 
-    if rank == 0 and args.config == "cfg2" and not args.no_latency:
+    # the single-face and per-face probes run at N = 1 only: under the driver's N > 1 launch they
+    # would keep rank 0 busy for tens of seconds after the others (the scaling run needs the line)
+    if rank == 0 and world == 1 and args.config == "cfg2" and not args.no_latency:
         result["single_face_latency_us"] = single_face_latency(dev, stream, user, origin)
 
-    if rank == 0 and args.config == "cfg2" and not args.no_faces:
+    if rank == 0 and world == 1 and args.config == "cfg2" and not args.no_faces:
         # per-face figure of the north star: each face type alone, batched over many fields
         # (beyond the Infinity Cache), and at the bench's own 16 fields (launch-bound)
         result["faces"] = face_throughput(dev, args.face_fields, max(5, min(args.steps, 20)))

@@ -163,6 +163,9 @@ static bridge_entry *bridge_type_of(const opal_convertor_t *conv, int *err)
     ++g_entries;
     ++g_imports;
     pthread_mutex_unlock(&g_mu);
+    /* the import is this datatype's commit on the device side: a large index list gets its
+     * address-ordered tables here, at prepare, not in the first fAdvance of a message */
+    (void) ddt_type_prepare_device(t);
     return e;
 }
 

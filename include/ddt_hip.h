@@ -126,10 +126,21 @@ int ddt_type_create_resized(const ddt_datatype_t *oldtype, ptrdiff_t lb, ptrdiff
                             ddt_datatype_t **newtype);
 /* ompi_datatype_duplicate (ompi_datatype_create.c:115-145) */
 int ddt_type_dup(const ddt_datatype_t *oldtype, ddt_datatype_t **newtype);
-/* opal_datatype_commit (opal_datatype_optimize.c:1739-1782): freezes the type map and
- * builds the device plan lazily on first use. */
+/* opal_datatype_commit (opal_datatype_optimize.c:1739-1782): freezes the type map, derives
+ * the reference's opt_desc from it (ddt_type_to_opal_opt_desc) and builds the device plan
+ * lazily on first use. */
 int ddt_type_commit(ddt_datatype_t *type);
-/* ompi_datatype_destroy / OBJ_RELEASE; predefined handles are ignored. */
+/* The device state a committed type's first move would build: for a large index list of small
+ * blocks (>= 1 Mi, the address-ordered engine) its lists and address-ordered tables, on the
+ * library-private stream of the current device, which the type's plan is then bound to.
+ * ddt_type_commit calls it for such types and the opal bridge at import, so the cost lands where
+ * Open MPI pays its own (opal_datatype_commit), not in the first pack of a message.  A no-op for
+ * other types and without a device. */
+int ddt_type_prepare_device(ddt_datatype_t *type);
+/* ompi_datatype_destroy / OBJ_RELEASE; predefined handles are ignored.  Never waits: the type's
+ * device memory goes back to the engine's pool behind events recorded on every stream its work
+ * was queued on, so those streams must still exist (HIP cannot tell a destroyed stream handle,
+ * using one is undefined); work enqueued inside a stream capture keeps its memory for the graph. */
 int ddt_type_destroy(ddt_datatype_t **type);
 
 /* ---- queries (opal_datatype.h:290-330) ---- */
@@ -147,11 +158,20 @@ int ddt_type_info(const ddt_datatype_t *type, int64_t *out8);
 int ddt_type_from_opal_desc(const void *desc, size_t used, size_t size, ptrdiff_t lb, ptrdiff_t ub,
                             ptrdiff_t true_lb, ptrdiff_t true_ub, ddt_datatype_t **newtype);
 
-/* The inverse, for tests and tools: the uncommitted type map of `type` as dt_elem_desc_t
- * entries (DATA per block run, LOOP/END_LOOP pairs, item counts as CREATE_LOOP_START/END
- * write them, opal_datatype_internal.h:171-189), without the END_LOOP sentinel.  Returns the
- * entry count, or minus the count needed when `cap` entries do not fit. */
+/* The inverse, for tests and tools: the uncommitted type map of `type` as the
+ * opal_datatype_t::desc opal_datatype_add would have built (opal_datatype_add.c:307-431:
+ * DATA entries, LOOP/END_LOOP pairs as CREATE_LOOP_START/END write them,
+ * opal_datatype_internal.h:171-189), without the END_LOOP sentinel.  Returns the entry count,
+ * or minus the count needed when `cap` entries do not fit. */
 int64_t ddt_type_to_opal_desc(const ddt_datatype_t *type, void *out, size_t cap);
+
+/* opal_datatype_t::opt_desc of `type` as opal_datatype_commit derives it from that desc
+ * (opal_datatype_optimize.c:1739-1782, restated in ddt_optimize.cpp: mixed-type regions re-typed
+ * to UINT8/4/2/1 carriers, :581-630), without the sentinel; *flags (optional) gets
+ * OPAL_DATATYPE_OPTIMIZED_RESTRICTED (0x10000) when a region was re-typed.  These are the
+ * elements the engine's pack fragments keep whole and its send positions snap to.  Same return
+ * convention as ddt_type_to_opal_desc. */
+int64_t ddt_type_to_opal_opt_desc(const ddt_datatype_t *type, void *out, size_t cap, uint32_t *flags);
 
 /* ================= convertor (opal/datatype/opal_convertor.h) ================= */
 

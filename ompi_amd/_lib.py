@@ -54,6 +54,8 @@ SIGNATURES = {
     "ddt_type_from_opal_desc": (c_int, [c_void_p, c_size_t, c_size_t, c_ssize_t, c_ssize_t,
                                         c_ssize_t, c_ssize_t, P(c_void_p)]),
     "ddt_type_to_opal_desc": (c_int64, [c_void_p, c_void_p, c_size_t]),
+    "ddt_type_prepare_device": (c_int, [c_void_p]),
+    "ddt_type_to_opal_opt_desc": (c_int64, [c_void_p, c_void_p, c_size_t, ctypes.POINTER(ctypes.c_uint32)]),
     "ddt_convertor_create": (c_void_p, []),
     "ddt_convertor_destroy": (None, [c_void_p]),
     "ddt_convertor_prepare_for_send": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),

@@ -481,9 +481,13 @@ struct ddt_convertor {
     hipEvent_t ev_chunk[2] = {nullptr, nullptr};
     hipEvent_t ev_free = nullptr;
     bool rec_free = false;
+    bool staged_in_capture = false;   // a staged call was enqueued into a stream capture
     // No host wait: a convertor without host staging holds no device memory, and the staging
-    // buffers of one that has it go to the engine's pool behind fences on the user stream and
-    // the copy stream (their last readers), like a destroyed plan's (ddt_pool.h).  So an
+    // buffers of one that has it go to the engine's pool behind fences, like a destroyed
+    // plan's (ddt_pool.h): ev_free, recorded after the last reader of the buffer on whichever
+    // stream the last staged call used (each staged call waits for the previous ev_free, so it
+    // covers them all -- ADVICE r3: the stream may have been changed since, and the bridge
+    // resets it to NULL after every call), plus the current user and copy streams.  So an
     // OBJ_RELEASE of a convertor never stalls, even during another thread's stream capture.
     ~ddt_convertor()
     {
@@ -496,7 +500,11 @@ struct ddt_convertor {
             std::vector<hipStream_t> ss{stream};
             if (copy_stream)
                 ss.push_back(copy_stream);
-            if (pool_fences(ss, fences, unknown)) {
+            if (!staged_in_capture && pool_fences(ss, fences, unknown)) {
+                if (rec_free && ev_free) {
+                    fences.push_back(ev_free);   // the pool owns and destroys it
+                    ev_free = nullptr;
+                }
                 pool_release(blocks, fences, unknown);
             } else {   // a capturing stream: its graph may read the staging buffer
                 for (hipEvent_t e : fences)
@@ -566,6 +574,11 @@ int execute(ddt_convertor *c, const std::vector<Window> &dev_wins,
             need = std::max(need, hw.first.w1 - hw.first.w0);
         if ((rc = c->ensure_staging(need)) != DDT_SUCCESS)
             return rc;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(c->stream, &cs) != hipSuccess)
+            (void) hipGetLastError();   // the legacy stream under a foreign capture: not captured
+        else if (cs != hipStreamCaptureStatusNone)
+            c->staged_in_capture = true;
         char *st = static_cast<char *>(c->stage);
         for (const auto &hw : host_wins) {
             for (uint64_t off = hw.first.w0; off < hw.first.w1;) {
@@ -1120,20 +1133,32 @@ namespace {
 // stream-ordered allocations, whose pool returns the memory at every synchronisation: a
 // 16 MiB MPI_Pack_external spent ~300 us of its 357 in allocation (profiles/r2_ext_bench.jsonl).
 // Only buffers up to kKeepBytes are kept by the thread: a larger request (a multi-GiB message)
-// gets a block of its own for the call, back to the engine's pool when the call ends (the
-// call has synchronised its stream), so a thread does not hold that much HBM for good;
-// ddt_trim() returns pooled memory to HIP.
+// gets a block of its own for the call, handed back to HIP when the call ends (the call has
+// synchronised its stream; ADVICE r3: not parked in the engine's pool, where co-resident
+// allocators could not have it); ddt_trim() returns pooled memory to HIP.
+// A call that returns early on an error may leave work queued on `stream` that still reads or
+// writes the buffer: the destructor then waits for that stream before the memory can be
+// reused by another thread (settled() marks the call's own final synchronisation).
 constexpr size_t kKeepBytes = size_t(256) << 20;
 struct DevBuf {
     void *p = nullptr;
     void *own = nullptr;
     int slot = 0;
-    explicit DevBuf(int s) : slot(s) {}
+    hipStream_t stream = nullptr;
+    bool queued = false;
+    explicit DevBuf(int s, hipStream_t st = nullptr) : slot(s), stream(st) {}
     DevBuf(const DevBuf &) = delete;
     DevBuf &operator=(const DevBuf &) = delete;
-    ~DevBuf() { pool_free(own); }
+    ~DevBuf()
+    {
+        if (queued)
+            (void) hipStreamSynchronize(stream);
+        pool_free_now(own);
+    }
+    void settled() { queued = false; }
     hipError_t alloc(size_t n)
     {
+        queued = true;
         if (n > kKeepBytes) {
             own = pool_alloc(n);
             p = own;
@@ -1214,16 +1239,15 @@ int ddt_sndrcv(const void *sbuf, size_t scount, const ddt_datatype_t *st, void *
     // two datatypes: pack into HBM scratch, unpack from it (the reference pipelines 64 KiB
     // host chunks; here it is one launch per side, stream-ordered)
     const size_t n = std::min(scount * ssz, rcount * rsz);
-    DevBuf tmp(2);
+    DevBuf tmp(2, s);   // an early return waits for `s` (the scratch is this thread's next call's)
     HIPCHK(tmp.alloc(n));
     rc = one_side(st, scount, sbuf, tmp.p, n, 0, &moved);
     if (rc == DDT_SUCCESS && moved)
         rc = one_side(rt, rcount, rbuf, tmp.p, moved, 1, &moved);
-    if (rc != DDT_SUCCESS) {
-        (void) hipStreamSynchronize(s);   // the scratch is reused by this thread's next call
+    if (rc != DDT_SUCCESS)
         return rc;
-    }
     HIPCHK(hipStreamSynchronize(s));
+    tmp.settled();
     return scount * ssz <= rcount * rsz ? DDT_SUCCESS : fail(DDT_ERR_TRUNCATE, "send larger than receive");
 }
 
@@ -1297,6 +1321,8 @@ int ddt_pack_external(const char *datarep, const void *inbuf, size_t incount,
     if (!dev_out)
         HIPCHK(hipMemcpy(dst, te.p, need, hipMemcpyDeviceToHost));
     HIPCHK(hipStreamSynchronize(nullptr));
+    tn.settled();
+    te.settled();
     *position += ptrdiff_t(need);
     return DDT_SUCCESS;
 }
@@ -1339,6 +1365,8 @@ int ddt_unpack_external(const char *datarep, const void *inbuf, ptrdiff_t insize
     size_t md = 0;
     if ((rc = advance(&c, &iov, &n, &md, 1)) < 0)
         return rc;
+    tn.settled();   // a synchronous advance ends with its stream synchronised
+    te.settled();
     *position += ptrdiff_t(need);
     return DDT_SUCCESS;
 }
@@ -1652,6 +1680,10 @@ int ddt_tune(const char *key, long value)
         tuning().sunroll = value >= 16 ? 16 : (value >= 8 ? 8 : 4);
     else if (k == "sseg")
         tuning().sseg = value == 128 ? 128 : 64;
+    else if (k == "schunk")
+        tuning().schunk = value == 2 ? 2 : 1;
+    else if (k == "sorted_commit")
+        tuning().sorted_commit = value ? 1 : 0;
     else if (k == "stage_mb")
         tuning().stage_mb = value < 1 ? 1 : value;
     else if (k == "snt")

@@ -34,6 +34,13 @@ enum : uint32_t {
     F_DATA = 0x0100u,
 };
 
+// LP64 x86-64 sizes of opal_datatype_local_sizes (opal_datatype_module.c:143-180) and natural
+// alignment (opal_datatype_constructors.h:87-96), by OPAL predefined id.
+inline constexpr int64_t kOpalSize[29] = {0, 0, 0, 0, 1, 2, 4, 8, 16, 1, 2, 4, 8, 16, 2,
+                                          4, 8, 16, 16, 4, 8, 16, 32, 1, 4, 8, 8, 32, 0};
+inline constexpr int64_t kOpalAlign[29] = {0, 0, 0, 0, 1, 2, 4, 8, 16, 1, 2, 4, 8, 16, 2,
+                                           4, 8, 16, 16, 2, 4, 8, 16, 1, 4, 8, 8, 16, 0};
+
 // Element boundaries inside one block of a merged mixed-type DATA run: the element
 // start offsets within one period.  Null pattern = every multiple of esize.
 struct Pattern {
@@ -63,6 +70,8 @@ struct Node {
     uint64_t blen = 0;      // DATA: bytes per block
     int64_t extent = 0;     // DATA: block stride; LOOP: iteration stride
     int64_t disp = 0;       // DATA: first block displacement; LIST: shift for every block
+    uint32_t flags = 0;     // uncommitted form: the entry's Open MPI flags (DATA/LIST: the element's,
+                            // LOOP: the repeated type's, opal_datatype_add.c:328-343, :406-409)
     std::vector<Node> body; // LOOP
     uint64_t body_size = 0; // LOOP: packed bytes per iteration (== END_LOOP size)
     std::shared_ptr<const IndexList> list;  // LIST
@@ -143,6 +152,7 @@ struct Retired {
 };
 
 struct ExtPlan;
+struct DescForm;
 
 struct Plan {
     std::vector<Leaf> leaves;
@@ -176,6 +186,8 @@ struct ddt_datatype {
     uint64_t nbElems = 0;
     std::vector<ddt::Node> desc;  // type map (uncommitted form)
     std::vector<ddt::Node> opt;   // committed + normalised form
+    bool imported = false;        // desc is already a committed opt_desc (ddt_type_from_opal_desc)
+    uint32_t opt_flags = 0;       // OPAL_DATATYPE_OPTIMIZED_RESTRICTED after commit (ddt_optimize.h)
     std::vector<uint64_t> opt_prefix;  // packed offset of each top-level opt node
     std::mutex plan_mu;
     std::shared_ptr<ddt::Plan> plan;
@@ -187,10 +199,14 @@ namespace ddt {
 // typemap.cpp
 ddt_datatype *new_type();
 int commit(ddt_datatype *t);
+// Open MPI's opt_desc of a committed type, as ddt_optimize.cpp derives it (false: not expressible)
+bool opt_desc_of(const ddt_datatype *t, DescForm &out);
 void normalize(std::vector<Node> &nodes);
 // Largest element boundary <= p (p in [0, count*size]) of the packed stream.
 uint64_t snap_down_to_element(const ddt_datatype *t, uint64_t p);
 // plan.cpp
 std::shared_ptr<Plan> get_plan(ddt_datatype *t);
 void ensure_device_lists(Plan &P);
+// commit / import time device setup of the address-ordered engine (ddt_plan.cpp)
+int prebuild_device(ddt_datatype *t);
 }  // namespace ddt

@@ -1,0 +1,748 @@
+// ddt_optimize.cpp -- Open MPI's commit optimizer, restated for the engine's type maps.
+//
+// The engine's constructors build a Node tree (ddt_core.h) that mirrors opal_datatype_add's
+// `desc`.  At commit the tree is written out as that description (build_opal_desc), run through
+// a restatement of opal_datatype_commit's optimizer (optimize_desc), and the result is read back
+// into Nodes exactly as the bridge reads a real Open MPI opt_desc (nodes_from_desc).  So the
+// elements a pack fragment keeps whole and a send position snaps to -- the carriers of fused
+// mixed-type regions included -- are the reference's, for every type, however it was built.
+//
+// Reference: opal/datatype/opal_datatype_optimize.c
+//   optimize_short (:890-1295)  one pass: merge / fuse DATA, compress contiguous loops, expand
+//                               short innermost loops, loop-boundary fusion, unrolling
+//   short_restart (:1347-1478)  passes to a fixed point; boundary expansion kept only when it
+//                               lowers the copy-range count (:406-435), growth <= 10x
+//   promoted_type (:581-611)    carrier of a mixed region: widest UINT8/4/2 that tiles it and
+//                               is aligned at disp (and extent when count > 1), else UINT1
+// with the run-time defaults of opal_datatype_module.c:85-88 (max_desc_growth 10, unroll 8 items
+// of <= 128 bytes, preserve_type on).  COUNT_OPTIMIZABLE (:385-401) is a hint no mover reads and
+// is not computed.
+//
+// Sealed lists (engine extension): an index list of more than kSealBlocks blocks (64 Mi for
+// BASELINE config 4) is not expanded into one entry per block.  It enters the optimizer as one
+// opaque element: nothing merges into or across it, loops holding it are neither unrolled,
+// expanded nor compressed.  Inside such a list the reference only ever merges blocks of its one
+// type, so its element boundaries are the same either way; a fusion of its first or last block
+// with a neighbour of another type is the one case the engine does not reproduce.
+#include "ddt_optimize.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace ddt {
+namespace {
+
+constexpr uint32_t kData = F_DATA;
+constexpr uint32_t kContig = F_CONTIGUOUS;
+constexpr uint32_t kElemMask = 0x01FFu;                                  // OPAL_DATATYPE_FLAG_ELEM_MASK
+constexpr uint32_t kBasic = F_PREDEFINED | F_CONTIGUOUS | F_NO_GAPS | F_DATA | F_COMMITTED;
+constexpr uint64_t kUnrollItems = 8, kUnrollBytes = 128;
+constexpr uint64_t kInlineBlocklen = 8;   // OPAL_DATATYPE_PREDEFINED_MAX_INLINE_BLOCKLEN
+constexpr int64_t kGrowth = 10;
+constexpr uint16_t kNoType = 0xFFFF;
+
+inline int64_t esz(uint16_t t) { return kOpalSize[t]; }
+inline int64_t bytes_of(const DescEntry &e) { return int64_t(e.blen) * esz(e.type); }
+inline uint32_t kept(uint32_t f) { return kBasic | (f & kTypeChanged); }
+inline bool is_data(const DescEntry &e) { return (e.flags & kData) != 0; }
+
+DescEntry loop_entry(uint32_t loops, uint32_t items, int64_t extent, uint32_t flags)
+{
+    DescEntry e;
+    e.flags = uint16_t(flags & ~kData);
+    e.type = kDescLoop;
+    e.count = items;
+    e.loops = loops;
+    e.blen = ~uint64_t(0);
+    e.extent = extent;
+    return e;
+}
+
+DescEntry end_entry(uint32_t items, int64_t first, uint64_t size, uint32_t flags)
+{
+    DescEntry e;
+    e.flags = uint16_t(flags & ~kData);
+    e.type = kDescEndLoop;
+    e.count = items;
+    e.loops = ~uint32_t(0);
+    e.blen = size;
+    e.disp = first;
+    return e;
+}
+
+// ------------------------------------------------------------------ the optimizer
+class Pass {
+public:
+    Pass(const std::vector<DescEntry> &d, uint32_t *flags) : d_(d), flags_(flags) {}
+
+    // one optimize_short pass; the output keeps the END_LOOP sentinel at [used]
+    void run(std::vector<DescEntry> &o, size_t &used, bool boundary, bool *expanded, bool *reevaluate);
+
+private:
+    const std::vector<DescEntry> &d_;
+    uint32_t *flags_;
+    std::vector<DescEntry> *o_ = nullptr;
+
+    // CREATE_ELEM (opal_datatype_internal.h:195-209)
+    void elem(uint16_t type, uint32_t flags, uint64_t blen, uint32_t count, int64_t disp, int64_t extent)
+    {
+        DescEntry e;
+        e.flags = uint16_t(flags | kData);
+        e.type = type;
+        e.count = count;
+        e.blen = blen;
+        e.extent = extent;
+        e.disp = disp;
+        if (extent == int64_t(blen * uint64_t(esz(type)))) {
+            e.blen *= count;
+            e.extent *= count;
+            e.count = 1;
+        }
+        o_->push_back(e);
+    }
+    void put(const DescEntry &e) { o_->push_back(e); }
+
+    uint32_t next_item(size_t pos, uint32_t item) const
+    {
+        const DescEntry &e = d_[pos + item];
+        return e.type == kDescLoop && !is_data(e) ? item + e.count + 1 : item + 1;
+    }
+    bool innermost(size_t pos) const
+    {
+        for (uint32_t k = 1; k < d_[pos].count; ++k)
+            if (d_[pos + k].type == kDescLoop && !is_data(d_[pos + k]))
+                return false;
+        return true;
+    }
+    bool holds_sealed(size_t pos) const
+    {
+        for (uint32_t k = 1; k < d_[pos].count; ++k)
+            if (d_[pos + k].sealed >= 0)
+                return true;
+        return false;
+    }
+    uint32_t unroll_factor(size_t pos) const;
+    bool as_elem(size_t pos, uint32_t item, DescEntry &out) const;
+    bool compress(size_t pos, DescEntry &out) const;
+    bool fuse_tail_head(const DescEntry &tail, const DescEntry &head, int64_t delta, uint32_t rcount,
+                        int64_t rextent, DescEntry &fused) const;
+    void copy_range(size_t pos, uint32_t from, uint32_t to, int64_t delta);
+    bool loop_boundary(size_t pos);
+    void unrolled(size_t pos, uint32_t f);
+};
+
+// opal_datatype_opt_collapse_elem (:539-549)
+void collapse(DescEntry &e)
+{
+    if (e.count > 1 && e.extent == bytes_of(e)) {
+        e.blen *= e.count;
+        e.extent *= e.count;
+        e.count = 1;
+    }
+}
+
+// opal_datatype_opt_promoted_type + set_mixed_region (:581-630)
+void mixed_region(DescEntry &e, int64_t bytes, uint32_t count, int64_t disp, int64_t extent)
+{
+    uint16_t type = 9;   // UINT1
+    for (uint16_t c : {uint16_t(12), uint16_t(11), uint16_t(10)}) {   // UINT8, UINT4, UINT2
+        const uint64_t sz = uint64_t(esz(c)), al = uint64_t(kOpalAlign[c]);
+        if (uint64_t(bytes) % sz || (uint64_t(disp) & (al - 1)) || (count > 1 && (uint64_t(extent) & (al - 1))))
+            continue;
+        type = c;
+        break;
+    }
+    e.type = type;
+    e.flags = uint16_t(kBasic | kTypeChanged);
+    e.blen = uint64_t(bytes / esz(type));
+    e.count = count;
+    e.disp = disp;
+    e.extent = extent;
+    e.sealed = -1;
+}
+
+uint32_t Pass::unroll_factor(size_t pos) const   // :72-110
+{
+    const DescEntry &L = d_[pos], &E = d_[pos + L.count];
+    if (L.loops < 4 || L.count < 2 || (L.flags & kContig) || E.type != kDescEndLoop || is_data(E))
+        return 1;
+    const uint32_t body = L.count - 1;
+    if (kUnrollItems < body)
+        return 1;
+    for (uint32_t k = 0; k < body; ++k) {
+        const DescEntry &e = d_[pos + k + 1];
+        if (!is_data(e) || e.sealed >= 0)
+            return 1;
+        const uint64_t ts = uint64_t(esz(e.type));
+        if (!ts || !e.blen || e.blen > kUnrollBytes / ts || e.count > kUnrollBytes / (e.blen * ts))
+            return 1;
+    }
+    const uint32_t f = std::min<uint32_t>(uint32_t(kUnrollItems / body), L.loops / 2);
+    return f > 1 ? f : 1;
+}
+
+void Pass::unrolled(size_t pos, uint32_t f)   // :165-215
+{
+    const DescEntry &L = d_[pos], &E = d_[pos + L.count];
+    const uint32_t body = L.count - 1, iters = L.loops / f, tail = L.loops % f, items = body * f;
+    put(loop_entry(iters, items + 1, L.extent * f, L.flags));
+    auto body_at = [&](int64_t shift) {
+        for (uint32_t k = 0; k < body; ++k) {
+            const DescEntry &e = d_[pos + k + 1];
+            elem(e.type, kept(e.flags), e.blen, e.count, e.disp + shift, e.extent);
+        }
+    };
+    for (uint32_t it = 0; it < f; ++it)
+        body_at(int64_t(it) * L.extent);
+    put(end_entry(items + 1, E.disp, E.blen * f, E.flags));
+    for (uint32_t it = 0; it < tail; ++it)
+        body_at(int64_t(iters * f + it) * L.extent);
+}
+
+bool Pass::as_elem(size_t pos, uint32_t item, DescEntry &out) const   // :716-734
+{
+    const DescEntry &e = d_[pos + item];
+    if (is_data(e)) {
+        if (e.sealed >= 0)
+            return false;
+        out = e;
+        out.flags = uint16_t(kept(out.flags));
+        collapse(out);
+        return out.count == 1;
+    }
+    if (e.type == kDescLoop)
+        return compress(pos + item, out) && out.count == 1;
+    return false;
+}
+
+bool Pass::compress(size_t pos, DescEntry &out) const   // :641-709
+{
+    const DescEntry &L = d_[pos], &E = d_[pos + L.count];
+    if (!(L.flags & kContig) || holds_sealed(pos))
+        return false;
+    uint16_t ctype = kNoType;
+    uint32_t cflags = kBasic;
+    uint64_t cblen = 0;
+    bool homog = true, any = false;
+    for (uint32_t i = 1; i < L.count; i = next_item(pos, i)) {
+        DescEntry cur;
+        any = true;
+        if (!as_elem(pos, i, cur)) {
+            homog = false;
+            break;
+        }
+        if (ctype == kNoType) {
+            ctype = cur.type;
+            cblen = cur.blen;
+            cflags |= cur.flags & kTypeChanged;
+            continue;
+        }
+        if (ctype != cur.type) {
+            homog = false;
+            break;
+        }
+        cblen += cur.blen;
+        cflags |= cur.flags & kTypeChanged;
+    }
+    if (!any)
+        return false;
+    if (homog) {
+        const uint64_t ts = uint64_t(esz(ctype));
+        if (!ts || E.blen % ts || E.blen != cblen * ts) {
+            homog = false;
+        } else {
+            out = DescEntry{};
+            out.type = ctype;
+            out.flags = uint16_t(cflags);
+            out.blen = E.blen / ts;
+            out.count = L.loops;
+            out.extent = L.extent;
+            out.disp = E.disp;
+        }
+    }
+    if (!homog)
+        mixed_region(out, int64_t(E.blen), L.loops, E.disp, L.extent);
+    collapse(out);
+    return true;
+}
+
+bool Pass::fuse_tail_head(const DescEntry &tail, const DescEntry &head, int64_t delta, uint32_t rcount,
+                          int64_t rextent, DescEntry &fused) const   // :741-786
+{
+    if (tail.count != 1 || head.count != 1)
+        return false;
+    const int64_t ts = bytes_of(tail), hs = bytes_of(head);
+    if (tail.disp + ts != head.disp + delta)
+        return false;
+    fused = tail;
+    if (tail.type == head.type) {
+        fused.flags = uint16_t(kBasic | ((tail.flags | head.flags) & kTypeChanged));
+        fused.blen += head.blen;
+    } else {
+        mixed_region(fused, ts + hs, rcount, tail.disp, rextent);
+    }
+    fused.count = 1;
+    fused.extent = ts + hs;
+    if (fused.flags & kTypeChanged)
+        *flags_ |= kRestricted;
+    return true;
+}
+
+void Pass::copy_range(size_t pos, uint32_t from, uint32_t to, int64_t delta)   // :515-533
+{
+    for (uint32_t i = from; i < to; ++i) {
+        DescEntry e = d_[pos + i];
+        if (is_data(e)) {
+            e.flags = uint16_t(kept(e.flags));
+            e.disp += delta;
+        } else if (e.type == kDescEndLoop) {
+            e.disp += delta;
+        }
+        put(e);
+    }
+}
+
+bool Pass::loop_boundary(size_t pos)   // :799-888
+{
+    const DescEntry &L = d_[pos], &E = d_[pos + L.count];
+    if (L.loops < 2 || L.count <= 2)
+        return false;
+    uint32_t last_item = 0, nitems = 0;
+    for (uint32_t i = 1; i < L.count; i = next_item(pos, i)) {
+        const DescEntry &e = d_[pos + i];
+        if (!(e.type == kDescLoop && !is_data(e)) && !is_data(e))
+            return false;
+        last_item = i;
+        ++nitems;
+    }
+    if (nitems < 2 || last_item == 0)
+        return false;
+    const uint32_t after_first = next_item(pos, 1);
+    DescEntry first, last, fused;
+    if (!as_elem(pos, 1, first) || !as_elem(pos, last_item, last))
+        return false;
+    if (!fuse_tail_head(last, first, L.extent, L.loops - 1, L.extent, fused))
+        return false;
+    copy_range(pos, 1, last_item, 0);
+    if (nitems == 2) {
+        elem(fused.type, fused.flags, fused.blen, L.loops - 1, fused.disp, L.extent);
+    } else {
+        const uint32_t steady = last_item - after_first + 2;
+        put(loop_entry(L.loops - 1, steady, L.extent, L.flags));
+        elem(fused.type, fused.flags, fused.blen, 1, fused.disp, fused.extent);
+        copy_range(pos, after_first, last_item, L.extent);
+        put(end_entry(steady, fused.disp, E.blen, L.flags));
+    }
+    elem(last.type, last.flags, last.blen, last.count, last.disp + int64_t(L.loops - 1) * L.extent,
+         last.extent);
+    return true;
+}
+
+void Pass::run(std::vector<DescEntry> &o, size_t &used, bool boundary, bool *expanded, bool *reevaluate)
+{
+    o.clear();
+    o_ = &o;
+    if (expanded)
+        *expanded = false;
+    if (reevaluate)
+        *reevaluate = false;
+    // the stack: output index just past each open LOOP, and whether that loop is innermost
+    std::vector<int64_t> open{-1};
+    std::vector<char> inner{0};
+    DescEntry last, cur;
+    last.flags = 0xFFFF;
+    size_t pos = 0;
+    auto flush_last = [&]() {
+        if (last.count) {
+            if (last.sealed >= 0)
+                put(last);
+            else
+                elem(last.type, kept(last.flags), last.blen, last.count, last.disp, last.extent);
+            last.count = 0;
+        }
+    };
+    while (!open.empty()) {
+        const DescEntry &e = d_[pos];
+        if (!is_data(e) && e.type == kDescEndLoop) {
+            flush_last();
+            const uint32_t items = uint32_t(int64_t(o.size()) - open.back() + 1);
+            put(end_entry(items, e.disp, e.blen, e.flags));
+            const int64_t at = open.back();
+            open.pop_back();
+            inner.pop_back();
+            if (!open.empty())
+                o[size_t(at - 1)].count = items;
+            ++pos;
+            continue;
+        }
+        if (!is_data(e) && e.type == kDescLoop) {
+            const DescEntry L = e;
+            DescEntry cmp;
+            if ((L.flags & kContig) && compress(pos, cmp)) {
+                if (reevaluate)
+                    *reevaluate = true;
+                if (cmp.flags & kTypeChanged)
+                    *flags_ |= kRestricted;
+                pos += L.count + 1;
+                cur = cmp;
+            } else {
+                flush_last();
+                last.type = kDescLoop;
+                if (L.count <= 4 && L.loops <= 2 && innermost(pos) && !holds_sealed(pos)) {
+                    // fully expand a short innermost loop (:1054-1082)
+                    if (reevaluate)
+                        *reevaluate = true;
+                    int64_t shift = 0;
+                    for (uint32_t i = 0; i < L.loops; ++i, shift += L.extent)
+                        for (uint32_t j = 0; j + 1 < L.count; ++j) {
+                            const DescEntry &c = d_[pos + 1 + j];
+                            elem(c.type, kept(c.flags), c.blen, c.count, c.disp + shift, c.extent);
+                        }
+                    pos += L.count + 1;
+                    continue;
+                }
+                if (boundary && loop_boundary(pos)) {
+                    if (expanded)
+                        *expanded = true;
+                    pos += L.count + 1;
+                    continue;
+                }
+                const uint32_t f = unroll_factor(pos);
+                if (f > 1) {
+                    unrolled(pos, f);
+                    pos += L.count + 1;
+                    continue;
+                }
+                put(loop_entry(L.loops, L.count, L.extent, L.flags));
+                open.push_back(int64_t(o.size()));
+                inner.push_back(char(innermost(pos)));
+                ++pos;
+                continue;
+            }
+        } else {
+            cur = e;
+            cur.flags = uint16_t(kept(cur.flags));
+            ++pos;
+            if (cur.sealed >= 0) {   // an opaque element: nothing merges into or across it
+                flush_last();
+                put(cur);
+                continue;
+            }
+        }
+        // DATA (or a compressed loop) against the pending element (:1146-1278)
+        if (last.count == 0) {
+            last = cur;
+            continue;
+        }
+        if (bytes_of(last) == last.extent) {
+            last.extent *= last.count;
+            last.blen *= last.count;
+            last.count = 1;
+        }
+        const int64_t lbs = bytes_of(last), cbs = bytes_of(cur);
+        if (lbs == cbs) {   // one entry of count last + cur
+            const bool mixed = last.type != cur.type;
+            int64_t mext = last.extent;
+            const uint32_t mcount = last.count + cur.count;
+            bool can = false;
+            if (last.extent * int64_t(last.count) + last.disp == cur.disp
+                && (cur.count == 1 || last.extent == cur.extent)) {
+                can = true;
+            } else if (last.count == 1 && (cur.count == 1 || last.disp + cur.extent == cur.disp)) {
+                mext = cur.count == 1 ? cur.disp - last.disp : cur.extent;
+                can = true;
+            }
+            if (can) {
+                if (reevaluate && inner.back())
+                    *reevaluate = true;
+                if (mixed) {
+                    mixed_region(last, lbs, mcount, last.disp, mext);
+                    *flags_ |= kRestricted;
+                } else {
+                    last.flags |= cur.flags & kTypeChanged;
+                    last.extent = mext;
+                    last.count = mcount;
+                }
+                continue;
+            }
+        }
+        const bool inline_pair = last.count > 1 && cur.count > 1 && last.blen <= kInlineBlocklen
+                                 && cur.blen <= kInlineBlocklen;
+        if (!inline_pair && last.disp + int64_t(last.count - 1) * last.extent + lbs == cur.disp) {
+            // fuse the last block of `last` with the first block of `cur`
+            const bool shrinks = last.count == 1 && cur.count == 1;
+            const int64_t fext = last.extent + cur.extent;
+            if (shrinks && reevaluate && inner.back())
+                *reevaluate = true;
+            if (last.count != 1) {
+                elem(last.type, kept(last.flags), last.blen, last.count - 1, last.disp, last.extent);
+                last.disp += int64_t(last.count - 1) * last.extent;
+                last.count = 1;
+            }
+            if (last.type == cur.type) {
+                last.flags |= cur.flags & kTypeChanged;
+                last.blen += cur.blen;
+            } else {
+                mixed_region(last, lbs + cbs, 1, last.disp, fext);
+                *flags_ |= kRestricted;
+            }
+            last.extent = fext;
+            if (cur.count != 1) {
+                elem(last.type, kept(last.flags), last.blen, last.count, last.disp, last.extent);
+                last = cur;
+                last.count -= 1;
+                last.disp += last.extent;
+            }
+            continue;
+        }
+        elem(last.type, kept(last.flags), last.blen, last.count, last.disp, last.extent);
+        last = cur;
+    }
+    flush_last();
+    used = o.size() - 1;   // the top-level END_LOOP is the sentinel
+}
+
+// opal_datatype_opt_count_range_groups_desc (:406-435); a sealed list counts its blocks
+uint64_t ranges(const std::vector<DescEntry> &d, const std::vector<std::shared_ptr<const IndexList>> &lists,
+                size_t from, size_t to)
+{
+    uint64_t r = 0;
+    for (size_t pos = from; pos < to;) {
+        const DescEntry &e = d[pos];
+        if (is_data(e)) {
+            r += e.sealed >= 0 ? lists[size_t(e.sealed)]->nblk() : e.count;
+            ++pos;
+        } else if (e.type == kDescLoop) {
+            const uint64_t lr = (e.flags & kContig) ? 1 : ranges(d, lists, pos + 1, pos + e.count);
+            r += lr * e.loops;
+            pos += e.count + 1;
+        } else {
+            ++pos;
+        }
+    }
+    return r;
+}
+
+}  // namespace
+
+void optimize_desc(const DescForm &in, int64_t size, DescForm &out, uint32_t *flags)
+{
+    // opal_datatype_optimize_short_restart (:1347-1478) from opal_datatype_commit (:1765-1777)
+    const int64_t limit = int64_t(in.used) * kGrowth;
+    const uint32_t init = *flags;
+    auto short_pass = [&](const std::vector<DescEntry> &src, DescForm &dst, bool boundary, bool *expanded,
+                          bool *reevaluate) {
+        Pass p(src, flags);
+        p.run(dst.e, dst.used, boundary, expanded, reevaluate);
+        dst.lists = in.lists;
+    };
+    auto count_ranges = [&](const DescForm &f) { return ranges(f.e, in.lists, 0, f.used); };
+    out = DescForm{};
+    if (in.used == 0) {
+        out.lists = in.lists;
+        return;
+    }
+    DescForm cand, next, base;
+    bool expanded = false, reeval = false;
+    *flags = init;
+    short_pass(in.e, cand, true, &expanded, &reeval);
+    uint32_t cand_flags = *flags;
+    bool any_expanded = expanded;
+    if (expanded || reeval) {
+        uint64_t cand_ranges = count_ranges(cand);
+        while (expanded || reeval) {
+            if (int64_t(cand.used) > limit)
+                break;
+            bool nexp = false, nre = false;
+            *flags = init | (cand_flags & kRestricted);
+            short_pass(cand.e, next, true, &nexp, &nre);
+            const uint64_t nr = count_ranges(next);
+            if (int64_t(next.used) > limit || (nexp && nr >= cand_ranges))
+                break;
+            any_expanded |= nexp;
+            cand_flags = *flags;
+            cand = std::move(next);
+            cand_ranges = nr;
+            expanded = nexp;
+            reeval = nre;
+        }
+        if (any_expanded) {
+            // the non-expanding baseline, converged the same way (:1427-1474)
+            *flags = init;
+            reeval = false;
+            short_pass(in.e, base, false, nullptr, &reeval);
+            uint32_t base_flags = *flags;
+            while (reeval) {
+                bool nre = false;
+                *flags = init | (base_flags & kRestricted);
+                short_pass(base.e, next, false, nullptr, &nre);
+                if (int64_t(next.used) > limit)
+                    break;
+                base_flags = *flags;
+                base = std::move(next);
+                reeval = nre;
+            }
+            if (!(int64_t(cand.used) <= limit && cand_ranges < count_ranges(base))) {
+                cand = std::move(base);
+                cand_flags = base_flags;
+            }
+        }
+    }
+    *flags = init | (cand_flags & kRestricted);
+    out = std::move(cand);
+    // opal_datatype_opt_set_fake_end_loop (:454-465) over the optimized description
+    const DescEntry &s = in.e[in.used];
+    out.e.resize(out.used + 1);
+    out.e[out.used] = end_entry(uint32_t(out.used), s.disp, uint64_t(size), 0);
+    out.e[out.used].flags = 0;
+}
+
+// ------------------------------------------------------------------ Node tree -> desc
+namespace {
+
+struct Writer {
+    DescForm &f;
+    bool ok = true;
+
+    void data(uint32_t flags, uint16_t tid, uint64_t count, uint64_t bytes, int64_t extent, int64_t disp)
+    {
+        const int64_t es = (tid >= 4 && tid <= 27) ? esz(tid) : 0;
+        if (es <= 0 || bytes % uint64_t(es) || count > 0xffffffffull) {
+            ok = false;
+            return;
+        }
+        DescEntry e;
+        e.flags = uint16_t(flags | kData);
+        e.type = tid;
+        e.count = uint32_t(count);
+        e.blen = bytes / uint64_t(es);
+        e.extent = extent;
+        e.disp = disp;
+        f.e.push_back(e);
+    }
+
+    static bool first_disp(const std::vector<Node> &nodes, int64_t &out)
+    {
+        for (const Node &n : nodes) {
+            switch (n.kind) {
+            case Node::DATA: out = n.disp; return true;
+            case Node::LIST:
+                if (n.list && n.list->nblk()) {
+                    out = n.disp + n.list->disp[0];
+                    return true;
+                }
+                break;
+            case Node::LOOP:
+                if (first_disp(n.body, out))
+                    return true;
+                break;
+            }
+        }
+        return false;
+    }
+
+    void nodes(const std::vector<Node> &ns)
+    {
+        for (const Node &n : ns) {
+            if (!ok)
+                return;
+            switch (n.kind) {
+            case Node::DATA:
+                data(n.flags, n.tid, n.count, n.blen, n.extent, n.disp);
+                break;
+            case Node::LIST: {
+                const IndexList &X = *n.list;
+                if (X.nblk() > kSealBlocks) {
+                    DescEntry e;
+                    e.flags = uint16_t(n.flags | kData);
+                    e.type = n.tid;
+                    e.count = 1;
+                    e.blen = X.total / uint64_t(esz(n.tid));
+                    e.extent = int64_t(X.total);
+                    e.disp = n.disp;
+                    e.sealed = int32_t(f.lists.size());
+                    f.lists.push_back(n.list);
+                    f.e.push_back(e);
+                    break;
+                }
+                for (size_t k = 0; k < X.nblk() && ok; ++k) {
+                    const uint64_t len = X.len.empty() ? X.ulen : X.len[k];
+                    data(n.flags, n.tid, 1, len, int64_t(len), n.disp + X.disp[k]);
+                }
+                break;
+            }
+            case Node::LOOP: {
+                if (n.count > 0xffffffffull) {
+                    ok = false;
+                    return;
+                }
+                const uint32_t lflags = n.flags & (kElemMask & ~F_COMMITTED);
+                const size_t at = f.e.size();
+                f.e.push_back(loop_entry(uint32_t(n.count), 0, n.extent, lflags));
+                nodes(n.body);
+                const uint32_t items = uint32_t(f.e.size() - at);
+                f.e[at].count = items;
+                int64_t first = 0;
+                first_disp(n.body, first);
+                f.e.push_back(end_entry(items, first, n.body_size, lflags));
+                break;
+            }
+            }
+        }
+    }
+};
+
+}  // namespace
+
+bool build_opal_desc(const std::vector<Node> &nodes, int64_t size, DescForm &out)
+{
+    out = DescForm{};
+    Writer w{out};
+    w.nodes(nodes);
+    if (!w.ok)
+        return false;
+    out.used = out.e.size();
+    int64_t first = 0;
+    if (size != 0)
+        Writer::first_disp(nodes, first);
+    DescEntry s = end_entry(uint32_t(out.used), first, uint64_t(size), 0);
+    s.flags = 0;
+    out.e.push_back(s);
+    return true;
+}
+
+void encode_desc(const DescForm &d, std::vector<unsigned char> &out)
+{
+    out.clear();
+    auto put = [&](uint16_t flags, uint16_t type, uint32_t a, uint32_t b, uint64_t c, int64_t x, int64_t y) {
+        unsigned char p[32] = {0};
+        std::memcpy(p, &flags, 2);
+        std::memcpy(p + 2, &type, 2);
+        std::memcpy(p + 4, &a, 4);
+        if (!(flags & kData) && (type == kDescLoop || type == kDescEndLoop)) {
+            std::memcpy(p + 8, &b, 4);
+            std::memcpy(p + 16, &c, 8);
+            std::memcpy(p + 24, type == kDescLoop ? &x : &y, 8);
+        } else {
+            std::memcpy(p + 8, &c, 8);
+            std::memcpy(p + 16, &x, 8);
+            std::memcpy(p + 24, &y, 8);
+        }
+        out.insert(out.end(), p, p + 32);
+    };
+    for (size_t i = 0; i < d.used; ++i) {
+        const DescEntry &e = d.e[i];
+        if (e.sealed >= 0) {
+            const IndexList &X = *d.lists[size_t(e.sealed)];
+            const uint64_t es = uint64_t(esz(e.type));
+            for (size_t k = 0; k < X.nblk(); ++k) {
+                const uint64_t len = X.len.empty() ? X.ulen : X.len[k];
+                put(e.flags, e.type, 1, 0, len / es, int64_t(len), e.disp + X.disp[k]);
+            }
+            continue;
+        }
+        put(e.flags, e.type, e.count, e.loops, e.blen, e.extent, e.disp);
+    }
+}
+
+}  // namespace ddt

@@ -12,6 +12,9 @@ namespace ddt {
 namespace {
 
 constexpr size_t kAlign = 256;
+// Free blocks a device's cache may hold before a new hipMalloc hands the largest back to HIP
+// (staging and scratch blocks of different sizes must not pile up for good).
+constexpr size_t kCacheCap = size_t(1) << 30;
 
 struct Block {
     size_t bytes = 0;
@@ -74,6 +77,44 @@ void reap(Pool &P)   // P.mu held
     }
 }
 
+// Before a new hipMalloc -- a call that already waits for the device and breaks a foreign
+// global-mode capture, so nothing is lost by freeing here too: blocks released behind a stream
+// that could take no fence (destroyed before the plan or convertor) are settled by one device
+// synchronisation, and the largest cached blocks go back to HIP until the cache is within
+// kCacheCap.
+void settle_and_cap(Pool &P, int dev)   // P.mu held
+{
+    bool unknown = false;
+    for (const Pending &r : P.pending)
+        unknown |= r.unknown;
+    if (unknown && hipDeviceSynchronize() == hipSuccess) {
+        for (size_t i = 0; i < P.pending.size();) {
+            Pending &r = P.pending[i];
+            if (!r.unknown) {
+                ++i;
+                continue;
+            }
+            for (hipEvent_t e : r.fences)
+                (void) hipEventDestroy(e);
+            for (void *p : r.blocks)
+                to_free(P, p);
+            P.pending.erase(P.pending.begin() + long(i));
+        }
+    }
+    (void) hipGetLastError();
+    auto &fl = P.free[dev];
+    size_t cached = 0;
+    for (auto &sb : fl)
+        cached += sb.first;
+    while (cached > kCacheCap && !fl.empty()) {
+        auto last = std::prev(fl.end());
+        cached -= last->first;
+        (void) hipFree(last->second);
+        P.blocks.erase(last->second);
+        fl.erase(last);
+    }
+}
+
 void *take_free(Pool &P, int dev, size_t bytes)   // P.mu held
 {
     auto &fl = P.free[dev];
@@ -99,6 +140,9 @@ void *pool_alloc(size_t bytes)
     }
     std::lock_guard<std::mutex> g(P.mu);
     reap(P);
+    if (void *p = take_free(P, dev, bytes))
+        return p;
+    settle_and_cap(P, dev);
     if (void *p = take_free(P, dev, bytes))
         return p;
     void *p = nullptr;
@@ -133,6 +177,20 @@ void pool_free(void *p)
     if (it == P.blocks.end() || it->second.state != 0)
         return;
     to_free(P, p);
+}
+
+void pool_free_now(void *p)
+{
+    if (!p)
+        return;
+    Pool &P = pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    auto it = P.blocks.find(p);
+    if (it == P.blocks.end() || it->second.state != 0)
+        return;
+    P.blocks.erase(it);
+    (void) hipFree(p);
+    (void) hipGetLastError();
 }
 
 void pool_release(const std::vector<void *> &blocks, const std::vector<hipEvent_t> &fences, bool unknown)

@@ -25,8 +25,16 @@ namespace ddt {
 void *pool_alloc(size_t bytes);
 // A block no queued work reads any more: reusable at once.
 void pool_free(void *p);
+// A block no queued work reads any more, handed straight back to HIP (hipFree waits for the
+// device): the end of a synchronous call's multi-GiB scratch, which the pool should not keep.
+void pool_free_now(void *p);
 // Blocks that queued work may still read: reusable once every event in `fences` has passed.
-// `unknown` (a launching stream that could take no event) keeps them until ddt_trim().
+// `unknown` (a launching stream that could take no event) keeps them until the next pool_alloc
+// that has to call hipMalloc settles them with one device synchronisation (or ddt_trim()).  The
+// cache of free blocks is capped at 1 GiB per device at that same point.  A stream that launched
+// a datatype's work must stay valid until the datatype (and a convertor using it) is destroyed:
+// the fences are recorded on it, and HIP does not detect a destroyed stream handle (using one
+// crashes the runtime, round 4), as CUDA leaves it undefined.
 // The pool owns and destroys the events.
 void pool_release(const std::vector<void *> &blocks, const std::vector<hipEvent_t> &fences, bool unknown);
 // A block a captured graph holds: never reused, never freed.

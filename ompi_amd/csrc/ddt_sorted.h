@@ -13,7 +13,9 @@ namespace ddt {
 struct SortedList {
     uint32_t n = 0;          // blocks (one element each)
     uint32_t esz = 0;        // element bytes: 4, 8 or 16
-    uint32_t ch = 0;         // elements per chunk (address order) == per bucket (packed order)
+    uint32_t ch = 0;         // elements per chunk (address order): rg / cdiv
+    uint32_t rg = 0;         // elements per bucket (packed order): a 128 KiB LDS image
+    uint32_t cdiv = 1;       // 2: half-size chunks, two pass-1 workgroups per CU
     uint32_t seg = 0;        // elements per segment of U
     uint32_t segb = 64;      // segment bytes: 64 or 128
     uint32_t nc = 0, nb = 0; // chunks, buckets
@@ -38,7 +40,7 @@ struct SortedList {
     // hand the tables and U to `out` (the plan releases them behind its stream fences)
     void take_blocks(std::vector<void *> &out);
     bool build(const int32_t *disp, uint32_t n, uint32_t esz, uint64_t span_elems, uint32_t segb,
-               hipStream_t stream);
+               hipStream_t stream, uint32_t cdiv = 1);
     // pol: access policy bits (POL_* in ddt_sorted.hip; ddt_tune "spol")
     // unroll: elements per thread in flight in pack 1's address-ordered gather (4, 8 or 16)
     // k2: the same for unpack pass 2' (4, 8 or 16)

@@ -138,14 +138,14 @@ __device__ __forceinline__ uint32_t rank_of(uint32_t a, const uint32_t *bm, cons
 // A[j] = a; count (chunk, bucket) and remember each block's rank inside its run
 __global__ __launch_bounds__(BT) void k_rank(const int32_t *__restrict__ disp, uint32_t n, uint32_t shift,
                                              const uint32_t *__restrict__ bm, const uint32_t *__restrict__ wpre,
-                                             uint32_t ch, uint32_t nb, uint32_t *__restrict__ A,
+                                             uint32_t ch, uint32_t rg, uint32_t nb, uint32_t *__restrict__ A,
                                              uint32_t *__restrict__ cnt, uint16_t *__restrict__ rr)
 {
     for (uint32_t i = blockIdx.x * BT + threadIdx.x; i < n; i += gridDim.x * BT) {
         const uint32_t a = uint32_t(disp[i]) >> shift;
         const uint32_t j = rank_of(a, bm, wpre);
         A[j] = a;
-        const uint32_t c = j / ch, k = i / ch;   // CH == RG
+        const uint32_t c = j / ch, k = i / rg;
         rr[i] = uint16_t(atomicAdd(&cnt[size_t(c) * nb + k], 1u));
     }
 }
@@ -218,17 +218,17 @@ __global__ __launch_bounds__(BT) void k_run_bases(const uint32_t *__restrict__ u
 
 __global__ __launch_bounds__(BT) void k_assign(const int32_t *__restrict__ disp, uint32_t n, uint32_t shift,
                                                const uint32_t *__restrict__ bm, const uint32_t *__restrict__ wpre,
-                                               uint32_t ch, uint32_t nb, const uint16_t *__restrict__ rr,
+                                               uint32_t ch, uint32_t rg, uint32_t nb, const uint16_t *__restrict__ rr,
                                                const uint16_t *__restrict__ off16, const uint32_t *__restrict__ ub,
                                                uint16_t *__restrict__ SL, uint16_t *__restrict__ upos)
 {
     for (uint32_t i = blockIdx.x * BT + threadIdx.x; i < n; i += gridDim.x * BT) {
         const uint32_t a = uint32_t(disp[i]) >> shift;
         const uint32_t j = rank_of(a, bm, wpre);
-        const uint32_t c = j / ch, k = i / ch;
+        const uint32_t c = j / ch, k = i / rg;
         const size_t ck = size_t(c) * nb + k;
         SL[j] = uint16_t(off16[ck] + rr[i]);
-        upos[ub[ck] + rr[i]] = uint16_t(i - k * ch);
+        upos[ub[ck] + rr[i]] = uint16_t(i - k * rg);
     }
 }
 
@@ -239,11 +239,11 @@ __global__ __launch_bounds__(BT) void k_assign(const int32_t *__restrict__ disp,
 // size (the sorted_plan size rule), so chunk image + tables = 155 KiB of the 160.
 constexpr uint32_t MAXNB = 4096;
 
-template <int E>
+template <int NT>
 __device__ __forceinline__ void stage_tables(const uint16_t *__restrict__ off16, const uint32_t *__restrict__ ub,
                                              uint32_t c, uint32_t nb, uint32_t m, uint16_t *toff, uint32_t *tub)
 {
-    for (uint32_t k = threadIdx.x; k < nb; k += PT) {
+    for (uint32_t k = threadIdx.x; k < nb; k += NT) {
         toff[k] = off16[size_t(c) * nb + k];
         tub[k] = ub[size_t(c) * nb + k];
     }
@@ -252,7 +252,7 @@ __device__ __forceinline__ void stage_tables(const uint16_t *__restrict__ off16,
 }
 
 // pack pass 1, second phase: the chunk image's runs out to U, bucket by bucket
-template <int E, int SEGB>
+template <int E, int SEGB, int NT>
 __device__ __forceinline__ void emit_runs(const typename Elem<E>::T *lds, const uint16_t *toff, const uint32_t *tub,
                                           uint8_t *__restrict__ U, uint32_t nb, bool nts)
 {
@@ -260,7 +260,7 @@ __device__ __forceinline__ void emit_runs(const typename Elem<E>::T *lds, const 
     constexpr uint32_t SEG = SEGB / E;
     T *dst = reinterpret_cast<T *>(U);
     const uint32_t sub = threadIdx.x / SEG, lane = threadIdx.x % SEG;
-    for (uint32_t k = sub; k < nb; k += PT / SEG) {
+    for (uint32_t k = sub; k < nb; k += NT / SEG) {
         const uint32_t o = toff[k], cn = toff[k + 1] - o;
         const uint32_t b = tub[k], pn = (cn + SEG - 1) / SEG * SEG;
         for (uint32_t q = lane; q < pn; q += SEG)
@@ -268,32 +268,36 @@ __device__ __forceinline__ void emit_runs(const typename Elem<E>::T *lds, const 
     }
 }
 
-// pack pass 1: gather the chunk in address order into LDS, emit its runs bucket by bucket
-template <int E, int SEGB, int K>
-__global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, const AddrList al,
-                                              const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
-                                              const uint32_t *__restrict__ ub, uint8_t *__restrict__ U, uint32_t n,
-                                              uint32_t nb, uint32_t pol)
+// pack pass 1: gather the chunk in address order into LDS, emit its runs bucket by bucket.
+// CDIV = 2 (round 4, ddt_tune("schunk", 2)): half-size chunks (64 KiB images, buckets stay
+// 128 KiB) in 512-thread workgroups, two per CU, so one chunk's gather overlaps another's run
+// emission; needs nb <= MAXNB / 2.
+template <int E, int SEGB, int K, int CDIV>
+__global__ __launch_bounds__(PT / CDIV) void k_pack1(const uint8_t *__restrict__ user, const AddrList al,
+                                                     const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
+                                                     const uint32_t *__restrict__ ub, uint8_t *__restrict__ U, uint32_t n,
+                                                     uint32_t nb, uint32_t pol)
 {
     using T = typename Elem<E>::T;
-    constexpr uint32_t CH = LDS_BYTES / E, SEG = SEGB / E;
+    constexpr uint32_t NT = PT / CDIV;
+    constexpr uint32_t CH = LDS_BYTES / E / CDIV, SEG = SEGB / E;
     const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS, ntu = pol & POL_USER_NTL;
     __shared__ T lds[CH + SEG];
-    __shared__ uint16_t toff[MAXNB + 1];
-    __shared__ uint32_t tub[MAXNB];
+    __shared__ uint16_t toff[MAXNB / CDIV + 1];
+    __shared__ uint32_t tub[MAXNB / CDIV];
     const uint32_t c = blockIdx.x, j0 = c * CH;
     const uint32_t m = min(CH, n - j0);
-    stage_tables<E>(off16, ub, c, nb, m, toff, tub);
+    stage_tables<NT>(off16, ub, c, nb, m, toff, tub);
     const T *src = reinterpret_cast<const T *>(user);
     // K elements per thread in flight: each is a dependent pair (offset, then the user
     // element), so K sets how many of the chunk's CH / PT per thread share one latency
     const uint32_t mg = (pol & POL_SKIP_USER) ? 0u : m;
-    for (uint32_t t0 = threadIdx.x; t0 < mg; t0 += PT * K) {
+    for (uint32_t t0 = threadIdx.x; t0 < mg; t0 += NT * K) {
         T v[K];
         uint32_t s[K];
 #pragma unroll
         for (int q = 0; q < K; ++q) {
-            const uint32_t t = t0 + q * PT;
+            const uint32_t t = t0 + q * NT;
             if (t < m) {
                 s[q] = ldp(&SL[j0 + t], ntl);
                 v[q] = ldp(&src[addr_at(al, j0 + t, ntl)], ntu);
@@ -301,11 +305,11 @@ __global__ __launch_bounds__(PT) void k_pack1(const uint8_t *__restrict__ user, 
         }
 #pragma unroll
         for (int q = 0; q < K; ++q)
-            if (t0 + q * PT < m)
+            if (t0 + q * NT < m)
                 lds[s[q]] = v[q];
     }
     __syncthreads();
-    emit_runs<E, SEGB>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, nts);
+    emit_runs<E, SEGB, NT>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, nts);
 }
 
 // pack pass 2: the bucket's runs scatter into LDS by destination, then stream out
@@ -392,12 +396,12 @@ __global__ __launch_bounds__(PT) void k_unpack2(const uint8_t *__restrict__ pack
 }
 
 // unpack pass 1', first phase: the chunk's runs from U into the LDS chunk image
-template <int E, int SEGB>
+template <int E, int SEGB, int NT>
 __device__ __forceinline__ void load_runs(typename Elem<E>::T *lds, const uint16_t *toff, const uint32_t *tub,
                                           const uint8_t *__restrict__ U, uint32_t nb, bool ntl)
 {
     using T = typename Elem<E>::T;
-    constexpr uint32_t SEG = SEGB / E, NSUB = PT / SEG;
+    constexpr uint32_t SEG = SEGB / E, NSUB = NT / SEG;
     const T *src = reinterpret_cast<const T *>(U);
     // B runs per round: their first two segments are loaded before any is stored (ILP: a
     // run averages one segment, so about half of them have a second); the rare third and
@@ -436,32 +440,33 @@ __device__ __forceinline__ void load_runs(typename Elem<E>::T *lds, const uint16
 }
 
 // unpack pass 1': the chunk's runs into LDS, then scattered to the user side in address order
-template <int E, int SEGB, int K>
-__global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, const AddrList al,
-                                                const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
-                                                const uint32_t *__restrict__ ub, const uint8_t *__restrict__ U,
-                                                uint32_t n, uint32_t nb, uint32_t pol)
+template <int E, int SEGB, int K, int CDIV>
+__global__ __launch_bounds__(PT / CDIV) void k_unpack1(uint8_t *__restrict__ user, const AddrList al,
+                                                       const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
+                                                       const uint32_t *__restrict__ ub, const uint8_t *__restrict__ U,
+                                                       uint32_t n, uint32_t nb, uint32_t pol)
 {
     using T = typename Elem<E>::T;
-    constexpr uint32_t CH = LDS_BYTES / E;
+    constexpr uint32_t NT = PT / CDIV;
+    constexpr uint32_t CH = LDS_BYTES / E / CDIV;
     const bool ntl = pol & POL_STREAM_NTL, wt = pol & POL_USER_WT;
     __shared__ T lds[CH];
-    __shared__ uint16_t toff[MAXNB + 1];
-    __shared__ uint32_t tub[MAXNB];
+    __shared__ uint16_t toff[MAXNB / CDIV + 1];
+    __shared__ uint32_t tub[MAXNB / CDIV];
     const uint32_t c = blockIdx.x, j0 = c * CH;
     const uint32_t m = min(CH, n - j0);
-    stage_tables<E>(off16, ub, c, nb, m, toff, tub);
+    stage_tables<NT>(off16, ub, c, nb, m, toff, tub);
     __syncthreads();
-    load_runs<E, SEGB>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, ntl);
+    load_runs<E, SEGB, NT>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, ntl);
     __syncthreads();
     T *dst = reinterpret_cast<T *>(user);
     const uint32_t ms = (pol & POL_SKIP_USER) ? 0u : m;
-    for (uint32_t t0 = threadIdx.x; t0 < ms; t0 += PT * K) {
+    for (uint32_t t0 = threadIdx.x; t0 < ms; t0 += NT * K) {
         uint32_t a[K];
         T v[K];
 #pragma unroll
         for (int q = 0; q < K; ++q) {
-            const uint32_t t = t0 + q * PT;
+            const uint32_t t = t0 + q * NT;
             if (t < m) {
                 a[q] = addr_at(al, j0 + t, ntl);
                 v[q] = lds[ldp(&SL[j0 + t], ntl)];
@@ -469,7 +474,7 @@ __global__ __launch_bounds__(PT) void k_unpack1(uint8_t *__restrict__ user, cons
         }
 #pragma unroll
         for (int q = 0; q < K; ++q)
-            if (t0 + q * PT < m) {
+            if (t0 + q * NT < m) {
                 if (wt)
                     st_sc1(&dst[a[q]], v[q]);
                 else
@@ -539,15 +544,17 @@ SortedList::~SortedList()
 // list's minimum displacement, every value a multiple of esz).  Returns false (and leaves
 // nothing allocated) when the displacements repeat.
 bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t span_elems, uint32_t segb_,
-                       hipStream_t stream)
+                       hipStream_t stream, uint32_t cdiv_)
 {
     n = n_;
     esz = esz_;
     segb = segb_ == 128 ? 128 : SEG_DEFAULT;
-    ch = LDS_BYTES / esz;
+    rg = LDS_BYTES / esz;
+    nb = (n + rg - 1) / rg;
+    cdiv = (cdiv_ == 2 && nb <= MAXNB / 2) ? 2 : 1;   // half chunks: the tables must fit half the LDS
+    ch = rg / cdiv;
     seg = segb / esz;
     nc = (n + ch - 1) / ch;
-    nb = nc;   // RG == CH
     uint32_t shift = 0;
     while ((1u << shift) < esz)
         ++shift;
@@ -594,8 +601,8 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
         off16 = dalloc<uint16_t>(runs, bytes);
         ub = dalloc<uint32_t>(runs, bytes);
         bstart = dalloc<uint32_t>(nb + 1, bytes);
-        hipLaunchKernelGGL(k_rank, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, bm, wpre, ch, nb, A,
-                           cnt, rr);
+        hipLaunchKernelGGL(k_rank, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, bm, wpre, ch, rg,
+                           nb, A, cnt, rr);
         {   // the 16-bit form of A, kept when every 64-element group spans < 64 Ki elements
             uint64_t cb = 0;
             A16 = dalloc<uint16_t>(n, cb);
@@ -628,8 +635,8 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
         upos = dalloc<uint16_t>(slots, bytes);
         U = dalloc<uint8_t>(size_t(slots) * esz, bytes);
         HK(hipMemsetAsync(upos, 0xFF, size_t(slots) * 2, stream));
-        hipLaunchKernelGGL(k_assign, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, bm, wpre, ch, nb,
-                           rr, off16, ub, SL, upos);
+        hipLaunchKernelGGL(k_assign, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, bm, wpre, ch, rg,
+                           nb, rr, off16, ub, SL, upos);
         HK(hipGetLastError());
         HK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
         HK(hipStreamSynchronize(stream));
@@ -662,16 +669,21 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol
         if (e != hipSuccess)
             return e;
     }
-    const dim3 gc(nc), gb(nb), blk(PT);
+    const dim3 gc(nc), gb(nb), blk(PT), blk1(PT / cdiv);
     const AddrList al{A, A16, Abase};
     uint8_t *u8 = static_cast<uint8_t *>(U);
+#define DDT_SORTED_PASS1(E, SB, K, CD)                                                                          \
+    if (dir == 0)                                                                                               \
+        hipLaunchKernelGGL((k_pack1<E, SB, K, CD>), gc, blk1, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol); \
+    else                                                                                                        \
+        hipLaunchKernelGGL((k_unpack1<E, SB, 4, CD>), gc, blk1, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);
 #define DDT_SORTED_LAUNCH_K(E, SB, K)                                                                           \
     if (dir == 0) {                                                                                             \
-        hipLaunchKernelGGL((k_pack1<E, SB, K>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);  \
+        if (cdiv == 2) { DDT_SORTED_PASS1(E, SB, K, 2) } else { DDT_SORTED_PASS1(E, SB, K, 1) }                 \
         launch_pass2<E, 0>(gb, blk, stream, u8, upos, bstart, packed, n, pol, k2);                             \
     } else {                                                                                                    \
         launch_pass2<E, 1>(gb, blk, stream, packed, upos, bstart, u8, n, pol, k2);                             \
-        hipLaunchKernelGGL((k_unpack1<E, SB, 4>), gc, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);\
+        if (cdiv == 2) { DDT_SORTED_PASS1(E, SB, K, 2) } else { DDT_SORTED_PASS1(E, SB, K, 1) }                 \
     }
 // K * E <= 64 bytes of elements per thread in flight: wider elements at K = 16 (or 16-byte
 // ones at 8) exceed the 128 VGPRs of a 1024-thread workgroup and spill
@@ -702,6 +714,7 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol
     }
 #undef DDT_SORTED_LAUNCH
 #undef DDT_SORTED_LAUNCH_K
+#undef DDT_SORTED_PASS1
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return e;

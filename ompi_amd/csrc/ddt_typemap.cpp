@@ -11,17 +11,15 @@
 
 #include "ddt_core.h"
 #include "ddt_hip.h"
+#include "ddt_optimize.h"
 
 using namespace ddt;
 
 namespace {
 
-// LP64 x86-64 sizes of opal_datatype_local_sizes (opal_datatype_module.c:143-180),
-// natural alignment (opal_datatype_constructors.h:87-96).
-const int64_t kSize[29] = {0, 0, 0, 0, 1, 2, 4, 8, 16, 1, 2, 4, 8, 16, 2,
-                           4, 8, 16, 16, 4, 8, 16, 32, 1, 4, 8, 8, 32, 0};
-const int64_t kAlign[29] = {0, 0, 0, 0, 1, 2, 4, 8, 16, 1, 2, 4, 8, 16, 2,
-                            4, 8, 16, 16, 2, 4, 8, 16, 1, 4, 8, 8, 16, 0};
+constexpr const int64_t *kSize = kOpalSize;
+constexpr const int64_t *kAlign = kOpalAlign;
+constexpr uint32_t kElemFlags = 0x01FFu & ~F_COMMITTED;   // OPAL_DATATYPE_FLAG_ELEM_MASK w/o COMMITTED
 
 constexpr size_t kListMin = 8;       // indexed runs longer than this become LIST nodes
 constexpr size_t kPatternMax = 256;  // max element starts kept for a merged mixed block
@@ -50,6 +48,8 @@ void init_predefined()
         n.blen = uint64_t(kSize[id]);
         n.extent = kSize[id];
         n.disp = 0;
+        // desc[0] of a predefined type (opal_datatype_module.c:418-426)
+        n.flags = F_PREDEFINED | F_DATA | F_CONTIGUOUS | F_NO_GAPS;
         t.desc.push_back(n);
         t.opt = t.desc;
         t.opt_prefix = {0, uint64_t(kSize[id])};
@@ -173,6 +173,7 @@ void type_add(ddt_datatype *base, const ddt_datatype *add, uint64_t count, int64
         n.esize = add->size;
         n.tid = add->id;
         n.disp = disp;
+        n.flags = add->flags & kElemFlags;
         if (extent == add->size) {
             n.count = 1;
             n.blen = count * uint64_t(add->size);
@@ -181,6 +182,8 @@ void type_add(ddt_datatype *base, const ddt_datatype *add, uint64_t count, int64
             n.count = count;
             n.blen = uint64_t(add->size);
             n.extent = extent;
+            if (count > 1)
+                n.flags &= ~(F_CONTIGUOUS | F_NO_GAPS);
         }
         base->desc.push_back(std::move(n));
     } else {
@@ -202,7 +205,8 @@ void type_add(ddt_datatype *base, const ddt_datatype *add, uint64_t count, int64
                 }
                 base->desc.push_back(e);
                 done = true;
-            } else if (extent == int64_t(e.count) * e.extent && e.count * count < (1ull << 40)) {
+            } else if (extent == int64_t(e.count) * e.extent && e.count * count <= 0xffffffffull) {
+                // the reference's element count is 32 bits; beyond it a loop is built (:379-390)
                 e.count *= count;
                 base->desc.push_back(e);
                 done = true;
@@ -217,6 +221,7 @@ void type_add(ddt_datatype *base, const ddt_datatype *add, uint64_t count, int64
                 l.kind = Node::LOOP;
                 l.count = count;
                 l.extent = extent;
+                l.flags = add->flags;
                 l.body = std::move(sub);
                 l.body_size = uint64_t(add->size);
                 base->desc.push_back(std::move(l));
@@ -335,6 +340,9 @@ ddt_datatype *build_indexed(const std::vector<Block> &blocks, const ddt_datatype
         n.kind = Node::LIST;
         n.esize = L->esize;
         n.tid = old->desc[0].tid;
+        // the flags of each block's DATA entry: the predefined type's own, or the copied
+        // entry of a one-entry derived type (opal_datatype_add.c:328-329, :359)
+        n.flags = is_predefined(old) ? (old->flags & kElemFlags) : old->desc[0].flags;
         n.list = finish_list(L);
         t->desc.push_back(std::move(n));
     } else {
@@ -477,11 +485,41 @@ void normalize(std::vector<Node> &nodes)
     nodes.swap(out);
 }
 
+bool opt_desc_of(const ddt_datatype *t, DescForm &out)
+{
+    DescForm in;
+    if (!build_opal_desc(t->desc, t->size, in))
+        return false;
+    uint32_t flags = 0;
+    optimize_desc(in, t->size, out, &flags);
+    return true;
+}
+
+// opal_datatype_commit (opal_datatype_optimize.c:1739-1782): the type map's Open MPI description
+// goes through the restated optimizer (ddt_optimize.cpp) and comes back as the committed tree, so
+// fragments and send positions stop on the reference's opt_desc elements.  An imported
+// description already is an opt_desc; a type map whose description the 32-byte form cannot hold
+// (a count beyond 32 bits) keeps its own elements.
 int commit(ddt_datatype *t)
 {
     if (t->flags & F_COMMITTED)
         return DDT_SUCCESS;
-    t->opt = t->desc;
+    bool optimized = false;
+    if (!t->imported) {
+        DescForm in, out;
+        std::vector<Node> nodes;
+        if (build_opal_desc(t->desc, t->size, in)) {
+            uint32_t flags = 0;
+            optimize_desc(in, t->size, out, &flags);
+            if (nodes_from_desc(out, nodes)) {
+                t->opt = std::move(nodes);
+                t->opt_flags = flags;
+                optimized = true;
+            }
+        }
+    }
+    if (!optimized)
+        t->opt = t->desc;
     normalize(t->opt);
     t->opt_prefix.assign(1, 0);
     for (const Node &n : t->opt)
@@ -977,7 +1015,20 @@ int ddt_type_commit(ddt_datatype_t *t)
 {
     if (!t)
         return DDT_ERR_BAD_PARAM;
-    return commit(t);
+    const int rc = commit(t);
+    if (rc == DDT_SUCCESS)
+        (void) prebuild_device(t);   // a large index list: its address-ordered tables now, not
+                                     // inside the first pack (a failure leaves that to first use)
+    return rc;
+}
+
+int ddt_type_prepare_device(ddt_datatype_t *t)
+{
+    if (!t)
+        return DDT_ERR_BAD_PARAM;
+    if (!(t->flags & F_COMMITTED))
+        return DDT_ERR_NOT_COMMITTED;
+    return prebuild_device(t);
 }
 
 int ddt_type_destroy(ddt_datatype_t **t)
@@ -1227,7 +1278,13 @@ struct Fold {
     }
 };
 
-bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<Node> &out)
+// `sealed`: the engine's own long index lists, passed through the optimizer whole
+// (ddt_optimize.h); a DATA entry of type 0 names one: count = its index, blocklen = the element
+// type, disp = the shift of every block.
+using SealedLists = std::vector<std::shared_ptr<const IndexList>>;
+
+bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<Node> &out,
+                const SealedLists *sealed = nullptr)
 {
     size_t i = begin;
     Fold run;
@@ -1236,6 +1293,26 @@ bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<
         uint16_t flags, type;
         std::memcpy(&flags, p, 2);
         std::memcpy(&type, p + 2, 2);
+        if ((flags & F_DATA) && type == 0 && sealed) {
+            uint32_t idx;
+            uint64_t tid;
+            int64_t shift;
+            std::memcpy(&idx, p + 4, 4);
+            std::memcpy(&tid, p + 8, 8);
+            std::memcpy(&shift, p + 24, 8);
+            if (idx >= sealed->size() || tid < 4 || tid > 27)
+                return false;
+            run.flush(out);
+            Node n;
+            n.kind = Node::LIST;
+            n.tid = uint16_t(tid);
+            n.esize = kSize[tid];
+            n.list = (*sealed)[idx];
+            n.disp = shift;
+            out.push_back(std::move(n));
+            ++i;
+            continue;
+        }
         if (flags & F_DATA) {
             uint32_t count;
             uint64_t blocklen;
@@ -1283,7 +1360,7 @@ bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<
             l.count = loops;
             l.extent = extent;
             l.body_size = size;
-            if (!parse_opal(raw, i + 1, endi, l.body))
+            if (!parse_opal(raw, i + 1, endi, l.body, sealed))
                 return false;
             uint64_t body = 0;
             for (const Node &n : l.body)
@@ -1300,6 +1377,7 @@ bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<
     return true;
 }
 }  // namespace
+
 
 namespace {
 // One entry per DATA block run / LOOP marker of the uncommitted type map, in the
@@ -1368,8 +1446,42 @@ int64_t ddt_type_to_opal_desc(const ddt_datatype_t *t, void *out, size_t cap)
     if (!t)
         return DDT_ERR_BAD_PARAM;
     std::vector<unsigned char> buf;
-    if (!export_nodes(t->desc, buf))
-        return DDT_ERR_NOT_SUPPORTED;
+    DescForm d;
+    if (t->imported) {
+        if (!export_nodes(t->desc, buf))
+            return DDT_ERR_NOT_SUPPORTED;
+    } else {
+        if (!build_opal_desc(t->desc, t->size, d))
+            return DDT_ERR_NOT_SUPPORTED;
+        encode_desc(d, buf);
+    }
+    const size_t used = buf.size() / 32;
+    if (used > cap)
+        return -int64_t(used);
+    if (out && used)
+        std::memcpy(out, buf.data(), buf.size());
+    return int64_t(used);
+}
+
+int64_t ddt_type_to_opal_opt_desc(const ddt_datatype_t *t, void *out, size_t cap, uint32_t *flags)
+{
+    if (!t)
+        return DDT_ERR_BAD_PARAM;
+    std::vector<unsigned char> buf;
+    uint32_t fl = t->opt_flags;
+    if (t->imported) {
+        if (!export_nodes(t->desc, buf))
+            return DDT_ERR_NOT_SUPPORTED;
+    } else {
+        DescForm in, o;
+        if (!build_opal_desc(t->desc, t->size, in))
+            return DDT_ERR_NOT_SUPPORTED;
+        fl = 0;
+        optimize_desc(in, t->size, o, &fl);
+        encode_desc(o, buf);
+    }
+    if (flags)
+        *flags = fl;
     const size_t used = buf.size() / 32;
     if (used > cap)
         return -int64_t(used);
@@ -1395,6 +1507,7 @@ int ddt_type_from_opal_desc(const void *desc, size_t used, size_t size, ptrdiff_
     t->true_ub = true_ub;
     t->flags = F_DATA;
     t->nbElems = 0;
+    t->imported = true;
     uint64_t s = 0;
     for (const Node &n : t->desc)
         s += n.packed_bytes();
@@ -1408,3 +1521,40 @@ int ddt_type_from_opal_desc(const void *desc, size_t used, size_t size, ptrdiff_
 }
 
 }  // extern "C"
+
+namespace ddt {
+// The committed tree of an optimized description: the bridge's own import (parse_opal), with
+// sealed lists carried through as LIST nodes.
+bool nodes_from_desc(const DescForm &d, std::vector<Node> &out)
+{
+    std::vector<unsigned char> raw(32 * d.used, 0);
+    for (size_t i = 0; i < d.used; ++i) {
+        const DescEntry &e = d.e[i];
+        unsigned char *p = raw.data() + 32 * i;
+        std::memcpy(p, &e.flags, 2);
+        if (e.sealed >= 0) {
+            const uint16_t zero = 0;
+            const uint32_t idx = uint32_t(e.sealed);
+            const uint64_t tid = e.type;
+            std::memcpy(p + 2, &zero, 2);
+            std::memcpy(p + 4, &idx, 4);
+            std::memcpy(p + 8, &tid, 8);
+            std::memcpy(p + 24, &e.disp, 8);
+            continue;
+        }
+        std::memcpy(p + 2, &e.type, 2);
+        std::memcpy(p + 4, &e.count, 4);
+        if (!(e.flags & F_DATA)) {
+            std::memcpy(p + 8, &e.loops, 4);
+            std::memcpy(p + 16, &e.blen, 8);
+            std::memcpy(p + 24, e.type == kDescLoop ? &e.extent : &e.disp, 8);
+        } else {
+            std::memcpy(p + 8, &e.blen, 8);
+            std::memcpy(p + 16, &e.extent, 8);
+            std::memcpy(p + 24, &e.disp, 8);
+        }
+    }
+    out.clear();
+    return parse_opal(raw.data(), 0, d.used, out, &d.lists);
+}
+}  // namespace ddt

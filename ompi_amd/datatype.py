@@ -127,6 +127,17 @@ class Datatype:
         got = check(lib().ddt_type_to_opal_desc(self.handle, buf, need), "ddt_type_to_opal_desc")
         return buf.raw[:got * 32]
 
+    def to_opal_opt_desc(self):
+        """(entries, flags): the committed opt_desc as Open MPI would derive it
+        (ddt_type_to_opal_opt_desc; flags & 0x10000 = OPAL_DATATYPE_OPTIMIZED_RESTRICTED)."""
+        fl = ctypes.c_uint32(0)
+        n = lib().ddt_type_to_opal_opt_desc(self.handle, None, 0, ctypes.byref(fl))
+        need = n if n >= 0 else -n
+        buf = ctypes.create_string_buffer(max(need, 1) * 32)
+        got = check(lib().ddt_type_to_opal_opt_desc(self.handle, buf, need, ctypes.byref(fl)),
+                    "ddt_type_to_opal_opt_desc")
+        return buf.raw[:got * 32], int(fl.value)
+
     def cache_info(self) -> dict:
         """Descriptor-set cache of the plan (ddt_type_cache_info)."""
         out = (ctypes.c_int64 * 4)()

@@ -120,10 +120,16 @@ def gather_packed(local, group=None):
     n = torch.tensor([local.numel()], device=local.device, dtype=torch.int64)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
-    mx = int(max(int(s.item()) for s in sizes))
+    lens = [int(s.item()) for s in sizes]
+    mx = max(lens)
+    if all(x == mx for x in lens):
+        # equal shards (the weak-scaling bench, an even split): gather in place, no padding copies
+        out = torch.empty(world * mx, dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+        return out
     buf = torch.zeros(mx, dtype=local.dtype, device=local.device)
     buf[:local.numel()] = local
     out = torch.empty(world * mx, dtype=local.dtype, device=local.device)
     dist.all_gather_into_tensor(out, buf, group=group)
-    parts = [out[r * mx: r * mx + int(sizes[r].item())] for r in range(world)]
+    parts = [out[r * mx: r * mx + lens[r]] for r in range(world)]
     return torch.cat(parts)

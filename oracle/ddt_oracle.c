@@ -50,6 +50,24 @@ typedef struct {
     int64_t tid;   /* OPAL id of those elements (external32 conversion) */
 } ort_run;
 
+/* One entry of an Open MPI description (dt_elem_desc_t, opal_datatype_internal.h:119-169),
+ * fields by role:  DATA      {flags, type >= 4, count, -, blocklen (elements), extent, disp}
+ *                  LOOP      {flags, 0, items, loops, -, extent, -}
+ *                  END_LOOP  {flags, 1, items, -, size, -, first_elem_disp}           */
+typedef struct {
+    uint16_t flags, type;
+    uint32_t count;
+    uint32_t loops;
+    uint64_t blocklen;
+    int64_t extent;
+    int64_t disp;
+} ort_elem;
+
+typedef struct {
+    ort_elem *e;
+    int64_t used, cap;
+} ort_desc;
+
 typedef struct ort_type {
     int id; /* OPAL predefined id, 0 for derived */
     uint32_t flags;
@@ -61,6 +79,16 @@ typedef struct ort_type {
     int64_t *pref; /* packed offset of each run (built lazily at first pack) */
     struct ort_group *grp; /* the runs as arithmetic progressions (built with pref) */
     int64_t ngrp;
+    ort_desc desc;   /* opal_datatype_t::desc as opal_datatype_add builds it */
+    /* built lazily by ort_commit: opal_datatype_t::opt_desc (opal_datatype_commit), the
+     * OPTIMIZED_RESTRICTED bit, and opt_desc flattened to runs of one carrier type -- the
+     * predefined elements a pack fragment never splits and a send position snaps to */
+    int committed;
+    ort_desc opt;
+    uint32_t opt_flags;
+    ort_run *oruns;
+    int64_t noruns, ocap;
+    int64_t *opref;
 } ort_type;
 
 /* Blocks of equal length at a constant stride (runs abutting in memory fused): the DATA entry
@@ -91,6 +119,19 @@ static ort_type *ort_new(void)
     return t;
 }
 
+static void ort_drop_commit(ort_type *t)
+{
+    free(t->opt.e);
+    free(t->oruns);
+    free(t->opref);
+    memset(&t->opt, 0, sizeof(t->opt));
+    t->oruns = NULL;
+    t->opref = NULL;
+    t->noruns = t->ocap = 0;
+    t->opt_flags = 0;
+    t->committed = 0;
+}
+
 void ort_free(ort_type *t)
 {
     if (!t)
@@ -98,29 +139,43 @@ void ort_free(ort_type *t)
     free(t->runs);
     free(t->pref);
     free(t->grp);
+    free(t->desc.e);
+    ort_drop_commit(t);
     free(t);
 }
 
-static void ort_push_run(ort_type *t, int64_t disp, int64_t len, int64_t esize, int64_t tid)
+static void run_append(ort_run **runs, int64_t *n, int64_t *cap, int64_t disp, int64_t len,
+                       int64_t esize, int64_t tid)
 {
     if (len <= 0)
         return;
-    if (t->nruns > 0) {
-        ort_run *p = &t->runs[t->nruns - 1];
+    if (*n > 0) {
+        ort_run *p = &(*runs)[*n - 1];
         if (p->disp + p->len == disp && p->esize == esize && p->tid == tid) {
             p->len += len;
             return;
         }
     }
-    if (t->nruns == t->cap) {
-        t->cap = t->cap ? 2 * t->cap : 16;
-        t->runs = (ort_run *) realloc(t->runs, (size_t) t->cap * sizeof(ort_run));
+    if (*n == *cap) {
+        *cap = *cap ? 2 * *cap : 16;
+        *runs = (ort_run *) realloc(*runs, (size_t) *cap * sizeof(ort_run));
     }
-    t->runs[t->nruns].disp = disp;
-    t->runs[t->nruns].len = len;
-    t->runs[t->nruns].esize = esize;
-    t->runs[t->nruns].tid = tid;
-    t->nruns++;
+    (*runs)[*n] = (ort_run){disp, len, esize, tid};
+    (*n)++;
+}
+
+static void ort_push_run(ort_type *t, int64_t disp, int64_t len, int64_t esize, int64_t tid)
+{
+    run_append(&t->runs, &t->nruns, &t->cap, disp, len, esize, tid);
+}
+
+static void od_push(ort_desc *d, ort_elem x)
+{
+    if (d->used == d->cap) {
+        d->cap = d->cap ? 2 * d->cap : 16;
+        d->e = (ort_elem *) realloc(d->e, (size_t) d->cap * sizeof(ort_elem));
+    }
+    d->e[d->used++] = x;
 }
 
 ort_type *ort_basic(int id)
@@ -138,6 +193,10 @@ ort_type *ort_basic(int id)
     t->nbElems = 1;
     t->flags = ORT_FLAG_PREDEFINED | ORT_FLAG_CONTIGUOUS | ORT_FLAG_NO_GAPS | ORT_FLAG_DATA;
     ort_push_run(t, 0, t->size, t->size, id);
+    /* desc[0] of a predefined type (opal_datatype_module.c:418-426) */
+    od_push(&t->desc, (ort_elem){ORT_FLAG_PREDEFINED | ORT_FLAG_DATA | ORT_FLAG_CONTIGUOUS
+                                     | ORT_FLAG_NO_GAPS,
+                                 (uint16_t) id, 1, 0, 1, t->size, 0});
     return t;
 }
 
@@ -166,11 +225,106 @@ ort_type *ort_dup(const ort_type *o)
     t->pref = NULL;
     t->grp = NULL;
     t->ngrp = 0;
+    /* opal_datatype_clone copies the description (opal_datatype_clone.c:51-53); the
+     * optimized one is a function of it and is rebuilt on demand */
+    t->desc.e = (ort_elem *) malloc((size_t) (o->desc.used ? o->desc.used : 1) * sizeof(ort_elem));
+    memcpy(t->desc.e, o->desc.e, (size_t) o->desc.used * sizeof(ort_elem));
+    t->desc.used = t->desc.cap = o->desc.used;
+    memset(&t->opt, 0, sizeof(t->opt));
+    t->committed = 0;
+    t->opt_flags = 0;
+    t->oruns = NULL;
+    t->opref = NULL;
+    t->noruns = t->ocap = 0;
     return t;
 }
 
 static inline int64_t lmin(int64_t a, int64_t b) { return a < b ? a : b; }
 static inline int64_t lmax(int64_t a, int64_t b) { return a < b ? b : a; }
+
+#define ORT_FLAG_COMMITTED 0x0004u
+#define ORT_ELEM_MASK 0x01FFu         /* OPAL_DATATYPE_FLAG_ELEM_MASK (opal_datatype.h:116-119) */
+#define ORT_TYPE_CHANGED 0x0200u      /* OPAL_DATATYPE_OPTIMIZED_TYPE_CHANGED (_internal.h:317) */
+#define ORT_RESTRICTED 0x00010000u    /* OPAL_DATATYPE_OPTIMIZED_RESTRICTED (opal_datatype.h:136) */
+#define ORT_BASIC (0x0002u | 0x0010u | 0x0020u | 0x0100u | 0x0004u) /* OPAL_DATATYPE_FLAG_BASIC */
+#define OE_LOOP 0
+#define OE_END_LOOP 1
+
+static ort_elem oe_loop(uint32_t loops, uint32_t items, int64_t extent, uint32_t flags)
+{   /* CREATE_LOOP_START (opal_datatype_internal.h:171-180) */
+    return (ort_elem){(uint16_t) (flags & ~ORT_FLAG_DATA), OE_LOOP, items, loops, UINT64_MAX, extent, 0};
+}
+
+static ort_elem oe_end(uint32_t items, int64_t first_disp, uint64_t size, uint32_t flags)
+{   /* CREATE_LOOP_END (:182-190) */
+    return (ort_elem){(uint16_t) (flags & ~ORT_FLAG_DATA), OE_END_LOOP, items, UINT32_MAX, size, 0,
+                      first_disp};
+}
+
+/* The description half of opal_datatype_add (opal_datatype_add.c:307-431): `count` replicas
+ * of `add` at disp + i*extent appended to base->desc. */
+static void ort_add_desc(ort_type *base, const ort_type *add, int64_t count, int64_t disp, int64_t extent)
+{
+    if ((add->flags & (ORT_FLAG_PREDEFINED | ORT_FLAG_DATA)) == (ORT_FLAG_PREDEFINED | ORT_FLAG_DATA)) {
+        /* a predefined element (:319-345) */
+        ort_elem e = {(uint16_t) (add->flags & (ORT_ELEM_MASK & ~ORT_FLAG_COMMITTED)), (uint16_t) add->id,
+                      1, 0, (uint64_t) count, count * extent, disp};
+        if (extent != add->size) {
+            e.count = (uint32_t) count;
+            e.blocklen = 1;
+            e.extent = extent;
+            if (count > 1)
+                e.flags &= (uint16_t) ~(ORT_FLAG_CONTIGUOUS | ORT_FLAG_NO_GAPS);
+        }
+        od_push(&base->desc, e);
+        return;
+    }
+    if (1 == add->desc.used) {   /* a one-entry description (:358-397) */
+        ort_elem e = add->desc.e[0];
+        e.disp += disp;
+        if (1 == count) {
+        } else if (1 == e.count) {
+            if (add->desc.e[0].extent == extent) {
+                e.blocklen *= (uint64_t) count;
+                e.extent *= count;
+            } else {
+                e.count = (uint32_t) count;
+                e.extent = extent;
+            }
+        } else if (extent == (int64_t) e.count * e.extent) {
+            uint32_t cnt = (uint32_t) ((uint64_t) e.count * (uint64_t) count);
+            if (cnt < e.count)
+                goto build_loop;
+            e.count = cnt;
+        } else {
+            goto build_loop;
+        }
+        od_push(&base->desc, e);
+        return;
+    }
+build_loop: /* (:400-431) */
+    {
+        const uint32_t lflags = add->flags & (ORT_ELEM_MASK & ~ORT_FLAG_COMMITTED);
+        const int64_t at = base->desc.used;
+        if (count != 1)
+            od_push(&base->desc, oe_loop((uint32_t) count, (uint32_t) add->desc.used + 1, extent, lflags));
+        for (int64_t i = 0; i < add->desc.used; i++) {
+            ort_elem e = add->desc.e[i];
+            if (e.flags & ORT_FLAG_DATA)
+                e.disp += disp;
+            else if (e.type == OE_END_LOOP)
+                e.disp += disp;
+            od_push(&base->desc, e);
+        }
+        if (count != 1) {
+            int64_t k = at;   /* GET_FIRST_NON_LOOP from the new LOOP */
+            while (base->desc.e[k].type == OE_LOOP)
+                k++;
+            od_push(&base->desc, oe_end((uint32_t) add->desc.used + 1, base->desc.e[k].disp,
+                                        (uint64_t) add->size, lflags));
+        }
+    }
+}
 
 /* Bounds/flags of opal_datatype_add (opal_datatype_add.c:133-460) + type-map append. */
 static void ort_add(ort_type *base, const ort_type *add, int64_t count, int64_t disp, int64_t extent)
@@ -233,6 +387,7 @@ static void ort_add(ort_type *base, const ort_type *add, int64_t count, int64_t 
         base->flags |= (add->flags & ORT_FLAG_USER_LB);
         base->flags |= (add->flags & ORT_FLAG_USER_UB);
     }
+    ort_add_desc(base, add, count, disp, extent);
     /* type map: count replicas of add's map at disp + i*extent, in order */
     for (int64_t i = 0; i < count; i++) {
         int64_t off = disp + i * extent;
@@ -617,6 +772,651 @@ void ort_run_at(const ort_type *t, int64_t i, int64_t *out)
     out[2] = t->runs[i].esize;
 }
 
+/* =====================================================================================
+ * opal_datatype_commit: the description optimizer (opal/datatype/opal_datatype_optimize.c),
+ * restated with the run-time defaults of opal_datatype_module.c:85-88 (max_desc_growth 10,
+ * loop_unroll_max_items 8, loop_unroll_max_data_bytes 128, preserve_type true) and
+ * OPAL_DATATYPE_OPTIMIZE_ALL.  The result decides where the accelerator movers may stop a
+ * pack fragment (a predefined element of opt_desc is never split,
+ * opal_datatype_pack_accelerator.c:52-58) and where a send convertor's position lands
+ * (opal_datatype_position.c:167-367 walks opt_desc): a fused mixed-type region is re-typed to
+ * the widest UINT8/4/2 carrier that tiles it, or UINT1.
+ * ===================================================================================== */
+#define OX_UNROLL_ITEMS 8u
+#define OX_UNROLL_BYTES 128u
+#define OX_GROWTH 10
+#define OX_INLINE_BLOCKLEN 8u   /* OPAL_DATATYPE_PREDEFINED_MAX_INLINE_BLOCKLEN (_internal.h:103) */
+#define OX_UNAVAILABLE 0xFFFFu
+
+static inline int64_t ox_bytes(const ort_elem *e) { return (int64_t) e->blocklen * ort_basic_size[e->type]; }
+
+/* CREATE_ELEM (opal_datatype_internal.h:195-209): a block stream whose stride equals its block
+ * is collapsed into one block */
+static void ox_elem(ort_desc *o, uint16_t type, uint32_t flags, uint64_t blocklen, uint32_t count,
+                    int64_t disp, int64_t extent)
+{
+    ort_elem e = {(uint16_t) (flags | ORT_FLAG_DATA), type, count, 0, blocklen, extent, disp};
+    if (extent == (int64_t) (blocklen * (uint64_t) ort_basic_size[type])) {
+        e.blocklen *= count;
+        e.extent *= count;
+        e.count = 1;
+    }
+    od_push(o, e);
+}
+
+static inline uint32_t ox_keep(uint32_t flags) { return ORT_BASIC | (flags & ORT_TYPE_CHANGED); }
+
+/* opal_datatype_opt_next_item (:57-65) */
+static uint32_t ox_next(const ort_elem *d, int64_t pos, uint32_t item)
+{
+    return d[pos + item].type == OE_LOOP ? item + d[pos + item].count + 1 : item + 1;
+}
+
+/* opal_datatype_opt_loop_unroll_factor (:72-110) */
+static uint32_t ox_unroll_factor(const ort_elem *d, int64_t pos)
+{
+    const ort_elem *L = &d[pos], *E = &d[pos + L->count];
+    if (L->loops < 4 || L->count < 2 || (L->flags & ORT_FLAG_CONTIGUOUS) || E->type != OE_END_LOOP)
+        return 1;
+    const uint32_t body = L->count - 1;
+    if (OX_UNROLL_ITEMS < body)
+        return 1;
+    for (uint32_t k = 0; k < body; k++) {
+        const ort_elem *e = &d[pos + k + 1];
+        if (!(e->flags & ORT_FLAG_DATA))
+            return 1;
+        const uint64_t ts = (uint64_t) ort_basic_size[e->type];
+        if (ts == 0 || e->blocklen == 0 || e->blocklen > OX_UNROLL_BYTES / ts)
+            return 1;
+        if (e->count > OX_UNROLL_BYTES / (e->blocklen * ts))
+            return 1;
+    }
+    uint32_t f = OX_UNROLL_ITEMS / body, lf = L->loops / 2;
+    f = f < lf ? f : lf;
+    return f > 1 ? f : 1;
+}
+
+/* opal_datatype_opt_loop_is_innermost (:113-123) */
+static int ox_innermost(const ort_elem *d, int64_t pos)
+{
+    for (uint32_t k = 1; k < d[pos].count; k++)
+        if (d[pos + k].type == OE_LOOP)
+            return 0;
+    return 1;
+}
+
+/* opal_datatype_opt_emit_unrolled_loop (:165-215) */
+static void ox_emit_unrolled(ort_desc *o, const ort_elem *d, int64_t pos, uint32_t f)
+{
+    const ort_elem *L = &d[pos], *E = &d[pos + L->count];
+    const uint32_t body = L->count - 1, iters = L->loops / f, tail = L->loops % f, items = body * f;
+    od_push(o, oe_loop(iters, items + 1, L->extent * f, L->flags));
+    for (uint32_t it = 0; it < f; it++)
+        for (uint32_t k = 0; k < body; k++) {
+            const ort_elem *e = &d[pos + k + 1];
+            ox_elem(o, e->type, ox_keep(e->flags), e->blocklen, e->count,
+                    e->disp + (int64_t) it * L->extent, e->extent);
+        }
+    od_push(o, oe_end(items + 1, E->disp, E->blocklen * f, E->flags));
+    for (uint32_t it = 0; it < tail; it++) {
+        const int64_t at = (int64_t) (iters * f + it) * L->extent;
+        for (uint32_t k = 0; k < body; k++) {
+            const ort_elem *e = &d[pos + k + 1];
+            ox_elem(o, e->type, ox_keep(e->flags), e->blocklen, e->count, e->disp + at, e->extent);
+        }
+    }
+}
+
+/* opal_datatype_opt_collapse_elem (:539-549) */
+static void ox_collapse(ort_elem *e)
+{
+    if (e->count > 1 && e->extent == ox_bytes(e)) {
+        e->blocklen *= e->count;
+        e->extent *= e->count;
+        e->count = 1;
+    }
+}
+
+/* opal_datatype_opt_promoted_type (:581-611): UINT8 (12), UINT4 (11), UINT2 (10), else UINT1 (9) */
+static uint16_t ox_carrier(int64_t disp, int64_t extent, uint32_t count, int64_t bytes)
+{
+    static const uint16_t cand[3] = {12, 11, 10};
+    for (int k = 0; k < 3; k++) {
+        const uint64_t sz = (uint64_t) ort_basic_size[cand[k]], al = (uint64_t) ort_basic_align[cand[k]];
+        if ((uint64_t) bytes % sz)
+            continue;
+        if ((uint64_t) disp & (al - 1))
+            continue;
+        if (count > 1 && ((uint64_t) extent & (al - 1)))
+            continue;
+        return cand[k];
+    }
+    return 9;
+}
+
+/* opal_datatype_opt_set_mixed_region (:618-630) */
+static void ox_mixed(ort_elem *e, int64_t bytes, uint32_t count, int64_t disp, int64_t extent)
+{
+    const uint16_t t = ox_carrier(disp, extent, count, bytes);
+    e->type = t;
+    e->flags = ORT_BASIC | ORT_TYPE_CHANGED;
+    e->blocklen = (uint64_t) (bytes / ort_basic_size[t]);
+    e->count = count;
+    e->disp = disp;
+    e->extent = extent;
+}
+
+static int ox_item_as_elem(const ort_elem *d, int64_t pos, uint32_t item, ort_elem *out);
+
+/* opal_datatype_opt_compress_contiguous_loop (:641-709) */
+static int ox_compress(const ort_elem *d, int64_t pos, ort_elem *out)
+{
+    const ort_elem *L = &d[pos], *E = &d[pos + L->count];
+    uint16_t ctype = OX_UNAVAILABLE;
+    uint32_t cflags = ORT_BASIC;
+    uint64_t cblen = 0;
+    int homog = 1, any = 0;
+    if (!(L->flags & ORT_FLAG_CONTIGUOUS))
+        return 0;
+    for (uint32_t i = 1; i < L->count; i = ox_next(d, pos, i)) {
+        ort_elem cur;
+        any = 1;
+        if (!ox_item_as_elem(d, pos, i, &cur)) {
+            homog = 0;
+            break;
+        }
+        if (ctype == OX_UNAVAILABLE) {
+            ctype = cur.type;
+            cblen = cur.blocklen;
+            cflags |= cur.flags & ORT_TYPE_CHANGED;
+            continue;
+        }
+        if (ctype != cur.type) {
+            homog = 0;
+            break;
+        }
+        cblen += cur.blocklen;
+        cflags |= cur.flags & ORT_TYPE_CHANGED;
+    }
+    if (!any)
+        return 0;
+    if (homog) {
+        const uint64_t ts = (uint64_t) ort_basic_size[ctype];
+        if (ts == 0 || E->blocklen % ts || E->blocklen != cblen * ts) {
+            homog = 0;
+        } else {
+            out->type = ctype;
+            out->flags = (uint16_t) cflags;
+            out->blocklen = E->blocklen / ts;
+        }
+    }
+    if (!homog)
+        ox_mixed(out, (int64_t) E->blocklen, L->loops, E->disp, L->extent);
+    else {
+        out->count = L->loops;
+        out->extent = L->extent;
+        out->disp = E->disp;
+    }
+    ox_collapse(out);
+    return 1;
+}
+
+/* opal_datatype_opt_item_as_elem (:716-734) */
+static int ox_item_as_elem(const ort_elem *d, int64_t pos, uint32_t item, ort_elem *out)
+{
+    const ort_elem *e = &d[pos + item];
+    if (e->flags & ORT_FLAG_DATA) {
+        *out = *e;
+        out->flags = (uint16_t) ox_keep(out->flags);
+        ox_collapse(out);
+        return out->count == 1;
+    }
+    if (e->type == OE_LOOP)
+        return ox_compress(d, pos + item, out) && out->count == 1;
+    return 0;
+}
+
+/* opal_datatype_opt_fuse_tail_head (:741-786) */
+static int ox_fuse_tail_head(uint32_t *dflags, const ort_elem *tail, const ort_elem *head, int64_t head_delta,
+                             uint32_t rcount, int64_t rextent, ort_elem *fused)
+{
+    if (tail->count != 1 || head->count != 1)
+        return 0;
+    const int64_t ts = ox_bytes(tail), hs = ox_bytes(head);
+    if (tail->disp + ts != head->disp + head_delta)
+        return 0;
+    *fused = *tail;
+    if (tail->type == head->type) {
+        fused->flags = (uint16_t) (ORT_BASIC | ((tail->flags | head->flags) & ORT_TYPE_CHANGED));
+        fused->blocklen += head->blocklen;
+    } else {
+        ox_mixed(fused, ts + hs, rcount, tail->disp, rextent);
+    }
+    fused->count = 1;
+    fused->extent = ts + hs;
+    if (fused->flags & ORT_TYPE_CHANGED)
+        *dflags |= ORT_RESTRICTED;
+    return 1;
+}
+
+/* opal_datatype_opt_emit_desc_range (:515-533) */
+static void ox_copy_range(ort_desc *o, const ort_elem *d, int64_t pos, uint32_t from, uint32_t to, int64_t delta)
+{
+    for (uint32_t i = from; i < to; i++) {
+        ort_elem e = d[pos + i];
+        if (e.flags & ORT_FLAG_DATA) {
+            e.flags = (uint16_t) ox_keep(e.flags);
+            e.disp += delta;
+        } else if (e.type == OE_END_LOOP) {
+            e.disp += delta;
+        }
+        od_push(o, e);
+    }
+}
+
+/* opal_datatype_optimize_loop_boundary (:799-888) */
+static int ox_loop_boundary(uint32_t *dflags, const ort_elem *d, int64_t pos, ort_desc *o)
+{
+    const ort_elem *L = &d[pos], *E = &d[pos + L->count];
+    uint32_t last_item = 0, nitems = 0;
+    if (L->loops < 2 || L->count <= 2)
+        return 0;
+    for (uint32_t i = 1; i < L->count; i = ox_next(d, pos, i)) {
+        if (d[pos + i].type != OE_LOOP && !(d[pos + i].flags & ORT_FLAG_DATA))
+            return 0;
+        last_item = i;
+        nitems++;
+    }
+    if (nitems < 2 || last_item == 0)
+        return 0;
+    const uint32_t after_first = ox_next(d, pos, 1);
+    ort_elem first, last, fused;
+    if (!ox_item_as_elem(d, pos, 1, &first) || !ox_item_as_elem(d, pos, last_item, &last))
+        return 0;
+    if (!ox_fuse_tail_head(dflags, &last, &first, L->extent, L->loops - 1, L->extent, &fused))
+        return 0;
+    ox_copy_range(o, d, pos, 1, last_item, 0);
+    if (nitems == 2) {
+        ox_elem(o, fused.type, fused.flags, fused.blocklen, L->loops - 1, fused.disp, L->extent);
+    } else {
+        const uint32_t steady = last_item - after_first + 2;
+        od_push(o, oe_loop(L->loops - 1, steady, L->extent, L->flags));
+        ox_elem(o, fused.type, fused.flags, fused.blocklen, 1, fused.disp, fused.extent);
+        ox_copy_range(o, d, pos, after_first, last_item, L->extent);
+        od_push(o, oe_end(steady, fused.disp, E->blocklen, L->flags));
+    }
+    ox_elem(o, last.type, last.flags, last.blocklen, last.count,
+            last.disp + (int64_t) (L->loops - 1) * L->extent, last.extent);
+    return 1;
+}
+
+/* opal_datatype_opt_loop_nesting_depth (:222-241) */
+static int64_t ox_depth(const ort_desc *d)
+{
+    int64_t depth = 0, mx = 0;
+    for (int64_t i = 0; i < d->used; i++) {
+        if (d->e[i].type == OE_LOOP) {
+            if (++depth > mx)
+                mx = depth;
+        } else if (d->e[i].type == OE_END_LOOP && depth > 0) {
+            --depth;
+        }
+    }
+    return mx;
+}
+
+/* opal_datatype_optimize_short (:890-1295) on `in` (END_LOOP sentinel at in->e[in->used]) */
+static void ox_short(uint32_t *dflags, const ort_desc *in, ort_desc *o, int enable_boundary,
+                     int top_only, int *expanded, int *reevaluate)
+{
+    const ort_elem *d = in->e;
+    const int64_t depth = ox_depth(in) + 2;
+    int64_t *sidx = (int64_t *) malloc((size_t) depth * sizeof(int64_t));
+    char *inner = (char *) calloc((size_t) depth, 1);
+    int64_t pos = 0, sp = 0;
+    ort_elem last = {0xFFFF, 0, 0, 0, 0, 0, 0}, cur, cmp;
+    memset(o, 0, sizeof(*o));
+    if (expanded)
+        *expanded = 0;
+    if (reevaluate)
+        *reevaluate = 0;
+    sidx[0] = -1;
+    while (sp >= 0) {
+        const ort_elem *e = &d[pos];
+        if (e->type == OE_END_LOOP) {
+            if (last.count) {
+                ox_elem(o, last.type, ox_keep(last.flags), last.blocklen, last.count, last.disp, last.extent);
+                last.count = 0;
+            }
+            const uint32_t items = (uint32_t) (o->used - sidx[sp] + 1);
+            od_push(o, oe_end(items, e->disp, e->blocklen, e->flags));
+            if (--sp >= 0)
+                o->e[sidx[sp + 1] - 1].count = items;   /* the LOOP's item count */
+            pos++;
+            continue;
+        }
+        if (e->type == OE_LOOP) {
+            const ort_elem *L = e;
+            if ((L->flags & ORT_FLAG_CONTIGUOUS) && ox_compress(d, pos, &cmp)) {
+                if (reevaluate)
+                    *reevaluate = 1;
+                if (cmp.flags & ORT_TYPE_CHANGED)
+                    *dflags |= ORT_RESTRICTED;
+                pos += L->count + 1;
+                cur = cmp;
+                goto fuse;
+            }
+            if (last.count) {
+                ox_elem(o, last.type, ox_keep(last.flags), last.blocklen, last.count, last.disp, last.extent);
+                last.count = 0;
+                last.type = OE_LOOP;
+            }
+            if (L->count <= 4 && L->loops <= 2 && ox_innermost(d, pos)) {
+                /* fully expand a short innermost loop (:1054-1082) */
+                if (reevaluate)
+                    *reevaluate = 1;
+                int64_t shift = 0;
+                for (uint32_t i = 0; i < L->loops; i++) {
+                    for (uint32_t j = 0; j + 1 < L->count; j++) {
+                        const ort_elem *c = &d[pos + 1 + j];
+                        ox_elem(o, c->type, ox_keep(c->flags), c->blocklen, c->count, c->disp + shift, c->extent);
+                    }
+                    shift += L->extent;
+                }
+                pos += L->count + 1;
+                continue;
+            }
+            if (enable_boundary && (!top_only || sp == 0) && ox_loop_boundary(dflags, d, pos, o)) {
+                if (expanded)
+                    *expanded = 1;
+                pos += L->count + 1;
+                continue;
+            }
+            {
+                const uint32_t f = ox_unroll_factor(d, pos);
+                if (f > 1) {
+                    ox_emit_unrolled(o, d, pos, f);
+                    pos += L->count + 1;
+                    continue;
+                }
+            }
+            od_push(o, oe_loop(L->loops, L->count, L->extent, L->flags));
+            sp++;
+            sidx[sp] = o->used;
+            inner[sp] = (char) ox_innermost(d, pos);
+            pos++;
+            continue;
+        }
+        /* a DATA entry */
+        cur = *e;
+        cur.flags = (uint16_t) ox_keep(cur.flags);
+        pos++;
+    fuse:
+        if (last.count == 0) {
+            last = cur;
+            continue;
+        }
+        if (ox_bytes(&last) == last.extent) {
+            last.extent *= last.count;
+            last.blocklen *= last.count;
+            last.count = 1;
+        }
+        {
+            const int64_t lbs = ox_bytes(&last), cbs = ox_bytes(&cur);
+            if (lbs == cbs) {   /* same block size: one entry of count last+cur (:1170-1207) */
+                const int mixed = last.type != cur.type;
+                int64_t mext = last.extent;
+                const uint32_t mcount = last.count + cur.count;
+                int can = 0;
+                if ((last.extent * (int64_t) last.count + last.disp) == cur.disp
+                    && (cur.count == 1 || last.extent == cur.extent)) {
+                    can = 1;
+                } else if (last.count == 1 && (cur.count == 1 || (last.disp + cur.extent) == cur.disp)) {
+                    mext = cur.count == 1 ? cur.disp - last.disp : cur.extent;
+                    can = 1;
+                }
+                if (can) {
+                    if (reevaluate && inner[sp])
+                        *reevaluate = 1;
+                    if (mixed) {
+                        ox_mixed(&last, lbs, mcount, last.disp, mext);
+                        *dflags |= ORT_RESTRICTED;
+                    } else {
+                        last.flags |= cur.flags & ORT_TYPE_CHANGED;
+                        last.extent = mext;
+                        last.count = mcount;
+                    }
+                    continue;
+                }
+            }
+            /* fuse the last block of `last` with the first of `cur` (:1208-1268) */
+            const int inline_pair = last.count > 1 && cur.count > 1 && last.blocklen <= OX_INLINE_BLOCKLEN
+                                    && cur.blocklen <= OX_INLINE_BLOCKLEN;
+            if (!inline_pair && (last.disp + (int64_t) (last.count - 1) * last.extent + lbs) == cur.disp) {
+                const int shrinks = last.count == 1 && cur.count == 1;
+                const int64_t fext = last.extent + cur.extent;
+                if (shrinks && reevaluate && inner[sp])
+                    *reevaluate = 1;
+                if (last.count != 1) {
+                    ox_elem(o, last.type, ox_keep(last.flags), last.blocklen, last.count - 1, last.disp,
+                            last.extent);
+                    last.disp += (int64_t) (last.count - 1) * last.extent;
+                    last.count = 1;
+                }
+                if (last.type == cur.type) {
+                    last.flags |= cur.flags & ORT_TYPE_CHANGED;
+                    last.blocklen += cur.blocklen;
+                } else {
+                    ox_mixed(&last, lbs + cbs, 1, last.disp, fext);
+                    *dflags |= ORT_RESTRICTED;
+                }
+                last.extent = fext;
+                if (cur.count != 1) {
+                    ox_elem(o, last.type, ox_keep(last.flags), last.blocklen, last.count, last.disp, last.extent);
+                    last = cur;
+                    last.count -= 1;
+                    last.disp += last.extent;
+                }
+                continue;
+            }
+        }
+        ox_elem(o, last.type, ox_keep(last.flags), last.blocklen, last.count, last.disp, last.extent);
+        last = cur;
+    }
+    if (last.count)
+        ox_elem(o, last.type, ox_keep(last.flags), last.blocklen, last.count, last.disp, last.extent);
+    o->used -= 1;   /* the sentinel END_LOOP stays at o->e[o->used] */
+    free(sidx);
+    free(inner);
+}
+
+/* opal_datatype_opt_count_range_groups_desc (:406-435) */
+static uint64_t ox_ranges(const ort_elem *d, int64_t start, int64_t end)
+{
+    uint64_t r = 0;
+    for (int64_t pos = start; pos < end;) {
+        const ort_elem *e = &d[pos];
+        if (e->flags & ORT_FLAG_DATA) {
+            r += e->count;
+            pos++;
+        } else if (e->type == OE_LOOP) {
+            const uint64_t lr = (e->flags & ORT_FLAG_CONTIGUOUS) ? 1 : ox_ranges(d, pos + 1, pos + e->count);
+            r += lr * e->loops;
+            pos += e->count + 1;
+        } else {
+            pos++;
+        }
+    }
+    return r;
+}
+
+static void ox_free(ort_desc *d)
+{
+    free(d->e);
+    memset(d, 0, sizeof(*d));
+}
+
+/* opal_datatype_optimize_short_restart (:1347-1478) */
+static void ox_restart(uint32_t *dflags, const ort_desc *in, ort_desc *out)
+{
+    const int64_t limit = in->used * OX_GROWTH;
+    const uint32_t init = *dflags;
+    ort_desc cand, next, base;
+    int expanded = 0, reeval = 0, any_expanded;
+    *dflags = init;
+    ox_short(dflags, in, &cand, 1, 0, &expanded, &reeval);
+    uint32_t cand_flags = *dflags;
+    any_expanded = expanded;
+    if (!expanded && !reeval) {
+        *out = cand;
+        return;
+    }
+    uint64_t cand_ranges = ox_ranges(cand.e, 0, cand.used);
+    while (expanded || reeval) {
+        int nexp = 0, nre = 0;
+        if (cand.used > limit)
+            break;
+        *dflags = init | (cand_flags & ORT_RESTRICTED);
+        ox_short(dflags, &cand, &next, 1, 0, &nexp, &nre);
+        const uint64_t nr = ox_ranges(next.e, 0, next.used);
+        if (next.used > limit || (nexp && nr >= cand_ranges)) {
+            ox_free(&next);
+            break;
+        }
+        any_expanded |= nexp;
+        cand_flags = *dflags;
+        ox_free(&cand);
+        cand = next;
+        cand_ranges = nr;
+        expanded = nexp;
+        reeval = nre;
+    }
+    if (!any_expanded) {
+        *out = cand;
+        *dflags = init | (cand_flags & ORT_RESTRICTED);
+        return;
+    }
+    *dflags = init;
+    reeval = 0;
+    ox_short(dflags, in, &base, 0, 0, NULL, &reeval);
+    uint32_t base_flags = *dflags;
+    while (reeval) {
+        int nre = 0;
+        *dflags = init | (base_flags & ORT_RESTRICTED);
+        ox_short(dflags, &base, &next, 0, 0, NULL, &nre);
+        if (next.used > limit) {
+            ox_free(&next);
+            break;
+        }
+        base_flags = *dflags;
+        ox_free(&base);
+        base = next;
+        reeval = nre;
+    }
+    const uint64_t base_ranges = ox_ranges(base.e, 0, base.used);
+    if (cand.used <= limit && cand_ranges < base_ranges) {
+        ox_free(&base);
+        *out = cand;
+        *dflags = init | (cand_flags & ORT_RESTRICTED);
+    } else {
+        ox_free(&cand);
+        *out = base;
+        *dflags = init | (base_flags & ORT_RESTRICTED);
+    }
+}
+
+/* flatten one level of a description into carrier runs: instance-relative disp `at` */
+static void ox_flatten(ort_type *t, const ort_elem *d, int64_t begin, int64_t end, int64_t at)
+{
+    for (int64_t pos = begin; pos < end;) {
+        const ort_elem *e = &d[pos];
+        if (e->flags & ORT_FLAG_DATA) {
+            const int64_t es = ort_basic_size[e->type], bl = (int64_t) e->blocklen * es;
+            for (uint32_t k = 0; k < e->count; k++)
+                run_append(&t->oruns, &t->noruns, &t->ocap, at + e->disp + (int64_t) k * e->extent, bl, es,
+                           e->type);
+            pos++;
+        } else if (e->type == OE_LOOP) {
+            for (uint32_t k = 0; k < e->loops; k++)
+                ox_flatten(t, d, pos + 1, pos + e->count, at + (int64_t) k * e->extent);
+            pos += e->count + 1;
+        } else {
+            pos++;
+        }
+    }
+}
+
+/* opal_datatype_commit (:1739-1782), then the carrier runs of opt_desc */
+void ort_commit(ort_type *t)
+{
+    if (t->committed)
+        return;
+    t->committed = 1;
+    t->opt_flags = 0;
+    if (t->desc.used > 0) {
+        /* the fake END_LOOP of opal_datatype_commit_description (:467-492) */
+        int64_t k = 0, first = 0;
+        while (t->desc.e[k].type == OE_LOOP)
+            k++;
+        if (t->size != 0)
+            first = t->desc.e[k].disp;
+        ort_desc in = t->desc;
+        in.e = (ort_elem *) malloc((size_t) (in.used + 1) * sizeof(ort_elem));
+        memcpy(in.e, t->desc.e, (size_t) in.used * sizeof(ort_elem));
+        in.e[in.used] = oe_end((uint32_t) in.used, first, (uint64_t) t->size, 0);
+        in.e[in.used].flags = 0;
+        ox_restart(&t->opt_flags, &in, &t->opt);
+        free(in.e);
+        if (t->opt.used) {
+            ort_elem *s = &t->opt.e[t->opt.used];
+            *s = oe_end((uint32_t) t->opt.used, first, (uint64_t) t->size, 0);
+        }
+        ox_flatten(t, t->opt.e, 0, t->opt.used, 0);
+    }
+    t->opref = (int64_t *) malloc((size_t) (t->noruns + 1) * sizeof(int64_t));
+    int64_t acc = 0;
+    for (int64_t r = 0; r < t->noruns; r++) {
+        t->opref[r] = acc;
+        acc += t->oruns[r].len;
+    }
+    t->opref[t->noruns] = acc;
+}
+
+/* opt_desc entry i (i == used: the END_LOOP sentinel): flags, type, count|items, loops,
+ * blocklen|size, extent, disp|first_elem_disp */
+int64_t ort_opt_used(ort_type *t)
+{
+    ort_commit(t);
+    return t->opt.used;
+}
+
+uint32_t ort_opt_flags(ort_type *t)
+{
+    ort_commit(t);
+    return t->opt_flags;
+}
+
+static void ox_entry_out(const ort_elem *e, int64_t *out)
+{
+    out[0] = e->flags;
+    out[1] = e->type;
+    out[2] = e->count;
+    out[3] = e->loops;
+    out[4] = (int64_t) e->blocklen;
+    out[5] = e->extent;
+    out[6] = e->disp;
+}
+
+void ort_opt_at(ort_type *t, int64_t i, int64_t *out)
+{
+    ort_commit(t);
+    ox_entry_out(&t->opt.e[i], out);
+}
+
+int64_t ort_desc_used(const ort_type *t) { return t->desc.used; }
+
+void ort_desc_at(const ort_type *t, int64_t i, int64_t *out) { ox_entry_out(&t->desc.e[i], out); }
+
 static void ort_prefix(ort_type *t)
 {
     if (t->pref)
@@ -697,6 +1497,23 @@ static void ort_locate(const ort_type *t, int64_t p, int64_t *inst, int64_t *run
     *within = q - t->pref[lo];
 }
 
+/* ort_locate on the carrier runs of opt_desc (ort_commit must have run) */
+static void ort_locate_opt(const ort_type *t, int64_t p, int64_t *inst, int64_t *run, int64_t *within)
+{
+    *inst = p / t->size;
+    int64_t q = p - *inst * t->size;
+    int64_t lo = 0, hi = t->noruns - 1;
+    while (lo < hi) {
+        int64_t mid = (lo + hi + 1) / 2;
+        if (t->opref[mid] <= q)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    *run = lo;
+    *within = q - t->opref[lo];
+}
+
 /*
  * Pack the window [position, position+len) of the packed stream of `count`
  * instances at `base` into `out`.  Stops early rather than split a basic element
@@ -716,14 +1533,15 @@ int64_t ort_pack(ort_type *t, int64_t count, const void *base, int64_t position,
      * fills every iovec to the byte: no element snapping */
     if ((t->flags & ORT_FLAG_NO_GAPS) || ((t->flags & ORT_FLAG_CONTIGUOUS) && count == 1))
         return ort_pack_bytes(t, count, base, position, out, len);
-    ort_prefix(t);
+    /* the elements a fragment never splits are those of opt_desc (ort_commit) */
+    ort_commit(t);
     const int64_t ext = ort_extent(t);
     int64_t inst, run, within, done = 0;
-    ort_locate(t, position, &inst, &run, &within);
+    ort_locate_opt(t, position, &inst, &run, &within);
     const char *b = (const char *) base;
     char *o = (char *) out;
     while (done < len && position + done < total) {
-        const ort_run *r = &t->runs[run];
+        const ort_run *r = &t->oruns[run];
         int64_t avail = r->len - within;
         int64_t space = len - done;
         int64_t n = avail;
@@ -743,7 +1561,7 @@ int64_t ort_pack(ort_type *t, int64_t count, const void *base, int64_t position,
         within += n;
         if (within == r->len) {
             within = 0;
-            if (++run == t->nruns) {
+            if (++run == t->noruns) {
                 run = 0;
                 inst++;
             }
@@ -780,10 +1598,10 @@ int64_t ort_set_position(ort_type *t, int64_t count, int64_t position, int send)
         return position;
     if (!send)
         return position;
-    ort_prefix(t);
+    ort_commit(t);
     int64_t inst, run, within;
-    ort_locate(t, position, &inst, &run, &within);
-    return position - within % t->runs[run].esize;
+    ort_locate_opt(t, position, &inst, &run, &within);
+    return position - within % t->oruns[run].esize;
 }
 
 /* Byte-exact transfer of the packed window [position, position+len): dir 0 packs

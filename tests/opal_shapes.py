@@ -140,19 +140,31 @@ def end_loop(items, size, first_elem_disp, flags=0):
 
 
 class OpalType:
-    """A committed opal_datatype_t whose desc and opt_desc are `entries` (+ sentinel)."""
+    """A committed opal_datatype_t whose desc is `entries` and whose opt_desc is
+    `opt_entries` (default: the same array), each followed by its END_LOOP sentinel
+    (opal_datatype_optimize.c:454-465: items = used, the first element's displacement, size)."""
 
-    def __init__(self, entries, size, lb, ub, true_lb, true_ub, flags=0, name=b"ddt"):
-        self.raw = np.frombuffer(b"".join(list(entries) + [end_loop(0, size, 0)]), dtype=np.uint8).copy()
-        used = len(entries)
+    def __init__(self, entries, size, lb, ub, true_lb, true_ub, flags=0, name=b"ddt", opt_entries=None,
+                 first_disp=0):
+        entries = list(entries)
+        self.raw = np.frombuffer(b"".join(entries + [end_loop(len(entries), size, first_disp)]),
+                                 dtype=np.uint8).copy()
         self.dt = OpalDatatype()
         d = self.dt
         d.super.obj_reference_count = 1
         d.flags = flags | F_COMMITTED | F_DATA
         d.size, d.lb, d.ub, d.true_lb, d.true_ub = size, lb, ub, true_lb, true_ub
         d.name = name[:63]
-        for dd in (d.desc, d.opt_desc):
-            dd.length, dd.used, dd.desc = used + 1, used, self.raw.ctypes.data
+        d.desc.length, d.desc.used, d.desc.desc = len(entries) + 1, len(entries), self.raw.ctypes.data
+        if opt_entries is None:
+            self.opt_raw = self.raw
+            d.opt_desc.length, d.opt_desc.used, d.opt_desc.desc = d.desc.length, d.desc.used, d.desc.desc
+        else:
+            opt_entries = list(opt_entries)
+            self.opt_raw = np.frombuffer(b"".join(opt_entries + [end_loop(len(opt_entries), size, first_disp)]),
+                                         dtype=np.uint8).copy()
+            d.opt_desc.length, d.opt_desc.used = len(opt_entries) + 1, len(opt_entries)
+            d.opt_desc.desc = self.opt_raw.ctypes.data
 
     @property
     def ptr(self):
@@ -169,7 +181,8 @@ class OpalType:
 def flat_from_oracle(otype, flags=0):
     """One DATA entry per run of the oracle's type map (a valid, unoptimised description:
     opal_datatype_add emits DATA entries with CREATE_ELEM's count=1 collapse,
-    opal_datatype_internal.h:195-209)."""
+    opal_datatype_internal.h:195-209).  Installed as opt_desc it is a description whose
+    elements are the type map's own, not the committed carriers: tests of the import only."""
     info = otype.info()
     ents = []
     for disp, ln, esize, tid in otype.typed_runs():
@@ -181,6 +194,49 @@ def flat_from_oracle(otype, flags=0):
     if info["flags"] & F_NO_GAPS:
         fl |= F_NO_GAPS
     return OpalType(ents, info["size"], info["lb"], info["ub"], info["true_lb"], info["true_ub"], fl)
+
+
+def pack_entry(e):
+    """A 7-tuple (flags, type, count|items, loops, blocklen|size, extent, disp|first_elem_disp)
+    as the 32-byte dt_elem_desc_t."""
+    fl, ty, a, lo, b, x, d = e
+    if fl & F_DATA:
+        return struct.pack("<HHIQqq", fl, ty, a, b, x, d)
+    if ty == 0:
+        return struct.pack("<HHIIIQq", fl, 0, a, lo, 0, b & ((1 << 64) - 1), x)
+    return struct.pack("<HHIIIQq", fl, 1, a, lo & 0xFFFFFFFF, 0, b, d)
+
+
+def unpack_entries(raw: bytes):
+    """32-byte dt_elem_desc_t entries -> 7-tuples (the inverse of pack_entry)."""
+    out = []
+    for i in range(len(raw) // 32):
+        p = raw[32 * i:32 * i + 32]
+        fl, ty = struct.unpack_from("<HH", p)
+        if fl & F_DATA:
+            c, b, x, d = struct.unpack_from("<IQqq", p, 4)
+            out.append((fl, ty, c, 0, b, x, d))
+        elif ty == 0:
+            it, lo, _, un, x = struct.unpack_from("<IIIQq", p, 4)
+            out.append((fl, ty, it, lo, un if un < (1 << 63) else -1, x, 0))
+        else:
+            it, un, _, sz, fd = struct.unpack_from("<IIIQq", p, 4)
+            out.append((fl, ty, it, un, sz, 0, fd))
+    return out
+
+
+def from_oracle(otype, flags=0):
+    """The opal_datatype_t Open MPI commits for the oracle's type: desc as opal_datatype_add
+    builds it, opt_desc as opal_datatype_commit optimizes it (both restated in
+    oracle/ddt_oracle.c), OPTIMIZED_RESTRICTED when a region was re-typed.  This is what the
+    bridge meets inside Open MPI: use_desc = &opt_desc (opal_convertor.c:533)."""
+    info = otype.info()
+    fl = flags | (info["flags"] & (F_CONTIGUOUS | F_NO_GAPS)) | (0x10000 if otype.restricted() else 0)
+    desc = [pack_entry(e) for e in otype.desc()]
+    opt = otype.opt_desc(sentinel=True)
+    first = opt[-1][6] if opt else 0
+    return OpalType(desc, info["size"], info["lb"], info["ub"], info["true_lb"], info["true_ub"], fl,
+                    opt_entries=[pack_entry(e) for e in opt[:-1]], first_disp=first)
 
 
 # ------------------------------------------------------------------ the convertor

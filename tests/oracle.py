@@ -53,6 +53,10 @@ def lib():
             "ort_raw": (i64, [vp, i64, i64, i64, i64, vp, vp, vp]),
             "ort_external": (i64, [vp, i64, vp, vp, i]),
             "ort_external_size": (i64, [vp]),
+            "ort_commit": (None, [vp]),
+            "ort_opt_used": (i64, [vp]), "ort_opt_at": (None, [vp, i64, vp]),
+            "ort_opt_flags": (ctypes.c_uint32, [vp]),
+            "ort_desc_used": (i64, [vp]), "ort_desc_at": (None, [vp, i64, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -100,6 +104,32 @@ class OType:
     def typed_runs(self):
         """[(disp, len, esize, opal id)] of the flattened type map, in type-map order."""
         return [r + (int(lib().ort_run_tid(self.h, i)),) for i, r in enumerate(self.runs())]
+
+    # --- descriptions (Open MPI's dt_elem_desc_t entries, as 7-tuples
+    #     (flags, type, count|items, loops, blocklen|size, extent, disp|first_elem_disp)) ---
+    def desc(self):
+        """opal_datatype_t::desc as opal_datatype_add builds it (no sentinel)."""
+        out = (ctypes.c_int64 * 7)()
+        res = []
+        for i in range(int(lib().ort_desc_used(self.h))):
+            lib().ort_desc_at(self.h, i, out)
+            res.append(tuple(out))
+        return res
+
+    def opt_desc(self, sentinel: bool = False):
+        """opal_datatype_t::opt_desc after opal_datatype_commit (the optimizer restated in
+        oracle/ddt_oracle.c); with `sentinel` the END_LOOP at [used] is included."""
+        out = (ctypes.c_int64 * 7)()
+        n = int(lib().ort_opt_used(self.h))
+        res = []
+        for i in range(n + (1 if sentinel and n else 0)):
+            lib().ort_opt_at(self.h, i, out)
+            res.append(tuple(out))
+        return res
+
+    def restricted(self) -> bool:
+        """OPAL_DATATYPE_OPTIMIZED_RESTRICTED after commit (a mixed-type region was re-typed)."""
+        return bool(lib().ort_opt_flags(self.h) & 0x10000)
 
     @property
     def size(self):

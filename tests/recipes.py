@@ -178,3 +178,49 @@ def random_recipe(rng: random.Random, depth: int = 0, basics=None) -> Any:
     if k == "resized":
         return ("resized", sub, rng.randint(-8, 8), rng.choice([-16, 0, 4, 8, 24, 64, 96]))
     return ("dup", sub)
+
+
+def random_mixed_recipe(rng: random.Random, depth: int = 0) -> Any:
+    """Recipes whose type maps put elements of different types side by side -- the regions
+    opal_datatype_commit fuses and re-types to UINT8/4/2/1 carriers
+    (opal_datatype_optimize.c:581-630, :1195-1199, :1250-1252) -- nested in the loops its
+    boundary fusion, compression, short-loop expansion and unrolling act on (:641-888, :1054-1122).
+    Structs are mostly packed (member i+1 starts where member i ends, or 1-3 bytes later), so
+    the merges and the carriers' alignment rules are exercised at every byte phase."""
+    if depth >= 3 or (depth > 0 and rng.random() < 0.2):
+        return ("basic", rng.choice(EXT_BASICS[:16])[0])
+    k = rng.choice(["struct", "struct", "struct", "vector", "hvector", "contig", "resized",
+                    "hindexed", "indexed_block"])
+    if k == "struct":
+        n = rng.randint(2, 5)
+        subs = [random_mixed_recipe(rng, depth + 1) for _ in range(n)]
+        built = [build_oracle(s) for s in subs]
+        blens = [rng.randint(1, 3) for _ in range(n)]
+        disps, at = [], rng.choice([0, 0, 1, 2, 4])
+        for b, t in zip(blens, built):
+            disps.append(at)
+            ext = t.extent if t.size else 1
+            at += b * ext + (rng.choice([0, 0, 0, 1, 2, 3, 4, 8]) if rng.random() < 0.4 else 0)
+        return ("struct", blens, disps, subs)
+    sub = random_mixed_recipe(rng, depth + 1)
+    t = build_oracle(sub)
+    ext = t.extent if t.size else 1
+    if k == "vector":
+        return ("vector", rng.randint(2, 9), rng.randint(1, 3), rng.choice([1, 2, 3, 4]), sub)
+    if k == "hvector":
+        return ("hvector", rng.randint(2, 9), rng.randint(1, 2),
+                rng.choice([ext, ext, ext + 4, ext + 8, 2 * ext, ext * 3 + 1]), sub)
+    if k == "contig":
+        return ("contig", rng.randint(2, 6), sub)
+    if k == "resized":
+        return ("resized", sub, 0, rng.choice([t.size, t.size, ext + 4, max(t.size, 1) * 2]))
+    if k == "hindexed":
+        n = rng.randint(2, 10)
+        ds, at = [], 0
+        bl = [rng.randint(1, 2) for _ in range(n)]
+        for b in bl:
+            ds.append(at)
+            at += b * ext + rng.choice([0, ext, 4, 8])
+        return ("hindexed", bl, ds, sub)
+    n = rng.randint(2, 10)
+    return ("indexed_block", rng.randint(1, 2), sorted(rng.sample(range(0, 3 * n), n)), sub)

@@ -67,3 +67,77 @@ def test_timed_region_and_gather_check_world2_gloo():
         assert wall >= 0.1
         assert chk["ok"] and chk["gathered_bytes"] == 7000 and chk["backend"] == "gloo"
     assert res[0][2] == res[1][2]
+
+
+@pytest.mark.parametrize("cfg", ["cfg1", "cfg2", "cfg3"])
+def test_floor_parts_move_exactly_the_workloads_bytes(cfg):
+    """bench.py's floor (bare kernels, ompi_amd/csrc/ddt_floor.hip) is priced on the workload's
+    own accesses: the user-side runs of its parts are exactly the type map's runs of `count`
+    instances (as sets of (offset, bytes)), and together they produce S packed bytes."""
+    import numpy as np
+    from ompi_amd import recipe as ER
+    from tests import plan_emu as E
+    rec, count, _ = bench.make_workload(cfg)
+    t = ER.build_committed(rec)
+    info = t.info()
+    ext = info["ub"] - info["lb"]
+    blk = E.engine_blocks(t)                    # (src, dst, len) of one instance
+    want = np.concatenate([blk[:, 0] + i * ext for i in range(count)])
+    wlen = np.tile(blk[:, 2], count)
+    got, glen = [], []
+    for _, kind, es, ls, ss, base, lw in bench.floor_parts(cfg):
+        i0 = np.arange(1 << ls[0], dtype=np.int64)
+        i1 = np.arange(1 << ls[1], dtype=np.int64)
+        i2 = np.arange(1 << ls[2], dtype=np.int64)
+        off = (base + i2[:, None, None] * ss[2] + i1[None, :, None] * ss[1] + i0[None, None, :] * ss[0]).reshape(-1)
+        got.append(off)
+        glen.append(np.full(off.size, es if kind == 0 else 16 << lw, dtype=np.int64))
+    got, glen = np.concatenate(got), np.concatenate(glen)
+    assert int(glen.sum()) == info["size"] * count
+
+    es = 8 if cfg != "cfg3" else 4   # the workload's element size: compare element multisets
+
+    def elements(o, n):   # faces share edge elements, so compare with multiplicity
+        reps = n // es
+        starts = np.repeat(o, reps)
+        k = np.arange(reps.sum(), dtype=np.int64) - np.repeat(np.cumsum(reps) - reps, reps)
+        return np.sort(starts + k * es)
+    np.testing.assert_array_equal(elements(want, wlen), elements(got, glen))
+
+
+def test_strong_cfg3_over_eight_ranks_covers_all_64_fields():
+    """The driver's 8-GPU strong run of BASELINE config 3 (`--gpus 8 --strong --config cfg3`): the
+    self-launch command is one rank per GPU with the same arguments, and the eight ranks' splits
+    (ompi_amd.shard.split_recipe by top-level count) take 8 fields each, in order, their packed
+    ranges tiling the whole 64-field stream."""
+    from ompi_amd import shard
+    argv = bench.self_launch_argv(8, ["--gpus", "8", "--strong", "--config", "cfg3"], 29600)
+    assert "--nproc-per-node=8" in argv
+    i = argv.index(os.path.abspath(bench.__file__))
+    assert argv[i + 1:] == ["--gpus", "8", "--strong", "--config", "cfg3"]
+    recipe, count, _ = bench.make_workload("cfg3")
+    field_size = shard._engine_info(recipe)[0]
+    total, first_pk = 0, 0
+    for rank in range(8):
+        rrec, rcount, uoff, poff = shard.split_recipe(recipe, 64, rank, 8)
+        assert rrec == recipe and rcount == 8
+        assert poff == first_pk and uoff == rank * 8 * shard._engine_info(recipe)[1]
+        first_pk += rcount * field_size
+        total += rcount
+    assert total == 64 and first_pk == 64 * field_size
+
+
+def test_gather_packed_equal_shards_skip_padding():
+    """shard.gather_packed with equal shards gathers in place (gloo, world 1 here: the same code
+    path as the equal-size branch) and returns the concatenation."""
+    import torch
+    import torch.distributed as dist
+    from ompi_amd import shard
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29611")
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        x = torch.arange(100, dtype=torch.uint8)
+        assert torch.equal(shard.gather_packed(x), x)
+    finally:
+        dist.destroy_process_group()

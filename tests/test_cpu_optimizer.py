@@ -1,0 +1,236 @@
+"""The commit optimizer on CPU: opal_datatype_commit
+(opal/datatype/opal_datatype_optimize.c:1739-1782) restated twice -- by the oracle
+(oracle/ddt_oracle.c, test infrastructure) and by the engine (ompi_amd/csrc/ddt_optimize.cpp,
+the product's commit) -- and pinned to what the reference itself produced:
+
+* SURVEY.md Appendix A, the `opal_datatype_dump` output of the real reference for the BASELINE
+  shapes (cfg1, the cfg2 faces, cfg3's dim-2 face, cfg5's struct{double,int[3]} and its hvector,
+  cfg4's two-block FLOAT4 pairs);
+* `position.c` on MPI_LONG_DOUBLE_INT (365 x 112-byte segments + 80, recorded from the
+  reference): the 20 fused bytes of {long double, int} are one UINT4 x 5 carrier;
+* datatype_corpus.c's merged struct{double,long,char} (17 contiguous bytes of three types:
+  one UINT1 carrier, opal_datatype_optimize.c:581-611).
+
+Then the two restatements are held to each other entry for entry (desc, opt_desc and the
+OPTIMIZED_RESTRICTED flag) on thousands of fuzzed recipes, half of them mixed-type structs in
+loops, and every opt_desc must describe exactly the bytes of its desc in the same order.
+"""
+from __future__ import annotations
+
+import random
+
+import pytest
+
+from tests import corpus as C
+from tests import opal_shapes as S
+from tests import oracle as O
+from tests import recipes as R
+from tests.positioning import create_segments
+
+INT4, UINT1, UINT4, FLOAT4, FLOAT8, FLOAT12, LONG, CHAR = 6, 9, 11, 15, 16, 17, 25, 4
+F_DATA = 0x100
+BASIC = 0x136   # OPAL_DATATYPE_FLAG_BASIC
+CHANGED = 0x200  # OPAL_DATATYPE_OPTIMIZED_TYPE_CHANGED
+
+
+def _data(e):
+    """DATA entry 7-tuple -> (type, count, blocklen, extent, disp)."""
+    assert e[0] & F_DATA
+    return (e[1], e[2], e[4], e[5], e[6])
+
+
+def _engine(rec):
+    b = R.Built(rec)
+    raw, fl = b.engine().to_opal_opt_desc()
+    return b, S.unpack_entries(raw), fl
+
+
+def _both(rec):
+    """(oracle opt_desc, engine opt_desc, oracle restricted, engine restricted)."""
+    b, eng, fl = _engine(rec)
+    return b.o.opt_desc(), eng, b.o.restricted(), bool(fl & 0x10000)
+
+
+# ------------------------------------------------------------------ Appendix A
+def test_appendix_a_cfg1_and_halo_faces():
+    """cfg1 vector(1024,1,2) double: FLOAT8 count 1024 blen 1 extent 16; the 256^3 x face
+    vector(65536,1,256): FLOAT8 count 65536 extent 2048; the y face vector(256,256,65536):
+    FLOAT8 count 256 blen 256 extent 524288 -- unchanged by the optimizer, no re-typing."""
+    d = ("basic", FLOAT8)
+    for rec, want in [
+        (("vector", 1024, 1, 2, d), (FLOAT8, 1024, 1, 16, 0)),
+        (("vector", 65536, 1, 256, d), (FLOAT8, 65536, 1, 2048, 0)),
+        (("vector", 256, 256, 65536, d), (FLOAT8, 256, 256, 524288, 0)),
+    ]:
+        o, e, ro, re_ = _both(rec)
+        assert [_data(x) for x in o] == [want] and o == e, rec
+        assert not ro and not re_
+
+
+def test_appendix_a_cfg3_thin_face():
+    """512^3 float subarray, sub {512,512,1} at start 511 (C order): FLOAT4 count 262144
+    disp 2044 blen 1 extent 2048."""
+    rec = ("subarray", [512, 512, 512], [512, 512, 1], [0, 0, 511], 0, ("basic", FLOAT4))
+    b, e, _ = _engine(rec)
+    assert [_data(x) for x in e] == [(FLOAT4, 262144, 1, 2048, 2044)]
+    assert b.o.opt_desc() == e
+
+
+def test_appendix_a_cfg5_struct_and_hvector():
+    """struct{double, int[3]}: opt_desc UINT4 count 1 blen 5 extent 20, RESTRICTED; hvector(N, 1,
+    32 B) of it: UINT4 count N blen 5 extent 32 (the contiguous loop compressed and re-typed,
+    :641-709).  N = 128 Mi through the engine (its description stays one LOOP entry), 64 Ki
+    through the oracle (which also flattens the type map)."""
+    st = ("struct", [1, 3], [0, 8], [("basic", FLOAT8), ("basic", INT4)])
+    o, e, ro, re_ = _both(st)
+    assert [_data(x) for x in e] == [(UINT4, 1, 5, 20, 0)] and o == e and ro and re_
+    assert e[0][0] & CHANGED
+    rec = ("hvector", 1 << 16, 1, 32, st)
+    b, e, fl = _engine(rec)
+    assert [_data(x) for x in e] == [(UINT4, 1 << 16, 5, 32, 0)] and fl & 0x10000
+    assert b.o.opt_desc() == e and b.o.restricted()
+    t = R.build_engine(("hvector", 128 << 20, 1, 32, st)).commit()   # engine only: no flat map
+    raw, fl = t.to_opal_opt_desc()
+    assert [_data(x) for x in S.unpack_entries(raw)] == [(UINT4, 128 << 20, 5, 32, 0)] and fl & 0x10000
+
+
+def test_appendix_a_cfg4_two_block_pairs():
+    """indexed(n, blocklens 1, LCG displacements) of float: the optimizer pairs consecutive
+    one-element blocks into `FLOAT4 count 2 blen 1 extent (d2 - d1)` (:1179-1185), so opt_desc
+    holds n/2 entries for n unique, non-adjacent displacements (App. A: 64 Mi -> 33,554,432)."""
+    n = 4096
+    x, disps = 0x5EED, []
+    for _ in range(n):
+        disps.append(x)
+        x = (1664525 * x + 1013904223) % (1 << 28)
+    rec = ("indexed", [1] * n, disps, ("basic", FLOAT4))
+    b, e, _ = _engine(rec)
+    o = b.o.opt_desc()
+    assert o == e
+    adjacent = sum(1 for a, c in zip(disps, disps[1:]) if c == a + 1)
+    assert len(b.o.desc()) == n - adjacent
+    pairs = [x for x in o if x[2] == 2]
+    assert len(pairs) >= (n - adjacent) // 2 - 2
+    for fl, ty, cnt, _, bl, ext, disp in pairs:
+        assert ty == FLOAT4 and bl == 1 and ext != 4
+
+
+# ------------------------------------------------------------------ reference answers
+def test_position_c_segments_from_the_constructors():
+    """position.c (:42-85, :211-272) on MPI_LONG_DOUBLE_INT x 2048 -- struct{long double @0,
+    int @16} resized to 32 -- built with the constructors, not hand-written: both restatements
+    fuse the 20 bytes into UINT4 x 5, so 113-byte fragments snap to 112 bytes: 365 segments of
+    112 and one of 80, as the reference ran.  The engine's own send positions agree."""
+    rec = ("resized", ("struct", [1, 1], [0, 16], [("basic", FLOAT12), ("basic", INT4)]), 0, 32)
+    b, e, fl = _engine(rec)
+    assert [_data(x) for x in e] == [(UINT4, 1, 5, 20, 0)] and fl & 0x10000
+    segs = create_segments(2048 * 20, 113, lambda p: b.o.set_position(2048, p, send=True))
+    assert [n for _, n in segs] == [112] * 365 + [80]
+    eng = b.engine()
+    assert segs == create_segments(2048 * 20, 113,
+                                   lambda p: 2048 * 20 if p >= 2048 * 20 else eng.snap_position(p))
+
+
+def test_merged_contig_with_gaps_is_one_byte_carrier():
+    """datatype_corpus.c:59-97 struct{double @0, long @8, char @16}: 17 contiguous bytes of three
+    types, no UINT8/4/2 tiles 17 -> UINT1 blen 17; a pack fragment may stop on any byte."""
+    rec, _ = C.merged_contig_with_gaps()
+    o, e, ro, re_ = _both(rec)
+    assert [_data(x) for x in e] == [(UINT1, 1, 17, 17, 0)] and o == e and ro and re_
+    b = R.Built(rec)
+    assert [b.o.set_position(7, p) for p in (1, 12, 30, 119)] == [1, 12, 30, 119]
+
+
+def test_mixed_same_size_blocks_take_the_aligned_carrier():
+    """Equal-size blocks of different types merge into one count-2 entry (:1170-1199): int @0 and
+    float @8 -> UINT4 count 2 extent 8; double @4 + long @12 abut, and at that 4-byte phase only
+    UINT4 tiles them (UINT8 needs 8-byte alignment, :600-606): UINT4 count 2 blen 2 extent 8,
+    which CREATE_ELEM collapses to one 16-byte block of UINT4 x 4; char[2] @0 + short @4 ->
+    UINT2 count 2 (the chars' byte boundaries are gone)."""
+    cases = [
+        (("struct", [1, 1], [0, 8], [("basic", INT4), ("basic", FLOAT4)]), (UINT4, 2, 1, 8, 0)),
+        (("struct", [1, 1], [4, 12], [("basic", FLOAT8), ("basic", LONG)]), (UINT4, 1, 4, 16, 4)),
+        (("struct", [2, 1], [0, 4], [("basic", CHAR), ("basic", 5)]), (10, 2, 1, 4, 0)),
+    ]
+    for rec, want in cases:
+        o, e, ro, re_ = _both(rec)
+        assert [_data(x) for x in e] == [want] and o == e and ro and re_, (rec, e)
+
+
+# ------------------------------------------------------------------ the two restatements agree
+def _flatten(ents, at=0):
+    """The byte runs a description moves, in order (adjacent runs joined)."""
+    out = []
+
+    def walk(lo, hi, base):
+        pos = lo
+        while pos < hi:
+            fl, ty, cnt, loops, bl, ext, disp = ents[pos]
+            if fl & F_DATA:
+                n = bl * S.BASIC_SIZE[ty]
+                for k in range(cnt):
+                    a = base + disp + k * ext
+                    if out and out[-1][0] + out[-1][1] == a:
+                        out[-1][1] += n
+                    else:
+                        out.append([a, n])
+                pos += 1
+            elif ty == 0:
+                for k in range(loops):
+                    walk(pos + 1, pos + cnt, base + k * ext)
+                pos += cnt + 1
+            else:
+                pos += 1
+    walk(0, len(ents), at)
+    return out
+
+
+@pytest.mark.parametrize("kind,seed", [("any", 0), ("any", 1), ("mixed", 0), ("mixed", 1), ("mixed", 2)])
+def test_engine_and_oracle_optimizers_agree(kind, seed):
+    """desc, opt_desc and OPTIMIZED_RESTRICTED: engine == oracle on fuzzed recipes, and each
+    opt_desc moves its desc's bytes in type-map order."""
+    rng = random.Random(4400 + 17 * seed + (kind == "mixed"))
+    gen = R.random_recipe if kind == "any" else R.random_mixed_recipe
+    n = restricted = 0
+    for _ in range(500):
+        rec = gen(rng)
+        b = R.Built(rec)
+        if b.o.info()["size"] == 0:
+            continue
+        e = b.engine()
+        od, oo = b.o.desc(), b.o.opt_desc()
+        ed = S.unpack_entries(e.to_opal_desc())
+        raw, fl = e.to_opal_opt_desc()
+        eo = S.unpack_entries(raw)
+        assert ed == od, rec
+        assert eo == oo, rec
+        assert bool(fl & 0x10000) == b.o.restricted(), rec
+        if len(oo) < 4000:
+            assert _flatten(oo) == _flatten(od), rec
+        n += 1
+        restricted += b.o.restricted()
+    assert n > 300
+    if kind == "mixed":
+        assert restricted > 150
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_engine_snap_follows_carriers_on_mixed_types(seed):
+    """Send positions on mixed-type recipes: the engine's snap (its committed opt_desc) ==
+    the oracle's walk of its own opt_desc, at random positions, counts 1-3."""
+    rng = random.Random(4500 + seed)
+    checked = 0
+    for _ in range(150):
+        b = R.Built(R.random_mixed_recipe(rng))
+        info = b.o.info()
+        if info["size"] == 0:
+            continue
+        e = b.engine()
+        for count in (1, 2, 3):
+            total = count * info["size"]
+            if (info["flags"] & 0x20) or ((info["flags"] & 0x10) and count == 1):
+                continue
+            for p in {rng.randrange(total) for _ in range(10)}:
+                assert e.snap_position(p) == b.o.set_position(count, p, send=True), (b.recipe, count, p)
+                checked += 1
+    assert checked > 500

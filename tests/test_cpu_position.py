@@ -123,7 +123,7 @@ def test_bridge_send_position_on_corpus_types():
         for count in (1, 7):
             if _no_op(info, count):
                 continue
-            ot = S.flat_from_oracle(oo)
+            ot = S.from_oracle(oo)
             total = count * info["size"]
             c = _bridge_send_positioner(ot, count)
             pos = 0

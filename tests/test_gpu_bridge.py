@@ -98,7 +98,7 @@ def test_bridge_corpus_fragments_vs_golden(device, name):
     span, origin = R.layout(info, count)
     host = R.fill(span, 0x5A)
     user = _dev(host, device)
-    ot = S.flat_from_oracle(b.o)
+    ot = S.from_oracle(b.o)
     packed = torch.zeros(max(size, 1), dtype=torch.uint8, device=device)
     ref = np.frombuffer(b.o.pack(count, host, origin, 0, size, element_granular=False), dtype=np.uint8)
     rng = random.Random(name)
@@ -310,15 +310,17 @@ def test_bridge_ddt_raw2_description(device):
 # ------------------------------------------------------------------ fuzz through the bridge
 @pytest.mark.parametrize("seed", range(int(os.environ.get("DDT_BRIDGE_FUZZ_SEEDS", "3"))))
 def test_bridge_fuzz_descriptions(device, seed):
-    """Random recipes handed to the bridge as Open MPI descriptions in two forms -- the flat
-    one (one DATA entry per run of the oracle's type map) and the LOOP-structured one the
-    engine exports (ddt_type_to_opal_desc) -- packed in random fragments (element-granular
-    max_data == oracle) and unpacked in shuffled windows, counts 1-3; bytes == oracle."""
+    """Random recipes (half of them mixed-type structs in loops) handed to the bridge as the
+    opal_datatype_t Open MPI commits, in two forms -- desc and opt_desc from the oracle's
+    restatement of opal_datatype_add + opal_datatype_commit, and the engine's own export of
+    the same (ddt_type_to_opal_desc / ddt_type_to_opal_opt_desc) -- packed in random fragments
+    (element-granular max_data == the oracle's walk of opt_desc) and unpacked in shuffled
+    windows, counts 1-3; bytes == oracle."""
     import torch
     rng = random.Random(1000 + seed)
     done = 0
     while done < 20:
-        rec = R.random_recipe(rng)
+        rec = R.random_recipe(rng) if done % 2 else R.random_mixed_recipe(rng)
         b = R.Built(rec)
         info = b.o.info()
         count = rng.choice([1, 2, 3])
@@ -336,12 +338,13 @@ def test_bridge_fuzz_descriptions(device, seed):
         user = _dev(host, device)
         ref = np.frombuffer(b.o.pack(count, host, origin, 0, size, element_granular=False), dtype=np.uint8)
         overlap = _overlaps(b.o.runs(), count, info["ub"] - info["lb"])
-        flat = S.flat_from_oracle(b.o)
+        committed = S.from_oracle(b.o)
         ents = b.engine().to_opal_desc()
-        looped = S.OpalType([ents[32 * i:32 * i + 32] for i in range(len(ents) // 32)], info["size"],
-                            info["lb"], info["ub"], info["true_lb"], info["true_ub"],
-                            flags=flat.dt.flags & (S.F_CONTIGUOUS | S.F_NO_GAPS))
-        for form, ot in (("flat", flat), ("looped", looped)):
+        opt, oflags = b.engine().to_opal_opt_desc()
+        split = lambda raw: [raw[32 * i:32 * i + 32] for i in range(len(raw) // 32)]  # noqa: E731
+        engine = S.OpalType(split(ents), info["size"], info["lb"], info["ub"], info["true_lb"],
+                            info["true_ub"], flags=committed.dt.flags, opt_entries=split(opt))
+        for form, ot in (("committed", committed), ("engine", engine)):
             packed = torch.zeros(size, dtype=torch.uint8, device=device)
             conv = S.Convertor()
             assert conv.prepare(ot, count, user.data_ptr() + origin, send=True) == S.OPAL_SUCCESS
@@ -547,7 +550,7 @@ def test_reference_unpack_ooo_traces(device, trace, path, iov):
     src = torch.from_numpy(pbar.copy())
     src = src.pin_memory() if iov == "host" else src.to(device)
     if path == "bridge":
-        ot = S.flat_from_oracle(b.o)
+        ot = S.from_oracle(b.o)
         conv = S.Convertor()
         assert conv.prepare(ot, N_OOO, bar.data_ptr(), send=False) == S.OPAL_SUCCESS
     else:

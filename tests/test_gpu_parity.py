@@ -879,6 +879,30 @@ def test_sorted_list_engine(device, sorted_from, esz, count, density):
     assert st["sorted"] == 1 and st["chunks"] == (n + ch - 1) // ch, st
 
 
+@pytest.mark.parametrize("esz,count,density", [(4, 1, 4), (4, 2, 3), (8, 1, 5), (16, 1, 4), (4, 1, 64)])
+def test_sorted_list_engine_half_chunks(device, sorted_from, esz, count, density):
+    """The address-ordered engine with half-size chunks (ddt_tune schunk 2: 64 KiB chunk images
+    in 512-thread workgroups, two per CU; buckets stay 128 KiB): twice as many chunks as
+    buckets, ragged last chunk and bucket, bit-exact both ways."""
+    import ompi_amd
+    L = ompi_amd.lib()
+    sorted_from(1)
+    L.ddt_tune(b"schunk", 2)
+    try:
+        rng = np.random.default_rng(esz * 1000 + count * 10 + density)
+        ch = (128 << 10) // esz
+        n = 3 * ch + 1237
+        unit = {4: ("basic", 15), 8: ("basic", 16), 16: ("basic", 16)}[esz]
+        per = esz // (8 if esz == 16 else esz)
+        disps = (rng.permutation(density * n)[:n] * per).astype(np.int64)
+        b = R.Built(("indexed_block", per, disps.tolist(), unit))
+        _roundtrip(b, count, device, 9 + esz)
+        st = b.engine().engine_info()
+        assert st["sorted"] == 1 and st["chunks"] == (n + ch // 2 - 1) // (ch // 2), st
+    finally:
+        L.ddt_tune(b"schunk", 1)
+
+
 @pytest.mark.parametrize("name", ["contig16", "adv_mixed_promote", "one_contig_instance"])
 def test_no_op_types_fill_fragments_to_the_byte(device, name):
     """A convertor the reference marks NO_OP (OPAL_CONVERTOR_PREPARE, opal_convertor.c:
@@ -962,12 +986,23 @@ def test_sorted_list_engine_falls_back(device, sorted_from):
     var = R.Built(("indexed", lens.tolist(), starts.tolist(), ("basic", 15)))
     _roundtrip(var, 2, device, 4)
     assert var.engine().engine_info()["sorted"] == 1
-    # fragments of a qualifying type use the per-block kernel; the whole message the engine
-    u = R.Built(("indexed_block", 1, rng.permutation(3 * n)[:n].tolist(), ("basic", 15)))
-    _roundtrip(u, 1, device, 6, frags=[4096, 12, 40])
-    assert u.engine().engine_info()["sorted"] == 0
-    _roundtrip(u, 1, device, 6)
+    # fragments of a qualifying type use the per-block kernel; the whole message the engine.
+    # The tables are built at commit (round 4, ddt_type_prepare_device); with that off
+    # (sorted_commit 0) fragments leave them unbuilt and the first whole message builds them.
+    perm = rng.permutation(3 * n)[:n].tolist()
+    u = R.Built(("indexed_block", 1, perm, ("basic", 15)))
     assert u.engine().engine_info()["sorted"] == 1
+    _roundtrip(u, 1, device, 6, frags=[4096, 12, 40])
+    L = ompi_amd.lib()
+    L.ddt_tune(b"sorted_commit", 0)
+    try:
+        w = R.Built(("indexed_block", 1, perm, ("basic", 15)))
+        _roundtrip(w, 1, device, 6, frags=[4096, 12, 40])
+        assert w.engine().engine_info()["sorted"] == 0
+        _roundtrip(w, 1, device, 6)
+        assert w.engine().engine_info()["sorted"] == 1
+    finally:
+        L.ddt_tune(b"sorted_commit", 1)
     # a user base that is not element-aligned: per-block kernel for that call
     info = u.o.info()
     size = info["size"]
@@ -1133,16 +1168,25 @@ def test_reference_ddt_test_c(device, name, recipe, count, chunks):
         _local_copy_with_convertor(b, count, ch, device)
 
 
-def test_sorted_list_engine_in_hip_graph(device, sorted_from):
-    """A qualifying list captured into a HIP graph before its first eager use keeps the
-    per-block kernel (the engine's build cannot run inside a capture); after an eager use the
-    engine itself is captured.  Both graphs replay bit-exact."""
+@pytest.mark.parametrize("at_commit", [True, False])
+def test_sorted_list_engine_in_hip_graph(device, sorted_from, at_commit):
+    """The address-ordered tables are built at commit (round 4): a graph captured before the
+    first eager use already captures the engine.  With the build deferred to first use
+    (sorted_commit 0), a capture before any eager use keeps the per-block kernel (the build
+    cannot run inside a capture), and after an eager use the engine itself is captured.  Every
+    graph replays bit-exact."""
     import torch
     import ompi_amd
     sorted_from(1)
+    L = ompi_amd.lib()
+    L.ddt_tune(b"sorted_commit", 1 if at_commit else 0)
     rng = np.random.default_rng(5)
     n = 70_000
-    b = R.Built(("indexed_block", 1, rng.permutation(4 * n)[:n].tolist(), ("basic", 15)))
+    try:
+        b = R.Built(("indexed_block", 1, rng.permutation(4 * n)[:n].tolist(), ("basic", 15)))
+        b.engine()
+    finally:
+        L.ddt_tune(b"sorted_commit", 1)
     info = b.o.info()
     size = info["size"]
     span, origin = R.layout(info, 1)
@@ -1150,7 +1194,7 @@ def test_sorted_list_engine_in_hip_graph(device, sorted_from):
     user = _dev(host, device)
     ref = np.frombuffer(b.o.pack(1, host, origin, 0, size, element_granular=False), dtype=np.uint8)
     e = b.engine()
-    for expect_state in (0, 1):
+    for expect_state in ((1, 1) if at_commit else (0, 1)):
         packed = torch.zeros(size, dtype=torch.uint8, device=device)
         s = torch.cuda.Stream(device)
         g = torch.cuda.CUDAGraph()

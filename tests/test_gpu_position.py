@@ -146,8 +146,9 @@ def test_position_c_through_engine(device, form):
     """position.c through the engine convertor.  `reference_carriers`: the type the reference's
     optimizer produces (5 UINT4, extent 32) -> the same 366 segments as the reference.
     `typed_struct`: struct{MPI_LONG_DOUBLE @0, MPI_INT @16} resized to 32 built with the engine's
-    constructors, whose commit keeps the typed elements (DESIGN.md §1 deviation 3): segments
-    follow the 16/4-byte element grid, as the oracle's walk of the same type map does."""
+    constructors: its commit (ddt_optimize.cpp, opal_datatype_optimize.c:581-630) re-types the
+    20 fused bytes to UINT4 x 5 exactly as the reference commits MPI_LONG_DOUBLE_INT, so the
+    segments are the reference's 365 x 112 B + 80 B too."""
     from ompi_amd import datatype as D
     if form == "reference_carriers":
         et = D.create_resized(D.create_contiguous(5, D.predefined(UINT4)), 0, 32).commit()
@@ -157,7 +158,7 @@ def test_position_c_through_engine(device, form):
         st = D.create_struct([1, 1], [0, 16], [D.predefined(FLOAT12), D.predefined(INT4)])
         et = D.create_resized(st, 0, 32).commit()
         oo = O.resized(O.struct([1, 1], [0, 16], [O.basic(FLOAT12), O.basic(INT4)]), 0, 32)
-        sizes = None
+        sizes = [112] * 365 + [80]
     send, recv, want = _ldi_buffers()
     got = _position_test(_EngineSide(et, 2048), oo, 2048, send, recv, device, expect_sizes=sizes)
     np.testing.assert_array_equal(got, want)
@@ -215,7 +216,7 @@ def test_send_set_position_mid_element_corpus(device, name):
             continue   # NO_OP: no fPosition, byte positions (opal_convertor.h:389-392)
         span, origin = R.layout(info, count)
         host = R.fill(span, 0x33)
-        ot = S.flat_from_oracle(b.o)
+        ot = S.from_oracle(b.o)
         _mid_element_packs(_BridgeSide(ot, count), b.o, count, host, origin, device, rng)
         _mid_element_packs(_EngineSide(b.engine(), count), b.o, count, host, origin, device, rng)
         ot.destruct()
@@ -232,7 +233,8 @@ def test_send_set_position_cfg5_promoted_record(device):
     host = R.fill(span, 5)
     rng = random.Random(55)
     _mid_element_packs(_BridgeSide(ot, 1), oo, 1, host, 0, device, rng, n_pos=64)
-    # the engine's own struct type snaps on its typed elements (double @0, ints @8..19)
+    # the engine's own struct type commits to the same UINT4 x 5 carrier (ddt_optimize.cpp):
+    # its send positions snap to multiples of 4 inside each record, like the bridge's
     from ompi_amd import datatype as D
     st = D.create_struct([1, 3], [0, 8], [D.predefined(FLOAT8), D.predefined(INT4)])
     et = D.create_hvector(n, 1, 32, st).commit()
