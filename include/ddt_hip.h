@@ -88,7 +88,9 @@ typedef struct ddt_convertor ddt_convertor_t;
 
 /* ================= datatype construction (ompi/datatype/ompi_datatype.h:217-284) ================= */
 
-/* Predefined type handle (opal_datatype_basicDatatypes[id], opal_datatype.h:216-248). Never freed. */
+/* Predefined type handle (opal_datatype_basicDatatypes[id], opal_datatype.h:216-248). Never freed.
+ * ids 4..27 are the basic types; 2 / 3 are the MPI_LB / MPI_UB bound markers (size 0; a constructor
+ * that adds one only moves the lower / upper bound to its displacement, opal_datatype_add.c:158-186). */
 const ddt_datatype_t *ddt_predefined(int id);
 
 /* ompi_datatype_create_contiguous (ompi_datatype_create_contiguous.c:31-44) */

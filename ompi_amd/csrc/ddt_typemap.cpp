@@ -29,6 +29,16 @@ std::once_flag g_predef_once;
 
 void init_predefined()
 {
+    // OPAL_DATATYPE_LB / _UB (opal_datatype_constructors.h:77-85, 169-172): size 0, no
+    // description, bounds markers only (MPI_LB / MPI_UB, ompi_datatype_module.c:92-93)
+    for (int id = 2; id <= 3; ++id) {
+        ddt_datatype &t = g_predef[id];
+        t.id = uint16_t(id);
+        t.lb = t.ub = t.true_lb = t.true_ub = 0;
+        t.align = 0;
+        t.nbElems = 1;
+        t.flags = F_PREDEFINED;
+    }
     for (int id = 4; id <= 27; ++id) {
         ddt_datatype &t = g_predef[id];
         t.id = uint16_t(id);
@@ -90,6 +100,21 @@ AddState add_bounds(ddt_datatype *base, const ddt_datatype *add, uint64_t count,
     if (count == 0)
         return st;
     extent = effective_extent(add, extent);
+    if (add->id == 2 || add->id == 3) {
+        // the LB / UB markers (:158-186): move the bound to disp, nothing is appended; the id
+        // survives a dup (opal_datatype_clone.c:74), so a duplicated marker is one too
+        if (add->id == 2) {
+            base->lb = (base->flags & F_USER_LB) ? std::min(base->lb, disp) : disp;
+            base->flags |= F_USER_LB;
+        } else {
+            base->ub = (base->flags & F_USER_UB) ? std::max(base->ub, disp) : disp;
+            base->flags |= F_USER_UB;
+        }
+        // (wrapping: the other bound may still be the constructor's INT64_MIN / MAX)
+        if (int64_t(uint64_t(base->ub) - uint64_t(base->lb)) != base->size)
+            base->flags &= ~F_NO_GAPS;
+        return st;
+    }
     int64_t lb, ub;
     {   // OPAL_DATATYPE_LB_UB_CONT (:98-116)
         int64_t upper = disp + extent * int64_t(count - 1), lower = disp;
@@ -246,7 +271,7 @@ ddt_datatype *clone_type(const ddt_datatype *o)
 {
     // opal_datatype_clone (opal_datatype_clone.c:35-80): copy everything, drop PREDEFINED
     ddt_datatype *t = new_type();
-    t->id = 0;
+    t->id = o->id;   // kept, as the reference does (:74): a dup of MPI_LB / MPI_UB stays a marker
     t->flags = o->flags & ~(F_PREDEFINED | F_COMMITTED);
     t->size = o->size;
     t->lb = o->lb;
@@ -592,7 +617,7 @@ extern "C" {
 const ddt_datatype_t *ddt_predefined(int id)
 {
     std::call_once(g_predef_once, init_predefined);
-    if (id < 4 || id > 27)
+    if (id < 2 || id > 27)
         return nullptr;
     return &g_predef[id];
 }

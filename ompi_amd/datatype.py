@@ -14,6 +14,7 @@ import numpy as np
 from ._lib import check, lib
 
 # OPAL predefined ids (opal/datatype/opal_datatype_internal.h:71-99)
+LB, UB = 2, 3
 INT1, INT2, INT4, INT8, INT16 = 4, 5, 6, 7, 8
 UINT1, UINT2, UINT4, UINT8, UINT16 = 9, 10, 11, 12, 13
 FLOAT2, FLOAT4, FLOAT8, FLOAT12, FLOAT16 = 14, 15, 16, 17, 18
@@ -277,6 +278,8 @@ class _Predefs:
         "MPI_C_FLOAT_COMPLEX": FLOAT_COMPLEX, "MPI_C_DOUBLE_COMPLEX": DOUBLE_COMPLEX,
         "MPI_C_LONG_DOUBLE_COMPLEX": LONG_DOUBLE_COMPLEX,
         "MPI_C_BOOL": BOOL, "MPI_WCHAR": WCHAR,
+        # MPI-1 bound markers (ompi_datatype_module.c:92-93; opal_datatype_add.c:158-186)
+        "MPI_LB": LB, "MPI_UB": UB,
     }
 
     def __getattr__(self, name):

@@ -180,6 +180,16 @@ static void od_push(ort_desc *d, ort_elem x)
 
 ort_type *ort_basic(int id)
 {
+    if (id == 2 || id == 3) {
+        /* the LB / UB markers (opal_datatype_constructors.h:77-85): size 0, no description */
+        ort_type *m = ort_new();
+        m->id = id;
+        m->lb = m->ub = m->true_lb = m->true_ub = 0;
+        m->align = 0;
+        m->nbElems = 1;
+        m->flags = ORT_FLAG_PREDEFINED;
+        return m;
+    }
     if (id < 4 || id > 27 || ort_basic_size[id] == 0)
         return NULL;
     ort_type *t = ort_new();
@@ -217,7 +227,7 @@ ort_type *ort_dup(const ort_type *o)
     /* opal_datatype_clone: copy everything, drop PREDEFINED (opal_datatype_clone.c:42-46) */
     ort_type *t = ort_new();
     *t = *o;
-    t->id = 0;
+    /* the id is kept (opal_datatype_clone.c:74): a dup of a marker is still a marker */
     t->flags &= ~ORT_FLAG_PREDEFINED;
     t->runs = (ort_run *) malloc((size_t) (o->nruns ? o->nruns : 1) * sizeof(ort_run));
     memcpy(t->runs, o->runs, (size_t) o->nruns * sizeof(ort_run));
@@ -334,6 +344,20 @@ static void ort_add(ort_type *base, const ort_type *add, int64_t count, int64_t 
         return;
     if (extent == -1)
         extent = add->ub - add->lb;
+    if (add->id == 2) {   /* OPAL_DATATYPE_LB (:161-172) */
+        base->lb = (base->flags & ORT_FLAG_USER_LB) ? lmin(base->lb, disp) : disp;
+        base->flags |= ORT_FLAG_USER_LB;
+        if ((int64_t) ((uint64_t) base->ub - (uint64_t) base->lb) != base->size)
+            base->flags &= ~ORT_FLAG_NO_GAPS;
+        return;
+    }
+    if (add->id == 3) {   /* OPAL_DATATYPE_UB (:173-184) */
+        base->ub = (base->flags & ORT_FLAG_USER_UB) ? lmax(base->ub, disp) : disp;
+        base->flags |= ORT_FLAG_USER_UB;
+        if ((int64_t) ((uint64_t) base->ub - (uint64_t) base->lb) != base->size)
+            base->flags &= ~ORT_FLAG_NO_GAPS;
+        return;
+    }
     /* OPAL_DATATYPE_LB_UB_CONT (:98-116) */
     {
         int64_t upper = disp + extent * (count - 1), lower = disp;

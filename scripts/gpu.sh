@@ -18,7 +18,8 @@ step=$1
 shift
 case "$step" in
 tests)
-    timeout -k 10 1000 python -u -m pytest -q -m gpu -x --timeout 300 --timeout-method thread ${@:-tests} \
+    [ $# -eq 0 ] && set -- tests
+    timeout -k 10 1000 python -u -m pytest -q -m gpu -x --timeout 300 --timeout-method thread "$@" \
         > gpurun_out/${TAG}_pytest_gpu.log 2>&1
     rc=$?
     tail -25 gpurun_out/${TAG}_pytest_gpu.log

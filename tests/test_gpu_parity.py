@@ -107,6 +107,16 @@ def test_fuzz_full_message(device, seed):
         _roundtrip(b, rng.choice([1, 2, 3, 7]), device, seed * 100 + n)
 
 
+def test_lb_ub_markers(device):
+    """MPI_LB / MPI_UB markers (opal_datatype_add.c:158-186) move only the bounds: the packed
+    stream of every count is the oracle's, and so is the unpacked user buffer."""
+    from .test_cpu_markers import marker_recipe
+    rng = random.Random(77)
+    for n in range(80):
+        b = R.Built(marker_recipe(rng))
+        _roundtrip(b, rng.choice([1, 2, 5]), device, 7000 + n)
+
+
 @pytest.mark.parametrize("seed", range(int(__import__("os").environ.get("DDT_FUZZ_BIG_SEEDS", "2"))))
 def test_fuzz_large_counts(device, seed):
     """Random types repeated to 0.5-4 MiB of packed data (thousands of instances), so the
