@@ -308,6 +308,22 @@ def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z"), flush="
             scribble.fill_(i)
         elif flush == "read":
             scribble.sum()
+    # the launch floor under the same protocol: the events around one 1-element kernel (at 16
+    # fields a y / z face moves 8 MiB in well under a microsecond of HBM time, so this is most of
+    # its event time; profiles/r4_small_launch_trace.txt separates the kernel durations)
+    tiny = torch.zeros(1, device=dev)
+    tev = []
+    for i in range(warmup + steps):
+        a, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if flush:
+            touch(2 * i)
+        a.record(stream)
+        tiny.add_(1)
+        b_.record(stream)
+        if i >= warmup:
+            tev.append((a, b_))
+    torch.cuda.synchronize()
+    out["launch_floor_us"] = round(float(np.median([a.elapsed_time(b_) for a, b_ in tev])) * 1e3, 2)
     for k in faces:
         ft = ER.build_committed(recs[k])
         fS = ft.info()["size"] * fields
