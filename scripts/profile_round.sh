@@ -13,7 +13,7 @@ run write_$CFG rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw
 run req_$CFG rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d gpurun_out/pmcr_$CFG -o pmc -- python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --no-graph --no-latency --no-faces
 python3 scripts/traffic.py $(find gpurun_out/pmcf_$CFG -name '*counter_collection.csv') $(find gpurun_out/pmcw_$CFG -name '*counter_collection.csv') $CFG > gpurun_out/traffic_$CFG.json
 python3 scripts/requests.py $(find gpurun_out/pmcr_$CFG -name '*counter_collection.csv') $CFG > gpurun_out/requests_$CFG.json
-python3 scripts/kstats.py $(find gpurun_out/prof_$CFG -name '*kernel_stats.csv') | head -8
+python3 scripts/kstats.py $(find gpurun_out/prof_$CFG -name "*kernel_stats.csv") > gpurun_out/kstats_$CFG.txt; head -8 gpurun_out/kstats_$CFG.txt
 if [ -n "$CALIB" ]; then
 run calib_fetch rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf_calib -o pmc -- python3 scripts/kbench.py --iters 3 --types z,x,cfg1
 run calib_write rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw_calib -o pmc -- python3 scripts/kbench.py --iters 3 --types z,x,cfg1
