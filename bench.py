@@ -475,6 +475,34 @@ def floor_run(name, user_ptr, packed_ptr, reps=10):
             "unpack_us": round(sum(v["unpack_us"] for v in res.values()), 2)}
 
 
+def copy_ceiling(dev, nbytes=1 << 30, reps=10):
+    """"also report against a measured contiguous D2D copy ceiling".  One
+    contiguous GiB copied each way by the floor library's block-copy kernel (16 KiB per
+    workgroup, non-temporal loads), 4x the Infinity Cache so HBM serves it; GB/s counts the
+    read and the write (2 x nbytes per copy), as the roofline's algorithmic bytes do."""
+    import ctypes
+    import torch
+    L, Part = floor_lib()
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    a.fill_(1)
+    b.fill_(2)
+    blocks = nbytes >> 14
+    l0 = blocks.bit_length() - 1
+    assert 1 << l0 == blocks
+    part = (Part * 1)(Part(1, 0, l0, 0, 0, 10, 16384, 0, 0, 0, 0))
+    out = (ctypes.c_float * 2)()
+    rc = L.ddt_floor_run(ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()), part, 1, reps, out)
+    del a, b
+    torch.cuda.empty_cache()
+    if rc != 0:
+        return {"error": f"hip error {rc}"}
+    gbs = [2 * nbytes / (out[i] * 1e-6) / 1e9 for i in range(2)]
+    return {"bytes": nbytes, "copy_us": [round(out[0], 2), round(out[1], 2)],
+            "GB_per_s": round(sum(gbs) / 2, 1),
+            "source": "ompi_amd/csrc/ddt_floor.hip copy_blocks, 1 GiB each way, median of 10"}
+
+
 # ------------------------------------------------------------------ multi-rank harness
 def self_launch_argv(gpus, argv, port):
     """The launcher command for `--gpus N` run by hand: one rank per GPU on this node, the
@@ -735,6 +763,12 @@ def main():
                                 "median of 10 rounds; floor = sum of the parts")
         floor = fl
         torch.cuda.synchronize()
+    copy = None
+    if rank == 0 and world == 1 and not args.no_floor:
+        try:
+            copy = copy_ceiling(dev)
+        except (OSError, AssertionError) as ex:
+            copy = {"error": f"{type(ex).__name__}: {ex}"[:200]}
 
     # The RCCL leg of SURVEY.md §8e, outside the timed region: a consumer that needs the
     # whole packed stream on one device all-gathers the shards (backend "nccl" = RCCL over
@@ -776,6 +810,9 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": None},
             "floor_us": floor,
         }
+        if copy and "GB_per_s" in copy:
+            copy["engine_frac_of_copy"] = round(achieved / 1e9 / copy["GB_per_s"], 4)
+        result["copy_ceiling"] = copy
         # the committed PMC passes were measured on the config's default (weak) message; a
         # --strong message of another size does not inherit them
         tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")

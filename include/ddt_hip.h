@@ -357,7 +357,7 @@ int ddt_debug_host_window(const void *p, size_t n, uint64_t *device_addr);
  * HBM staging); "hd_grid" / "hd_grid_pack" = workgroup cap of such an unpack / pack launch (256 / 0 default,
  * 0 none); "stage_mb" =
  * staging buffer MiB for pageable host iovecs (256 default; read when a convertor first stages); "sseg" =
- * address-ordered engine segment bytes (64 or 128); "sunroll" = its pack-1 elements per
+ * address-ordered engine segment bytes (32, 64 default, 128); "sunroll" = its pack-1 elements per
  * thread in flight (4, 8, 16 default); "s2unroll" = the same for its unpack pass 2' (4, 8
  * default, 16);
  * "reset" = restore the defaults.

@@ -1679,7 +1679,7 @@ int ddt_tune(const char *key, long value)
     else if (k == "sunroll")
         tuning().sunroll = value >= 16 ? 16 : (value >= 8 ? 8 : 4);
     else if (k == "sseg")
-        tuning().sseg = value == 128 ? 128 : 64;
+        tuning().sseg = (value == 128 || value == 32) ? value : 64;
     else if (k == "schunk")
         tuning().schunk = value == 2 ? 2 : 1;
     else if (k == "sorted_commit")

@@ -53,6 +53,8 @@ constexpr uint32_t LDS_BYTES = 128u << 10;
 // U runs are padded to whole segments of SEGB bytes (a plan's choice, SortedList::segb): 64 B
 // (round 1; 32 B segments: less padding, but cfg4 1461 -> 1512 us) or 128 B (round 2: half the
 // memory requests of the scattered run writes and reads, more padding; ddt_tune("sseg")).
+// 32 B is kept for half chunks (round 4): their runs are half as long, so 32-byte segments
+// pad them as little as 64-byte segments pad full-chunk runs.
 constexpr uint32_t SEG_DEFAULT = 64;
 constexpr uint16_t PAD = 0xFFFF;       // upos of a padding slot
 
@@ -548,7 +550,7 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
 {
     n = n_;
     esz = esz_;
-    segb = segb_ == 128 ? 128 : SEG_DEFAULT;
+    segb = (segb_ == 128 || segb_ == 32) ? segb_ : SEG_DEFAULT;
     rg = LDS_BYTES / esz;
     nb = (n + rg - 1) / rg;
     cdiv = (cdiv_ == 2 && nb <= MAXNB / 2) ? 2 : 1;   // half chunks: the tables must fit half the LDS
@@ -702,6 +704,14 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol
             DDT_SORTED_LAUNCH(8, 128)
         } else {
             DDT_SORTED_LAUNCH(16, 128)
+        }
+    } else if (segb == 32) {
+        if (esz == 4) {
+            DDT_SORTED_LAUNCH(4, 32)
+        } else if (esz == 8) {
+            DDT_SORTED_LAUNCH(8, 32)
+        } else {
+            DDT_SORTED_LAUNCH(16, 32)
         }
     } else {
         if (esz == 4) {

@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/../ompi_amd/csrc"
 mkdir -p build_asan
-for f in ddt_typemap ddt_plan ddt_convertor ddt_external ddt_pool; do
+for f in ddt_typemap ddt_optimize ddt_plan ddt_convertor ddt_external ddt_pool; do
   /opt/rocm/bin/hipcc -std=c++17 -O1 -g -fPIC -I../../include --offload-arch=gfx950 \
     -Xarch_host -fsanitize=address -fno-omit-frame-pointer -c $f.cpp -o build_asan/$f.o
 done

@@ -889,15 +889,17 @@ def test_sorted_list_engine(device, sorted_from, esz, count, density):
     assert st["sorted"] == 1 and st["chunks"] == (n + ch - 1) // ch, st
 
 
+@pytest.mark.parametrize("seg", [64, 32])
 @pytest.mark.parametrize("esz,count,density", [(4, 1, 4), (4, 2, 3), (8, 1, 5), (16, 1, 4), (4, 1, 64)])
-def test_sorted_list_engine_half_chunks(device, sorted_from, esz, count, density):
+def test_sorted_list_engine_half_chunks(device, sorted_from, esz, count, density, seg):
     """The address-ordered engine with half-size chunks (ddt_tune schunk 2: 64 KiB chunk images
     in 512-thread workgroups, two per CU; buckets stay 128 KiB): twice as many chunks as
-    buckets, ragged last chunk and bucket, bit-exact both ways."""
+    buckets, ragged last chunk and bucket, bit-exact both ways; with 64- and 32-byte U segments."""
     import ompi_amd
     L = ompi_amd.lib()
     sorted_from(1)
     L.ddt_tune(b"schunk", 2)
+    L.ddt_tune(b"sseg", seg)
     try:
         rng = np.random.default_rng(esz * 1000 + count * 10 + density)
         ch = (128 << 10) // esz
@@ -911,6 +913,7 @@ def test_sorted_list_engine_half_chunks(device, sorted_from, esz, count, density
         assert st["sorted"] == 1 and st["chunks"] == (n + ch // 2 - 1) // (ch // 2), st
     finally:
         L.ddt_tune(b"schunk", 1)
+        L.ddt_tune(b"sseg", 64)
 
 
 @pytest.mark.parametrize("name", ["contig16", "adv_mixed_promote", "one_contig_instance"])
