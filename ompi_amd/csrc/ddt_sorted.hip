@@ -405,13 +405,14 @@ __device__ __forceinline__ void load_runs(typename Elem<E>::T *lds, const uint16
     using T = typename Elem<E>::T;
     constexpr uint32_t SEG = SEGB / E, NSUB = NT / SEG;
     const T *src = reinterpret_cast<const T *>(U);
-    // B runs per round: their first two segments are loaded before any is stored (ILP: a
-    // run averages one segment, so about half of them have a second); the rare third and
-    // later segments follow
+    // B runs per round: their first NPF segments are loaded before any is stored (ILP: a run
+    // averages 64 bytes, one 64-byte segment, so about half of them have a second; with 32-byte
+    // segments the same bytes take up to four); the rare later segments follow
     constexpr int B = 8;
+    constexpr int NPF = (SEGB == 32 && E <= 8) ? 4 : 2;
     const uint32_t sub = threadIdx.x / SEG, lane = threadIdx.x % SEG;
     for (uint32_t kb = sub; kb < nb; kb += NSUB * B) {
-        T v[B], w[B];
+        T v[B][NPF];
         uint32_t o[B], cn[B], bb[B];
 #pragma unroll
         for (int i = 0; i < B; ++i) {
@@ -421,22 +422,22 @@ __device__ __forceinline__ void load_runs(typename Elem<E>::T *lds, const uint16
                 o[i] = toff[k];
                 cn[i] = toff[k + 1] - o[i];
                 bb[i] = tub[k];
-                if (lane < cn[i])
-                    v[i] = ldp(&src[bb[i] + lane], ntl);
-                if (lane + SEG < cn[i])
-                    w[i] = ldp(&src[bb[i] + lane + SEG], ntl);
+#pragma unroll
+                for (int f = 0; f < NPF; ++f)
+                    if (lane + f * SEG < cn[i])
+                        v[i][f] = ldp(&src[bb[i] + lane + f * SEG], ntl);
             }
         }
 #pragma unroll
         for (int i = 0; i < B; ++i) {
-            if (lane < cn[i])
-                lds[o[i] + lane] = v[i];
-            if (lane + SEG < cn[i])
-                lds[o[i] + lane + SEG] = w[i];
+#pragma unroll
+            for (int f = 0; f < NPF; ++f)
+                if (lane + f * SEG < cn[i])
+                    lds[o[i] + lane + f * SEG] = v[i][f];
         }
 #pragma unroll
         for (int i = 0; i < B; ++i)
-            for (uint32_t q = lane + 2 * SEG; q < cn[i]; q += SEG)
+            for (uint32_t q = lane + NPF * SEG; q < cn[i]; q += SEG)
                 lds[o[i] + q] = src[bb[i] + q];
     }
 }
