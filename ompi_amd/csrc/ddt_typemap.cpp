@@ -150,7 +150,11 @@ AddState add_bounds(ddt_datatype *base, const ddt_datatype *add, uint64_t count,
     base->ub = ub;
     base->align = std::max(base->align, add->align);
     if (!(base->flags & F_USER_UB)) {
-        int64_t eps = (base->ub - base->lb) % base->align;  // C remainder, as the reference
+        // C remainder, as the reference (a negative extent gives a negative remainder); a
+        // power-of-two alignment (every predefined type's) takes it without a division
+        const int64_t x = base->ub - base->lb, a = base->align;
+        const int64_t eps = (a & (a - 1)) ? x % a
+                                          : (x >= 0 ? (x & (a - 1)) : -int64_t(uint64_t(-x) & uint64_t(a - 1)));
         if (eps != 0)
             base->ub += base->align - eps;
     }
@@ -294,6 +298,16 @@ bool simple_block(const ddt_datatype *old)
 
 uint64_t gcd64(uint64_t a, uint64_t b) { return b ? gcd64(b, a % b) : a; }
 
+// gcd(g, x) for the running gcd of a list: once g is a power of two (it is from the first few
+// blocks on for any list of aligned displacements) it is min(g, lowest set bit of x), with no
+// division -- a 64 Mi-block list no longer spends seconds in 64-bit remainders
+inline uint64_t gcd_acc(uint64_t g, uint64_t x)
+{
+    if (g && !(g & (g - 1)))
+        return x ? std::min(g, x & (~x + 1)) : g;
+    return gcd64(g, x);
+}
+
 std::shared_ptr<IndexList> finish_list(std::shared_ptr<IndexList> L)
 {
     size_t n = L->disp.size();
@@ -305,10 +319,10 @@ std::shared_ptr<IndexList> finish_list(std::shared_ptr<IndexList> L)
         for (size_t i = 0; i < n; ++i) {
             L->poff[i] = acc;
             acc += L->len[i];
-            gl = gcd64(gl, L->len[i]);
+            gl = gcd_acc(gl, L->len[i]);
             L->min_disp = std::min(L->min_disp, L->disp[i]);
             L->max_end = std::max(L->max_end, L->disp[i] + int64_t(L->len[i]));
-            g = gcd64(g, uint64_t(L->disp[i] < 0 ? -L->disp[i] : L->disp[i]));
+            g = gcd_acc(g, uint64_t(L->disp[i] < 0 ? -L->disp[i] : L->disp[i]));
         }
         // all equal lengths -> uniform list
         if (n > 0 && gl == L->len[0]) {
@@ -327,7 +341,7 @@ std::shared_ptr<IndexList> finish_list(std::shared_ptr<IndexList> L)
         for (size_t i = 0; i < n; ++i) {
             L->min_disp = std::min(L->min_disp, L->disp[i]);
             L->max_end = std::max(L->max_end, L->disp[i] + int64_t(L->ulen));
-            g = gcd64(g, uint64_t(L->disp[i] < 0 ? -L->disp[i] : L->disp[i]));
+            g = gcd_acc(g, uint64_t(L->disp[i] < 0 ? -L->disp[i] : L->disp[i]));
         }
     }
     L->total = acc;
@@ -337,45 +351,92 @@ std::shared_ptr<IndexList> finish_list(std::shared_ptr<IndexList> L)
 }
 
 // Shared driver of the four indexed constructors (ompi_datatype_create_indexed.c:35-183):
-// merges blocks that abut in type-map order, then either emits per-block adds or, for
-// long runs of a simple element type, one LIST node with the identical bounds.
+// the caller merges blocks that abut in type-map order and feeds them here one at a time; the
+// first kListMin are held back, and the type becomes either per-block adds or, for a longer run
+// of a simple element type, one LIST node with the identical bounds.  Streaming, with the block
+// lengths kept only once two differ: a 64 Mi-block list is built in one pass over its
+// displacements, with no intermediate block array.
 struct Block {
     int64_t disp_bytes;
     uint64_t nelem;
 };
 
-ddt_datatype *build_indexed(const std::vector<Block> &blocks, const ddt_datatype *old)
-{
-    ddt_datatype *t = new_type();
-    int64_t extent = old->extent();
-    if (blocks.size() > kListMin && simple_block(old)) {
-        auto L = std::make_shared<IndexList>();
-        L->esize = old->desc[0].esize;
-        L->disp.reserve(blocks.size());
-        L->len.reserve(blocks.size());
-        for (const Block &b : blocks) {
-            AddState st = add_bounds(t, old, b.nelem, b.disp_bytes, extent);
-            if (!st.skip) {
-                L->disp.push_back(b.disp_bytes);
-                L->len.push_back(b.nelem * uint64_t(old->size));
-                add_finish(t, old, b.nelem, b.disp_bytes, extent, st);
+class IndexedBuilder {
+public:
+    IndexedBuilder(const ddt_datatype *old, size_t hint)
+        : old_(old), t_(new_type()), extent_(old->extent()), hint_(hint), simple_(simple_block(old))
+    {
+        held_.reserve(kListMin + 1);
+    }
+
+    void add(int64_t disp_bytes, uint64_t nelem)
+    {
+        if (!L_) {
+            held_.push_back({disp_bytes, nelem});
+            if (held_.size() > kListMin && simple_) {   // a list: replay the held blocks into it
+                L_ = std::make_shared<IndexList>();
+                L_->esize = old_->desc[0].esize;
+                L_->disp.reserve(hint_);
+                for (const Block &b : held_)
+                    to_list(b.disp_bytes, b.nelem);
+                held_.clear();
             }
+            return;
         }
+        to_list(disp_bytes, nelem);
+    }
+
+    ddt_datatype *finish()
+    {
+        if (!L_) {
+            for (const Block &b : held_)
+                type_add(t_, old_, b.nelem, b.disp_bytes, extent_);
+            return t_;
+        }
+        if (L_->len.empty())
+            L_->ulen = ulen_;   // every block the same length (finish_list: no poff)
+        else
+            L_->len.shrink_to_fit();
         Node n;
         n.kind = Node::LIST;
-        n.esize = L->esize;
-        n.tid = old->desc[0].tid;
+        n.esize = L_->esize;
+        n.tid = old_->desc[0].tid;
         // the flags of each block's DATA entry: the predefined type's own, or the copied
         // entry of a one-entry derived type (opal_datatype_add.c:328-329, :359)
-        n.flags = is_predefined(old) ? (old->flags & kElemFlags) : old->desc[0].flags;
-        n.list = finish_list(L);
-        t->desc.push_back(std::move(n));
-    } else {
-        for (const Block &b : blocks)
-            type_add(t, old, b.nelem, b.disp_bytes, extent);
+        n.flags = is_predefined(old_) ? (old_->flags & kElemFlags) : old_->desc[0].flags;
+        n.list = finish_list(L_);
+        t_->desc.push_back(std::move(n));
+        return t_;
     }
-    return t;
-}
+
+private:
+    void to_list(int64_t disp_bytes, uint64_t nelem)
+    {
+        AddState st = add_bounds(t_, old_, nelem, disp_bytes, extent_);
+        if (st.skip)
+            return;
+        const uint64_t bytes = nelem * uint64_t(old_->size);
+        if (L_->disp.empty())
+            ulen_ = bytes;
+        else if (L_->len.empty() && bytes != ulen_) {   // the first differing length
+            L_->len.reserve(hint_);
+            L_->len.assign(L_->disp.size(), ulen_);
+        }
+        L_->disp.push_back(disp_bytes);
+        if (!L_->len.empty())
+            L_->len.push_back(bytes);
+        add_finish(t_, old_, nelem, disp_bytes, extent_, st);
+    }
+
+    const ddt_datatype *old_;
+    ddt_datatype *t_;
+    int64_t extent_;
+    size_t hint_;
+    bool simple_;
+    std::vector<Block> held_;
+    std::shared_ptr<IndexList> L_;
+    uint64_t ulen_ = 0;
+};
 
 }  // namespace
 
@@ -709,8 +770,7 @@ static int indexed_common(size_t count, const size_t *blens, const ptrdiff_t *di
         return DDT_SUCCESS;
     }
     auto bl = [&](size_t k) { return uniform ? ublen : blens[k]; };
-    std::vector<Block> blocks;
-    blocks.reserve(count - i);
+    IndexedBuilder build(old, count - i);
     int64_t disp = disps[i];
     uint64_t dlen = bl(i);
     int64_t endat = bytes ? disp + int64_t(dlen) * extent : disp + int64_t(dlen);
@@ -721,14 +781,14 @@ static int indexed_common(size_t count, const size_t *blens, const ptrdiff_t *di
             dlen += bl(i);
             endat += bytes ? int64_t(bl(i)) * extent : int64_t(bl(i));
         } else {
-            blocks.push_back({bytes ? disp : disp * extent, dlen});
+            build.add(bytes ? disp : disp * extent, dlen);
             disp = disps[i];
             dlen = bl(i);
             endat = bytes ? disp + int64_t(dlen) * extent : disp + int64_t(dlen);
         }
     }
-    blocks.push_back({bytes ? disp : disp * extent, dlen});
-    *out = build_indexed(blocks, old);
+    build.add(bytes ? disp : disp * extent, dlen);
+    *out = build.finish();
     return DDT_SUCCESS;
 }
 
