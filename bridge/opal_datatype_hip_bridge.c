@@ -99,74 +99,111 @@ static void bridge_release(bridge_entry *e)
     pthread_mutex_unlock(&g_mu);
 }
 
-/* The cache entry of the convertor's description (imported on first use), held for the
- * caller until bridge_release: a destruct or an eviction on another thread in between only
- * unlinks it. */
-static bridge_entry *bridge_type_of(const opal_convertor_t *conv, int *err)
+/* The entry of (dt, ud) in its bucket, with g_mu held; a different description found at the
+ * same address is retired on the way (the old datatype died unseen). */
+static bridge_entry *lookup_locked(const opal_datatype_t *dt, const dt_type_desc_t *ud, uint64_t sig)
 {
-    const opal_datatype_t *dt = conv->pDesc;
-    const dt_type_desc_t *ud = conv->use_desc ? conv->use_desc : (dt ? &dt->opt_desc : NULL);
+    for (bridge_entry **pp = &g_buckets[bucket_of(dt)]; *pp;) {
+        if ((*pp)->key != dt) {
+            pp = &(*pp)->next;
+            continue;
+        }
+        if (same_fingerprint(*pp, dt, ud, sig))
+            return *pp;
+        bridge_entry *old = *pp;
+        *pp = old->next;
+        retire_locked(old);
+        ++g_stale;
+    }
+    return NULL;
+}
+
+/* The cache entry of (dt, ud), imported on first use.  `hold`: keep it for the caller until
+ * bridge_release (a destruct or an eviction on another thread in between only unlinks it).
+ * The import itself -- seconds for a description of tens of millions of entries -- runs
+ * outside the cache lock, so other threads' calls on other datatypes never wait for it; two
+ * threads importing the same datatype at once keep the first entry and drop the second. */
+static bridge_entry *bridge_entry_of(const opal_datatype_t *dt, const dt_type_desc_t *ud, int hold, int *err)
+{
     *err = OPAL_SUCCESS;
     if (!dt || !ud || !ud->desc || !(dt->flags & OPAL_DATATYPE_FLAG_COMMITTED)) {
         *err = OPAL_ERR_BAD_PARAM;
         return NULL;
     }
     const uint64_t sig = desc_sig(ud->desc, ud->used);
-    const size_t b = bucket_of(dt);
     pthread_mutex_lock(&g_mu);
-    bridge_entry **pp = &g_buckets[b];
-    for (; *pp; pp = &(*pp)->next) {
-        if ((*pp)->key != dt)
-            continue;
-        if (same_fingerprint(*pp, dt, ud, sig)) {
-            ++g_hits;
-            bridge_entry *e = *pp;
+    bridge_entry *e = lookup_locked(dt, ud, sig);
+    if (e) {
+        ++g_hits;
+        if (hold)
             ++e->inflight;
-            pthread_mutex_unlock(&g_mu);
-            return e;
-        }
-        /* a different description at this address: the old datatype died unseen */
-        bridge_entry *old = *pp;
-        *pp = old->next;
-        retire_locked(old);
-        ++g_stale;
-        break;
+        pthread_mutex_unlock(&g_mu);
+        return e;
     }
+    pthread_mutex_unlock(&g_mu);
+
     ddt_datatype_t *t = NULL;
     const int rc = ddt_type_from_opal_desc(ud->desc, ud->used, dt->size, dt->lb, dt->ub, dt->true_lb,
                                            dt->true_ub, &t);
     if (rc != DDT_SUCCESS) {
-        pthread_mutex_unlock(&g_mu);
         *err = rc == DDT_ERR_OUT_OF_RESOURCE ? OPAL_ERR_OUT_OF_RESOURCE : OPAL_ERR_BAD_PARAM;
         return NULL;
     }
-    bridge_entry *e = (bridge_entry *) calloc(1, sizeof(*e));
-    if (!e) {
-        pthread_mutex_unlock(&g_mu);
+    /* the import is this datatype's commit on the device side: a large index list gets its
+     * address-ordered tables here (at commit or prepare), never in the first fAdvance */
+    (void) ddt_type_prepare_device(t);
+    bridge_entry *n = (bridge_entry *) calloc(1, sizeof(*n));
+    if (!n) {
         ddt_type_destroy(&t);
         *err = OPAL_ERR_OUT_OF_RESOURCE;
         return NULL;
     }
-    e->key = dt;
-    e->desc = ud->desc;
-    e->used = ud->used;
-    e->size = dt->size;
-    e->lb = dt->lb;
-    e->ub = dt->ub;
-    e->true_lb = dt->true_lb;
-    e->true_ub = dt->true_ub;
-    e->sig = sig;
-    e->type = t;
-    e->inflight = 1;
-    e->next = g_buckets[b];
-    g_buckets[b] = e;
+    n->key = dt;
+    n->desc = ud->desc;
+    n->used = ud->used;
+    n->size = dt->size;
+    n->lb = dt->lb;
+    n->ub = dt->ub;
+    n->true_lb = dt->true_lb;
+    n->true_ub = dt->true_ub;
+    n->sig = sig;
+    n->type = t;
+
+    pthread_mutex_lock(&g_mu);
+    e = lookup_locked(dt, ud, sig);
+    if (e) {   /* another thread imported it meanwhile */
+        ++g_hits;
+        if (hold)
+            ++e->inflight;
+        pthread_mutex_unlock(&g_mu);
+        ddt_type_destroy(&n->type);
+        free(n);
+        return e;
+    }
+    const size_t b = bucket_of(dt);
+    n->inflight = hold ? 1 : 0;
+    n->next = g_buckets[b];
+    g_buckets[b] = n;
     ++g_entries;
     ++g_imports;
     pthread_mutex_unlock(&g_mu);
-    /* the import is this datatype's commit on the device side: a large index list gets its
-     * address-ordered tables here, at prepare, not in the first fAdvance of a message */
-    (void) ddt_type_prepare_device(t);
-    return e;
+    return n;
+}
+
+static bridge_entry *bridge_type_of(const opal_convertor_t *conv, int *err)
+{
+    const opal_datatype_t *dt = conv->pDesc;
+    return bridge_entry_of(dt, conv->use_desc ? conv->use_desc : (dt ? &dt->opt_desc : NULL), 1, err);
+}
+
+int opal_hip_bridge_datatype_commit(const opal_datatype_t *dt)
+{
+    if (!dt || !(dt->flags & OPAL_DATATYPE_FLAG_COMMITTED) || !dt->opt_desc.desc || dt->opt_desc.used == 0
+        || dt->opt_desc.used < OPAL_HIP_BRIDGE_COMMIT_IMPORT_MIN)
+        return OPAL_SUCCESS;   /* nothing to move, or cheap enough to import at first use */
+    int err;
+    (void) bridge_entry_of(dt, &dt->opt_desc, 0, &err);
+    return err;
 }
 
 void opal_hip_bridge_datatype_destruct(const opal_datatype_t *dt)

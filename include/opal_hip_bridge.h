@@ -49,6 +49,17 @@ int32_t opal_position_hip(opal_convertor_t *conv, size_t *position);
  * heterogeneous), or < 0 when the description cannot be imported. */
 int opal_hip_bridge_attach(opal_convertor_t *conv);
 
+/* Commit hook: call at the end of opal_datatype_commit (opal_datatype_optimize.c:1739-1782, after
+ * the fake END_LOOP is set) so a large description -- at least OPAL_HIP_BRIDGE_COMMIT_IMPORT_MIN
+ * opt_desc entries -- is imported (and a large index list gets its device tables) inside
+ * MPI_Type_commit, where Open MPI pays its own optimizer pass, instead of at the first prepare of
+ * a message; smaller descriptions import at first use in microseconds.  The convertor's use_desc
+ * of a homogeneous convertor is &dt->opt_desc (OPAL_CONVERTOR_PREPARE, opal_convertor.c:533), so
+ * attach then finds the entry.  Returns OPAL_SUCCESS or the import's error (the datatype stays
+ * usable: attach retries). */
+#define OPAL_HIP_BRIDGE_COMMIT_IMPORT_MIN 65536
+int opal_hip_bridge_datatype_commit(const opal_datatype_t *dt);
+
 /* Drop the cached import of `dt`; call from opal_datatype_destruct (opal_datatype_create.c:61-91)
  * so a datatype freed and reallocated at the same address is never served a stale plan. */
 void opal_hip_bridge_datatype_destruct(const opal_datatype_t *dt);

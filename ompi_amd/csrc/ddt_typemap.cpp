@@ -1311,7 +1311,9 @@ struct Fold {
                 L->len.push_back(r.blen);
         }
     }
-    void push(const RawData &r)
+    // `left`: entries of this level from r on, so the list can reserve for a run that
+    // continues to the level's end (no regrowth copies of a 256 MiB displacement array)
+    void push(const RawData &r, size_t left)
     {
         if (empty())
             type = r.type;
@@ -1324,6 +1326,7 @@ struct Fold {
             return;
         L = std::make_shared<IndexList>();
         L->esize = kSize[type];
+        L->disp.reserve(std::min<size_t>(head.size() * kFoldCount + left * size_t(r.count), size_t(1) << 27));
         uni = true;
         ulen = head[0].blen;
         for (const RawData &h : head)
@@ -1413,7 +1416,7 @@ bool parse_opal(const unsigned char *raw, size_t begin, size_t end, std::vector<
             if (!run.empty() && (!foldable || run.type != type))
                 run.flush(out);
             if (foldable)
-                run.push(d);
+                run.push(d, end - i);
             else
                 out.push_back(Fold::data_node(d));
             ++i;

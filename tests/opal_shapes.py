@@ -97,6 +97,7 @@ def bridge_lib():
             "opal_position_hip": (ctypes.c_int32, [vp, ctypes.POINTER(c_size_t)]),
             "opal_hip_bridge_attach": (ctypes.c_int, [vp]),
             "opal_hip_bridge_datatype_destruct": (None, [vp]),
+            "opal_hip_bridge_datatype_commit": (ctypes.c_int, [vp]),
             "opal_hip_bridge_finalize": (None, []),
             "opal_hip_bridge_stats": (None, [ctypes.POINTER(c_size_t)]),
             "opal_hip_bridge_layout": (None, [ctypes.POINTER(c_size_t)]),
@@ -176,6 +177,10 @@ class OpalType:
 
     def destruct(self):
         bridge_lib().opal_hip_bridge_datatype_destruct(self.ptr)
+
+    def commit_hook(self):
+        """What opal_datatype_commit calls last in the patched tree."""
+        return bridge_lib().opal_hip_bridge_datatype_commit(self.ptr)
 
 
 def flat_from_oracle(otype, flags=0):

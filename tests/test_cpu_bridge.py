@@ -82,6 +82,31 @@ def test_import_cache_hits_invalidation_and_stale_addresses():
     assert S.stats()["entries"] == 0
 
 
+def test_commit_hook_imports_large_descriptions_at_commit():
+    """opal_hip_bridge_datatype_commit (called at the end of opal_datatype_commit): a
+    description of >= 64 Ki opt_desc entries is imported there, so the first prepare of a
+    message only hits the cache; a small one is left to its first prepare."""
+    L = S.bridge_lib()
+    L.opal_hip_bridge_finalize()
+    base = S.stats()
+    n = 70000
+    big = S.OpalType([S.data(FLOAT8, 1, 1, 8, 24 * i) for i in range(n)], 8 * n, 0, 24 * n, 0,
+                     24 * (n - 1) + 8)
+    assert big.commit_hook() == S.OPAL_SUCCESS
+    st = S.stats()
+    assert st["imports"] - base["imports"] == 1 and st["entries"] == 1
+    assert S.Convertor().prepare(big, 2, 0x7000_0000_0000, send=True) == S.OPAL_SUCCESS
+    st2 = S.stats()
+    assert st2["imports"] == st["imports"] and st2["hits"] - st["hits"] == 1
+    assert big.commit_hook() == S.OPAL_SUCCESS and S.stats()["imports"] == st["imports"]   # idempotent
+    small = _xface()
+    assert small.commit_hook() == S.OPAL_SUCCESS
+    assert S.stats()["imports"] == st["imports"] and S.stats()["entries"] == 1
+    big.destruct()
+    small.destruct()
+    assert S.stats()["entries"] == 0
+
+
 def test_no_op_and_empty_convertors_skip_the_bridge():
     """OPAL_CONVERTOR_PREPARE returns before dispatch for NO_GAPS types (opal_convertor.c:
     562-567) and empty messages (:539-544): opal_convertor_pack copies those itself."""
