@@ -64,7 +64,10 @@ def test_engine_commit_builds_the_tables(device, disps):
     assert host_s < 1e-3, f"first asynchronous pack took {host_s * 1e3:.2f} ms of host time"
 
 
-def test_bridge_import_builds_the_tables(device, disps):
+@pytest.mark.parametrize("hook", [False, True], ids=["import_at_prepare", "commit_hook"])
+def test_bridge_import_builds_the_tables(device, disps, hook):
+    """With the commit hook (opal_hip_bridge_datatype_commit) the 1 Mi-entry description is
+    imported inside the commit, so the prepare of the first message only hits the cache."""
     import torch
     order = np.arange(N)
     pairs = order[0::2]
@@ -83,8 +86,17 @@ def test_bridge_import_builds_the_tables(device, disps):
     user = torch.randint(1, 255, (SPAN_FLOATS * 4,), dtype=torch.uint8, device=device)
     packed = torch.zeros(N * 4, dtype=torch.uint8, device=device)
     s = torch.cuda.Stream(device)
+    base = S.stats()
+    if hook:
+        assert ot.commit_hook() == S.OPAL_SUCCESS
+        assert S.stats()["imports"] - base["imports"] == 1
     conv = S.Convertor()
+    t0 = time.perf_counter()
     assert conv.prepare(ot, 1, user.data_ptr(), send=True, stream=s.cuda_stream) == S.OPAL_SUCCESS
+    prep_s = time.perf_counter() - t0
+    assert S.stats()["imports"] - base["imports"] == 1
+    if hook:
+        assert prep_s < 5e-3, f"prepare after the commit hook took {prep_s * 1e3:.2f} ms"
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     rc, _, md = conv.pack([(packed.data_ptr(), N * 4)])
