@@ -711,7 +711,7 @@ bool build_opal_desc(const std::vector<Node> &nodes, int64_t size, DescForm &out
     return true;
 }
 
-void encode_desc(const DescForm &d, std::vector<unsigned char> &out)
+void encode_desc(const DescForm &d, std::vector<unsigned char> &out, bool optimized)
 {
     out.clear();
     auto put = [&](uint16_t flags, uint16_t type, uint32_t a, uint32_t b, uint64_t c, int64_t x, int64_t y) {
@@ -730,15 +730,95 @@ void encode_desc(const DescForm &d, std::vector<unsigned char> &out)
         }
         out.insert(out.end(), p, p + 32);
     };
+    // a sealed list expands into many entries: the LOOP / END_LOOP pairs around it count the
+    // entries actually written (CREATE_LOOP_START / _END items, opal_datatype_internal.h:171-189)
+    std::vector<size_t> open;
     for (size_t i = 0; i < d.used; ++i) {
         const DescEntry &e = d.e[i];
+        if (!(e.flags & kData) && e.type == kDescLoop) {
+            open.push_back(out.size() / 32);
+        } else if (!(e.flags & kData) && e.type == kDescEndLoop && !open.empty()) {
+            const size_t at = open.back();
+            open.pop_back();
+            const uint32_t items = uint32_t(out.size() / 32 - at);
+            std::memcpy(out.data() + 32 * at + 4, &items, 4);
+            put(e.flags, e.type, items, e.loops, e.blen, e.extent, e.disp);
+            continue;
+        }
         if (e.sealed >= 0) {
             const IndexList &X = *d.lists[size_t(e.sealed)];
             const uint64_t es = uint64_t(esz(e.type));
+            if (!optimized) {
+                for (size_t k = 0; k < X.nblk(); ++k) {
+                    const uint64_t len = X.len.empty() ? X.ulen : X.len[k];
+                    put(e.flags, e.type, 1, 0, len / es, int64_t(len), e.disp + X.disp[k]);
+                }
+                continue;
+            }
+            // Pass::run's DATA path over the list's blocks (one element type, so no mixed
+            // regions), streamed: `last` is the pending element, emitted as elem() does
+            auto emit = [&](const DescEntry &x) {
+                uint64_t blen = x.blen;
+                int64_t ext = x.extent;
+                uint32_t cnt = x.count;
+                if (ext == int64_t(blen * es)) {   // CREATE_ELEM's contiguous collapse
+                    blen *= cnt;
+                    ext *= int64_t(cnt);
+                    cnt = 1;
+                }
+                put(uint16_t(x.flags | kData), x.type, cnt, 0, blen, ext, x.disp);
+            };
+            DescEntry last;
+            last.count = 0;
             for (size_t k = 0; k < X.nblk(); ++k) {
                 const uint64_t len = X.len.empty() ? X.ulen : X.len[k];
-                put(e.flags, e.type, 1, 0, len / es, int64_t(len), e.disp + X.disp[k]);
+                DescEntry cur;
+                cur.flags = e.flags;
+                cur.type = e.type;
+                cur.count = 1;
+                cur.blen = len / es;
+                cur.extent = int64_t(len);
+                cur.disp = e.disp + X.disp[k];
+                if (last.count == 0) {
+                    last = cur;
+                    continue;
+                }
+                if (bytes_of(last) == last.extent) {
+                    last.extent *= last.count;
+                    last.blen *= last.count;
+                    last.count = 1;
+                }
+                const int64_t lbs = bytes_of(last), cbs = bytes_of(cur);
+                if (lbs == cbs) {
+                    if (last.extent * int64_t(last.count) + last.disp == cur.disp) {
+                        last.count += 1;   // cur.count == 1
+                        continue;
+                    }
+                    if (last.count == 1) {
+                        last.extent = cur.disp - last.disp;
+                        last.count = 2;
+                        continue;
+                    }
+                }
+                // cur.count == 1, so never an inline pair: adjacent blocks fuse
+                if (last.disp + int64_t(last.count - 1) * last.extent + lbs == cur.disp) {
+                    const int64_t fext = last.extent + cur.extent;
+                    if (last.count != 1) {
+                        DescEntry head = last;
+                        head.count -= 1;
+                        emit(head);
+                        last.disp += int64_t(last.count - 1) * last.extent;
+                        last.count = 1;
+                    }
+                    last.blen += cur.blen;
+                    last.extent = fext;
+                    continue;
+                }
+                emit(last);
+                last = cur;
             }
+            if (last.count)
+                emit(last);
             continue;
         }
         put(e.flags, e.type, e.count, e.loops, e.blen, e.extent, e.disp);

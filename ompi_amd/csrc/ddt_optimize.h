@@ -58,7 +58,10 @@ void optimize_desc(const DescForm &in, int64_t size, DescForm &out, uint32_t *fl
 // Node tree of a committed description (the bridge's import, sealed lists passed through).
 bool nodes_from_desc(const DescForm &d, std::vector<Node> &out);
 
-// 32-byte entries of a description (sealed lists expanded one DATA entry per block).
-void encode_desc(const DescForm &d, std::vector<unsigned char> &out);
+// 32-byte entries of a description.  Sealed lists expand one DATA entry per block, or, with
+// `optimized` (the output of optimize_desc), with the optimizer's DATA merges applied along the
+// list (count-2 pairs at their distance, arithmetic runs extended: opal_datatype_optimize.c
+// :1146-1278), so the export of a committed 64 Mi-block list is the reference's opt_desc.
+void encode_desc(const DescForm &d, std::vector<unsigned char> &out, bool optimized = false);
 
 }  // namespace ddt

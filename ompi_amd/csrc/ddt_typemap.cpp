@@ -1566,7 +1566,7 @@ int64_t ddt_type_to_opal_opt_desc(const ddt_datatype_t *t, void *out, size_t cap
             return DDT_ERR_NOT_SUPPORTED;
         fl = 0;
         optimize_desc(in, t->size, o, &fl);
-        encode_desc(o, buf);
+        encode_desc(o, buf, true);
     }
     if (flags)
         *flags = fl;

@@ -234,3 +234,24 @@ def test_engine_snap_follows_carriers_on_mixed_types(seed):
                 assert e.snap_position(p) == b.o.set_position(count, p, send=True), (b.recipe, count, p)
                 checked += 1
     assert checked > 500
+
+
+def test_sealed_list_exports_the_reference_opt_desc():
+    """An index list of more than 2^20 blocks passes the optimizer sealed (one opaque element),
+    but its export applies the optimizer's DATA merges along the list (count-2 pairs at their
+    distance, arithmetic runs extended, blocks the constructor already fused kept whole:
+    opal_datatype_optimize.c:1146-1278), and the LOOPs around it count the expanded entries: the
+    committed description equals the oracle's entry for entry, as config 4's 33.5 M pairs would
+    (SURVEY.md §8a a3).  Its boundary with a neighbouring element stays the documented deviation."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    n = (1 << 20) + 4099
+    d = rng.permutation(8 * n)[:n] * 2
+    d[1000:1100] = 5 * np.arange(100) + 20 * n     # an arithmetic run: one entry of count 100
+    d[2000:2010] = np.arange(10) + 22 * n          # adjacent blocks: fused by the constructor
+    lst = ("indexed_block", 1, d.tolist(), ("basic", FLOAT4))
+    for rec in (lst, ("contig", 2, lst)):
+        b, eng, fl = _engine(rec)
+        assert eng == b.o.opt_desc(), rec[0]
+        assert S.unpack_entries(b.e.to_opal_desc()) == b.o.desc(), rec[0]
+        assert not fl & 0x10000
