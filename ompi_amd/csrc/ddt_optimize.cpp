@@ -20,14 +20,20 @@
 //
 // Sealed lists (engine extension): an index list of more than kSealBlocks blocks (64 Mi for
 // BASELINE config 4) is not expanded into one entry per block.  It enters the optimizer as one
-// opaque element: nothing merges into or across it, loops holding it are neither unrolled,
-// expanded nor compressed.  Inside such a list the reference only ever merges blocks of its one
-// type, so its element boundaries are the same either way; a fusion of its first or last block
-// with a neighbour of another type is the one case the engine does not reproduce.
+// entry standing for its blocks [sb, se): a pass runs the pending element against its first
+// blocks as it would against separate DATA entries, then the rest of the list is the greedy
+// merge of its blocks from a fresh start (sealed_opt_entries, O(blocks), cached), whose last
+// pending element stays pending so the next element can merge into it.  Only that greedy's
+// result is kept as a block range, never expanded.  Loops holding a list are neither unrolled,
+// expanded, compressed nor boundary-fused (none of the reference's limits lets a loop of more than
+// 2^20 items take those paths, except a boundary fusion of the list's last block with the next
+// iteration's first, the one case not reproduced: DESIGN.md §1).
 #include "ddt_optimize.h"
 
 #include <algorithm>
 #include <cstring>
+#include <map>
+#include <tuple>
 
 namespace ddt {
 namespace {
@@ -70,10 +76,113 @@ DescEntry end_entry(uint32_t items, int64_t first, uint64_t size, uint32_t flags
     return e;
 }
 
+// The optimized entries of blocks [k0, k1) of a sealed list from a fresh start: Pass::run's DATA
+// path (:1146-1278) over them, streamed -- one element type, so no mixed regions; count-1 blocks,
+// so never an inline pair -- each entry emitted as elem() writes it (CREATE_ELEM's contiguous
+// collapse).  With `pend`, the final pending element is returned there instead of emitted, with
+// the first block it covers in *pend_start; *merged tells whether any two blocks merged or fused.
+struct SealedTail {
+    DescEntry pend;
+    size_t start = 0;
+    bool merged = false;
+};
+
+template <class Emit>
+void sealed_opt_entries(const IndexList &X, uint16_t type, uint16_t flags, int64_t disp, size_t k0, size_t k1,
+                        Emit &&out, SealedTail *tail = nullptr)
+{
+    const uint64_t es = uint64_t(esz(type));
+    auto emit = [&](DescEntry x) {
+        if (x.extent == int64_t(x.blen * es)) {
+            x.blen *= x.count;
+            x.extent *= int64_t(x.count);
+            x.count = 1;
+        }
+        x.flags = uint16_t(x.flags | kData);
+        out(x);
+    };
+    DescEntry last;
+    last.count = 0;
+    size_t ls = k0, les = k0;   // first block of the pending entry / of its last element
+    bool merged = false;
+    for (size_t k = k0; k < k1; ++k) {
+        const uint64_t len = X.len.empty() ? X.ulen : X.len[k];
+        DescEntry cur;
+        cur.flags = flags;
+        cur.type = type;
+        cur.count = 1;
+        cur.blen = len / es;
+        cur.extent = int64_t(len);
+        cur.disp = disp + X.disp[k];
+        if (last.count == 0) {
+            last = cur;
+            ls = les = k;
+            continue;
+        }
+        if (bytes_of(last) == last.extent) {
+            last.extent *= last.count;
+            last.blen *= last.count;
+            last.count = 1;
+        }
+        const int64_t lbs = bytes_of(last), cbs = bytes_of(cur);
+        if (lbs == cbs) {
+            if (last.extent * int64_t(last.count) + last.disp == cur.disp) {
+                last.count += 1;
+                les = k;
+                merged = true;
+                continue;
+            }
+            if (last.count == 1) {
+                last.extent = cur.disp - last.disp;
+                last.count = 2;
+                les = k;
+                merged = true;
+                continue;
+            }
+        }
+        if (last.disp + int64_t(last.count - 1) * last.extent + lbs == cur.disp) {   // adjacent: fuse
+            const int64_t fext = last.extent + cur.extent;
+            if (last.count != 1) {
+                DescEntry head = last;
+                head.count -= 1;
+                emit(head);
+                last.disp += int64_t(last.count - 1) * last.extent;
+                last.count = 1;
+                ls = les;
+            }
+            last.blen += cur.blen;
+            last.extent = fext;
+            merged = true;
+            continue;
+        }
+        emit(last);
+        last = cur;
+        ls = les = k;
+    }
+    if (tail) {
+        tail->pend = last;
+        tail->start = ls;
+        tail->merged = merged;
+    } else if (last.count) {
+        emit(last);
+    }
+}
+
+// Fresh-start tails of sealed lists, computed once per (list, range) for all passes of a commit.
+struct SealedCache {
+    std::map<std::tuple<int32_t, uint32_t, uint32_t>, SealedTail> tails;
+    std::map<std::tuple<int32_t, uint32_t, uint32_t>, int64_t> counts;
+};
+
 // ------------------------------------------------------------------ the optimizer
+using Lists = std::vector<std::shared_ptr<const IndexList>>;
+
 class Pass {
 public:
-    Pass(const std::vector<DescEntry> &d, uint32_t *flags) : d_(d), flags_(flags) {}
+    Pass(const std::vector<DescEntry> &d, uint32_t *flags, const Lists &lists, SealedCache &cache)
+        : d_(d), flags_(flags), lists_(lists), cache_(cache)
+    {
+    }
 
     // one optimize_short pass; the output keeps the END_LOOP sentinel at [used]
     void run(std::vector<DescEntry> &o, size_t &used, bool boundary, bool *expanded, bool *reevaluate);
@@ -81,7 +190,20 @@ public:
 private:
     const std::vector<DescEntry> &d_;
     uint32_t *flags_;
+    const Lists &lists_;
+    SealedCache &cache_;
     std::vector<DescEntry> *o_ = nullptr;
+    bool *reeval_ = nullptr;
+    // the pending element is the fresh-start tail of the sealed entry at o_[tail_at_] (blocks up
+    // to tail_end_): emitted unchanged, it goes back into that entry's range instead
+    bool tail_on_ = false;
+    size_t tail_at_ = 0;
+    uint32_t tail_end_ = 0;
+    DescEntry tail_;
+
+    bool absorb(DescEntry &last, const DescEntry &cur, bool inner);
+    void emit_pending(DescEntry &last);
+    void take_sealed(const DescEntry &cur, DescEntry &last, bool inner);
 
     // CREATE_ELEM (opal_datatype_internal.h:195-209)
     void elem(uint16_t type, uint32_t flags, uint64_t blen, uint32_t count, int64_t disp, int64_t extent)
@@ -338,10 +460,150 @@ bool Pass::loop_boundary(size_t pos)   // :799-888
     return true;
 }
 
+// The DATA path of optimize_short (:1146-1278): `cur` against the pending `last`.  True when cur
+// was merged or fused into last (a head of last may have been emitted); false when the caller
+// emits last and makes cur the pending element.
+bool Pass::absorb(DescEntry &last, const DescEntry &cur, bool inner)
+{
+    if (bytes_of(last) == last.extent) {
+        last.extent *= last.count;
+        last.blen *= last.count;
+        last.count = 1;
+    }
+    const int64_t lbs = bytes_of(last), cbs = bytes_of(cur);
+    if (lbs == cbs) {   // one entry of count last + cur
+        const bool mixed = last.type != cur.type;
+        int64_t mext = last.extent;
+        const uint32_t mcount = last.count + cur.count;
+        bool can = false;
+        if (last.extent * int64_t(last.count) + last.disp == cur.disp
+            && (cur.count == 1 || last.extent == cur.extent)) {
+            can = true;
+        } else if (last.count == 1 && (cur.count == 1 || last.disp + cur.extent == cur.disp)) {
+            mext = cur.count == 1 ? cur.disp - last.disp : cur.extent;
+            can = true;
+        }
+        if (can) {
+            if (reeval_ && inner)
+                *reeval_ = true;
+            if (mixed) {
+                mixed_region(last, lbs, mcount, last.disp, mext);
+                *flags_ |= kRestricted;
+            } else {
+                last.flags |= cur.flags & kTypeChanged;
+                last.extent = mext;
+                last.count = mcount;
+            }
+            tail_on_ = false;
+            return true;
+        }
+    }
+    const bool inline_pair = last.count > 1 && cur.count > 1 && last.blen <= kInlineBlocklen
+                             && cur.blen <= kInlineBlocklen;
+    if (!inline_pair && last.disp + int64_t(last.count - 1) * last.extent + lbs == cur.disp) {
+        // fuse the last block of `last` with the first block of `cur`
+        const bool shrinks = last.count == 1 && cur.count == 1;
+        const int64_t fext = last.extent + cur.extent;
+        if (shrinks && reeval_ && inner)
+            *reeval_ = true;
+        tail_on_ = false;
+        if (last.count != 1) {
+            elem(last.type, kept(last.flags), last.blen, last.count - 1, last.disp, last.extent);
+            last.disp += int64_t(last.count - 1) * last.extent;
+            last.count = 1;
+        }
+        if (last.type == cur.type) {
+            last.flags |= cur.flags & kTypeChanged;
+            last.blen += cur.blen;
+        } else {
+            mixed_region(last, lbs + cbs, 1, last.disp, fext);
+            *flags_ |= kRestricted;
+        }
+        last.extent = fext;
+        if (cur.count != 1) {
+            elem(last.type, kept(last.flags), last.blen, last.count, last.disp, last.extent);
+            last = cur;
+            last.count -= 1;
+            last.disp += last.extent;
+        }
+        return true;
+    }
+    return false;
+}
+
+void Pass::emit_pending(DescEntry &last)
+{
+    if (last.count) {
+        const DescEntry &t = tail_;
+        if (tail_on_ && last.flags == t.flags && last.type == t.type && last.count == t.count
+            && last.blen == t.blen && last.extent == t.extent && last.disp == t.disp)
+            (*o_)[tail_at_].se = tail_end_;   // the list's own tail, untouched: back into its range
+        else
+            elem(last.type, kept(last.flags), last.blen, last.count, last.disp, last.extent);
+        last.count = 0;
+    }
+    tail_on_ = false;
+}
+
+// A sealed list against the pending element: its first blocks go through the DATA path like
+// separate entries until one starts afresh; from there the list is its fresh-start greedy, kept
+// as a block range, with that greedy's last pending element as the new pending element.
+void Pass::take_sealed(const DescEntry &cur, DescEntry &last, bool inner)
+{
+    const IndexList &X = *lists_[size_t(cur.sealed)];
+    const uint64_t es = uint64_t(esz(cur.type));
+    uint32_t k = cur.sb;
+    const uint32_t end = cur.se;
+    if (last.count) {
+        for (; k < end; ++k) {
+            const uint64_t len = X.len.empty() ? X.ulen : X.len[k];
+            DescEntry b;
+            b.flags = cur.flags;
+            b.type = cur.type;
+            b.count = 1;
+            b.blen = len / es;
+            b.extent = int64_t(len);
+            b.disp = cur.disp + X.disp[k];
+            if (!absorb(last, b, inner))
+                break;
+        }
+        if (k == end)
+            return;
+        emit_pending(last);
+    }
+    const auto key = std::make_tuple(cur.sealed, k, end);
+    auto it = cache_.tails.find(key);
+    if (it == cache_.tails.end()) {
+        SealedTail t;
+        sealed_opt_entries(X, cur.type, cur.flags, 0, k, end, [](const DescEntry &) {}, &t);
+        it = cache_.tails.emplace(key, t).first;
+    }
+    const SealedTail &t = it->second;
+    // merges among the list's own blocks happen in the first pass over them (cur.loops == 0);
+    // later passes see their result, a fixed point of the same rules
+    if (t.merged && cur.loops == 0 && reeval_ && inner)
+        *reeval_ = true;
+    last = t.pend;
+    last.disp += cur.disp;
+    if (t.start > k) {
+        DescEntry s = cur;
+        s.sb = k;
+        s.se = uint32_t(t.start);
+        s.loops = 1;   // in merged form from here on
+        put(s);
+        tail_on_ = true;
+        tail_at_ = o_->size() - 1;
+        tail_end_ = end;
+        tail_ = last;
+    }
+}
+
 void Pass::run(std::vector<DescEntry> &o, size_t &used, bool boundary, bool *expanded, bool *reevaluate)
 {
     o.clear();
     o_ = &o;
+    reeval_ = reevaluate;
+    tail_on_ = false;
     if (expanded)
         *expanded = false;
     if (reevaluate)
@@ -352,15 +614,7 @@ void Pass::run(std::vector<DescEntry> &o, size_t &used, bool boundary, bool *exp
     DescEntry last, cur;
     last.flags = 0xFFFF;
     size_t pos = 0;
-    auto flush_last = [&]() {
-        if (last.count) {
-            if (last.sealed >= 0)
-                put(last);
-            else
-                elem(last.type, kept(last.flags), last.blen, last.count, last.disp, last.extent);
-            last.count = 0;
-        }
-    };
+    auto flush_last = [&]() { emit_pending(last); };
     while (!open.empty()) {
         const DescEntry &e = d_[pos];
         if (!is_data(e) && e.type == kDescEndLoop) {
@@ -423,79 +677,20 @@ void Pass::run(std::vector<DescEntry> &o, size_t &used, bool boundary, bool *exp
             cur = e;
             cur.flags = uint16_t(kept(cur.flags));
             ++pos;
-            if (cur.sealed >= 0) {   // an opaque element: nothing merges into or across it
-                flush_last();
-                put(cur);
+            if (cur.sealed >= 0) {
+                take_sealed(cur, last, inner.back());
                 continue;
             }
         }
         // DATA (or a compressed loop) against the pending element (:1146-1278)
         if (last.count == 0) {
             last = cur;
+            tail_on_ = false;
             continue;
         }
-        if (bytes_of(last) == last.extent) {
-            last.extent *= last.count;
-            last.blen *= last.count;
-            last.count = 1;
-        }
-        const int64_t lbs = bytes_of(last), cbs = bytes_of(cur);
-        if (lbs == cbs) {   // one entry of count last + cur
-            const bool mixed = last.type != cur.type;
-            int64_t mext = last.extent;
-            const uint32_t mcount = last.count + cur.count;
-            bool can = false;
-            if (last.extent * int64_t(last.count) + last.disp == cur.disp
-                && (cur.count == 1 || last.extent == cur.extent)) {
-                can = true;
-            } else if (last.count == 1 && (cur.count == 1 || last.disp + cur.extent == cur.disp)) {
-                mext = cur.count == 1 ? cur.disp - last.disp : cur.extent;
-                can = true;
-            }
-            if (can) {
-                if (reevaluate && inner.back())
-                    *reevaluate = true;
-                if (mixed) {
-                    mixed_region(last, lbs, mcount, last.disp, mext);
-                    *flags_ |= kRestricted;
-                } else {
-                    last.flags |= cur.flags & kTypeChanged;
-                    last.extent = mext;
-                    last.count = mcount;
-                }
-                continue;
-            }
-        }
-        const bool inline_pair = last.count > 1 && cur.count > 1 && last.blen <= kInlineBlocklen
-                                 && cur.blen <= kInlineBlocklen;
-        if (!inline_pair && last.disp + int64_t(last.count - 1) * last.extent + lbs == cur.disp) {
-            // fuse the last block of `last` with the first block of `cur`
-            const bool shrinks = last.count == 1 && cur.count == 1;
-            const int64_t fext = last.extent + cur.extent;
-            if (shrinks && reevaluate && inner.back())
-                *reevaluate = true;
-            if (last.count != 1) {
-                elem(last.type, kept(last.flags), last.blen, last.count - 1, last.disp, last.extent);
-                last.disp += int64_t(last.count - 1) * last.extent;
-                last.count = 1;
-            }
-            if (last.type == cur.type) {
-                last.flags |= cur.flags & kTypeChanged;
-                last.blen += cur.blen;
-            } else {
-                mixed_region(last, lbs + cbs, 1, last.disp, fext);
-                *flags_ |= kRestricted;
-            }
-            last.extent = fext;
-            if (cur.count != 1) {
-                elem(last.type, kept(last.flags), last.blen, last.count, last.disp, last.extent);
-                last = cur;
-                last.count -= 1;
-                last.disp += last.extent;
-            }
+        if (absorb(last, cur, inner.back()))
             continue;
-        }
-        elem(last.type, kept(last.flags), last.blen, last.count, last.disp, last.extent);
+        emit_pending(last);
         last = cur;
     }
     flush_last();
@@ -510,7 +705,7 @@ uint64_t ranges(const std::vector<DescEntry> &d, const std::vector<std::shared_p
     for (size_t pos = from; pos < to;) {
         const DescEntry &e = d[pos];
         if (is_data(e)) {
-            r += e.sealed >= 0 ? lists[size_t(e.sealed)]->nblk() : e.count;
+            r += e.sealed >= 0 ? uint64_t(e.se - e.sb) : e.count;
             ++pos;
         } else if (e.type == kDescLoop) {
             const uint64_t lr = (e.flags & kContig) ? 1 : ranges(d, lists, pos + 1, pos + e.count);
@@ -530,9 +725,40 @@ void optimize_desc(const DescForm &in, int64_t size, DescForm &out, uint32_t *fl
     // opal_datatype_optimize_short_restart (:1347-1478) from opal_datatype_commit (:1765-1777)
     const int64_t limit = int64_t(in.used) * kGrowth;
     const uint32_t init = *flags;
+    // The growth cap counts entries as the reference holds them: a sealed list is nblk entries in
+    // `desc` and its optimized entries (sealed_opt_entries) after a pass.  In sealed-as-one units a
+    // form within `limit` is within the reference's cap too (a list never gains entries), so the
+    // O(blocks) count runs only when that cheaper check fails.
+    SealedCache cache;
+    int64_t in_extra = 0;
+    for (size_t i = 0; i < in.used; ++i)
+        if (in.e[i].sealed >= 0)
+            in_extra += int64_t(in.e[i].se - in.e[i].sb) - 1;
+    auto over = [&](const DescForm &f) {
+        if (int64_t(f.used) <= limit)
+            return false;
+        if (!in_extra)
+            return true;
+        int64_t extra = 0;
+        for (size_t i = 0; i < f.used; ++i) {
+            const DescEntry &x = f.e[i];
+            if (x.sealed < 0)
+                continue;
+            const auto key = std::make_tuple(x.sealed, x.sb, x.se);
+            auto it = cache.counts.find(key);
+            if (it == cache.counts.end()) {
+                int64_t m = 0;
+                sealed_opt_entries(*in.lists[size_t(x.sealed)], x.type, x.flags, 0, x.sb, x.se,
+                                   [&](const DescEntry &) { ++m; });
+                it = cache.counts.emplace(key, m).first;
+            }
+            extra += it->second - 1;
+        }
+        return int64_t(f.used) + extra > (int64_t(in.used) + in_extra) * kGrowth;
+    };
     auto short_pass = [&](const std::vector<DescEntry> &src, DescForm &dst, bool boundary, bool *expanded,
                           bool *reevaluate) {
-        Pass p(src, flags);
+        Pass p(src, flags, in.lists, cache);
         p.run(dst.e, dst.used, boundary, expanded, reevaluate);
         dst.lists = in.lists;
     };
@@ -551,13 +777,13 @@ void optimize_desc(const DescForm &in, int64_t size, DescForm &out, uint32_t *fl
     if (expanded || reeval) {
         uint64_t cand_ranges = count_ranges(cand);
         while (expanded || reeval) {
-            if (int64_t(cand.used) > limit)
+            if (over(cand))
                 break;
             bool nexp = false, nre = false;
             *flags = init | (cand_flags & kRestricted);
             short_pass(cand.e, next, true, &nexp, &nre);
             const uint64_t nr = count_ranges(next);
-            if (int64_t(next.used) > limit || (nexp && nr >= cand_ranges))
+            if (over(next) || (nexp && nr >= cand_ranges))
                 break;
             any_expanded |= nexp;
             cand_flags = *flags;
@@ -576,13 +802,13 @@ void optimize_desc(const DescForm &in, int64_t size, DescForm &out, uint32_t *fl
                 bool nre = false;
                 *flags = init | (base_flags & kRestricted);
                 short_pass(base.e, next, false, nullptr, &nre);
-                if (int64_t(next.used) > limit)
+                if (over(next))
                     break;
                 base_flags = *flags;
                 base = std::move(next);
                 reeval = nre;
             }
-            if (!(int64_t(cand.used) <= limit && cand_ranges < count_ranges(base))) {
+            if (!(!over(cand) && cand_ranges < count_ranges(base))) {
                 cand = std::move(base);
                 cand_flags = base_flags;
             }
@@ -661,6 +887,8 @@ struct Writer {
                     e.extent = int64_t(X.total);
                     e.disp = n.disp;
                     e.sealed = int32_t(f.lists.size());
+                    e.sb = 0;
+                    e.se = uint32_t(X.nblk());
                     f.lists.push_back(n.list);
                     f.e.push_back(e);
                     break;
@@ -749,76 +977,15 @@ void encode_desc(const DescForm &d, std::vector<unsigned char> &out, bool optimi
             const IndexList &X = *d.lists[size_t(e.sealed)];
             const uint64_t es = uint64_t(esz(e.type));
             if (!optimized) {
-                for (size_t k = 0; k < X.nblk(); ++k) {
+                for (size_t k = e.sb; k < e.se; ++k) {
                     const uint64_t len = X.len.empty() ? X.ulen : X.len[k];
                     put(e.flags, e.type, 1, 0, len / es, int64_t(len), e.disp + X.disp[k]);
                 }
                 continue;
             }
-            // Pass::run's DATA path over the list's blocks (one element type, so no mixed
-            // regions), streamed: `last` is the pending element, emitted as elem() does
-            auto emit = [&](const DescEntry &x) {
-                uint64_t blen = x.blen;
-                int64_t ext = x.extent;
-                uint32_t cnt = x.count;
-                if (ext == int64_t(blen * es)) {   // CREATE_ELEM's contiguous collapse
-                    blen *= cnt;
-                    ext *= int64_t(cnt);
-                    cnt = 1;
-                }
-                put(uint16_t(x.flags | kData), x.type, cnt, 0, blen, ext, x.disp);
-            };
-            DescEntry last;
-            last.count = 0;
-            for (size_t k = 0; k < X.nblk(); ++k) {
-                const uint64_t len = X.len.empty() ? X.ulen : X.len[k];
-                DescEntry cur;
-                cur.flags = e.flags;
-                cur.type = e.type;
-                cur.count = 1;
-                cur.blen = len / es;
-                cur.extent = int64_t(len);
-                cur.disp = e.disp + X.disp[k];
-                if (last.count == 0) {
-                    last = cur;
-                    continue;
-                }
-                if (bytes_of(last) == last.extent) {
-                    last.extent *= last.count;
-                    last.blen *= last.count;
-                    last.count = 1;
-                }
-                const int64_t lbs = bytes_of(last), cbs = bytes_of(cur);
-                if (lbs == cbs) {
-                    if (last.extent * int64_t(last.count) + last.disp == cur.disp) {
-                        last.count += 1;   // cur.count == 1
-                        continue;
-                    }
-                    if (last.count == 1) {
-                        last.extent = cur.disp - last.disp;
-                        last.count = 2;
-                        continue;
-                    }
-                }
-                // cur.count == 1, so never an inline pair: adjacent blocks fuse
-                if (last.disp + int64_t(last.count - 1) * last.extent + lbs == cur.disp) {
-                    const int64_t fext = last.extent + cur.extent;
-                    if (last.count != 1) {
-                        DescEntry head = last;
-                        head.count -= 1;
-                        emit(head);
-                        last.disp += int64_t(last.count - 1) * last.extent;
-                        last.count = 1;
-                    }
-                    last.blen += cur.blen;
-                    last.extent = fext;
-                    continue;
-                }
-                emit(last);
-                last = cur;
-            }
-            if (last.count)
-                emit(last);
+            sealed_opt_entries(X, e.type, e.flags, e.disp, e.sb, e.se, [&](const DescEntry &x) {
+                put(x.flags, x.type, x.count, 0, x.blen, x.extent, x.disp);
+            });
             continue;
         }
         put(e.flags, e.type, e.count, e.loops, e.blen, e.extent, e.disp);

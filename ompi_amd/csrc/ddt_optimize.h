@@ -22,8 +22,9 @@ namespace ddt {
 //   DATA      {flags, type >= 4, count, -, blocklen (elements), extent, disp}
 //   LOOP      {flags, 0, items, loops, -, extent, -}
 //   END_LOOP  {flags, 1, items, -, size, -, first_elem_disp}
-// `sealed` >= 0 marks an engine index list too long to expand entry by entry (DescForm::lists):
-// it takes part in the optimizer as one opaque element (ddt_optimize.cpp, "sealed lists").
+// `sealed` >= 0 marks an engine index list too long to expand entry by entry (DescForm::lists),
+// its blocks [sb, se) standing for the entries the optimizer makes of them (ddt_optimize.cpp,
+// "sealed lists").
 struct DescEntry {
     uint16_t flags = 0, type = 0;
     uint32_t count = 0;
@@ -32,6 +33,7 @@ struct DescEntry {
     int64_t extent = 0;
     int64_t disp = 0;
     int32_t sealed = -1;
+    uint32_t sb = 0, se = 0;
 };
 
 struct DescForm {

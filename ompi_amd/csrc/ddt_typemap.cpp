@@ -1616,13 +1616,26 @@ namespace ddt {
 bool nodes_from_desc(const DescForm &d, std::vector<Node> &out)
 {
     std::vector<unsigned char> raw(32 * d.used, 0);
+    SealedLists lists = d.lists;   // + the slices of lists whose ends merged with a neighbour
     for (size_t i = 0; i < d.used; ++i) {
         const DescEntry &e = d.e[i];
         unsigned char *p = raw.data() + 32 * i;
         std::memcpy(p, &e.flags, 2);
         if (e.sealed >= 0) {
             const uint16_t zero = 0;
-            const uint32_t idx = uint32_t(e.sealed);
+            uint32_t idx = uint32_t(e.sealed);
+            const IndexList &X = *d.lists[idx];
+            if (e.sb != 0 || e.se != X.nblk()) {
+                auto S = std::make_shared<IndexList>();
+                S->esize = X.esize;
+                S->disp.assign(X.disp.begin() + e.sb, X.disp.begin() + e.se);
+                if (X.len.empty())
+                    S->ulen = X.ulen;
+                else
+                    S->len.assign(X.len.begin() + e.sb, X.len.begin() + e.se);
+                idx = uint32_t(lists.size());
+                lists.push_back(finish_list(S));
+            }
             const uint64_t tid = e.type;
             std::memcpy(p + 2, &zero, 2);
             std::memcpy(p + 4, &idx, 4);
@@ -1643,6 +1656,6 @@ bool nodes_from_desc(const DescForm &d, std::vector<Node> &out)
         }
     }
     out.clear();
-    return parse_opal(raw.data(), 0, d.used, out, &d.lists);
+    return parse_opal(raw.data(), 0, d.used, out, &lists);
 }
 }  // namespace ddt

@@ -255,3 +255,30 @@ def test_sealed_list_exports_the_reference_opt_desc():
         assert eng == b.o.opt_desc(), rec[0]
         assert S.unpack_entries(b.e.to_opal_desc()) == b.o.desc(), rec[0]
         assert not fl & 0x10000
+
+
+def test_sealed_list_boundaries_merge_like_separate_entries():
+    """The elements around a sealed list meet its first and last blocks as the reference's
+    separate DATA entries would: a FLOAT4 before the list pairs with block 0 (shifting the pairing
+    of the whole list), an INT4 adjacent after the last block fuses into a UINT4 carrier
+    (OPTIMIZED_RESTRICTED), a DOUBLE adjacent before block 0 fuses into a mixed region; also inside
+    loops.  Engine == oracle entry for entry, and the committed tree (with the list sliced where
+    its ends merged) still walks the type map's bytes in order (raw export == oracle's)."""
+    import numpy as np
+    from tests.test_cpu_raw import engine_raw_all, stitched
+    rng = np.random.default_rng(9)
+    n = (1 << 20) + 33
+    d = (rng.permutation(8 * n)[:n] * 2 + 100).astype(np.int64)
+    lst = ("hindexed_block", 1, (d * 4).tolist(), ("basic", FLOAT4))
+    first, last = int(d[0]) * 4, int(d[-1]) * 4
+    both = ("struct", [1, 1, 1], [first - 12, 0, last + 4], [("basic", FLOAT4), lst, ("basic", INT4)])
+    cases = [both, ("struct", [1, 1], [first - 8, 0], [("basic", FLOAT8), lst]), ("contig", 2, both)]
+    for rec in cases:
+        b, eng, fl = _engine(rec)
+        assert eng == b.o.opt_desc() and bool(fl & 0x10000) == b.o.restricted()
+    b = R.Built(both)
+    info = b.o.info()
+    base = (1 << 40) + R.layout(info, 1)[1]
+    full, got = b.o.raw(1, base, 0, 1 << 22)
+    chunks, tot = engine_raw_all(b.engine(), 1, base, 1 << 22)
+    assert tot == got == info["size"] and stitched(chunks) == full

@@ -107,6 +107,21 @@ def test_fuzz_full_message(device, seed):
         _roundtrip(b, rng.choice([1, 2, 3, 7]), device, seed * 100 + n)
 
 
+def test_sealed_list_with_merged_ends(device):
+    """A >2^20-block list whose first block pairs with a FLOAT4 before it and whose last block
+    fuses with an adjacent INT4 (the optimizer slices the list for the plan, ddt_optimize.cpp):
+    packed stream, fragments and unpacked buffer bit-exact against the oracle."""
+    rng = np.random.default_rng(9)
+    n = (1 << 20) + 33
+    d = (rng.permutation(8 * n)[:n] * 2 + 100).astype(np.int64)
+    lst = ("hindexed_block", 1, (d * 4).tolist(), ("basic", 15))
+    first, last = int(d[0]) * 4, int(d[-1]) * 4
+    both = ("struct", [1, 1, 1], [first - 12, 0, last + 4], [("basic", 15), lst, ("basic", 6)])
+    b = R.Built(both)
+    _roundtrip(b, 1, device, 99)
+    _roundtrip(b, 2, device, 98, frags=[4 << 20, 12, 4096])
+
+
 def test_lb_ub_markers(device):
     """MPI_LB / MPI_UB markers (opal_datatype_add.c:158-186) move only the bounds: the packed
     stream of every count is the oracle's, and so is the unpacked user buffer."""
