@@ -269,9 +269,9 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             P.device = dev;
     }
     if (P.device != dev)
-        return fail(DDT_ERR_NOT_SUPPORTED, "datatype plan lives on device " + std::to_string(P.device)
+        return fail(DDT_ERR_NOT_SUPPORTED, "convertor prepared on device " + std::to_string(P.device)
                                                + "; current device is " + std::to_string(dev)
-                                               + " (one device per committed datatype)");
+                                               + " (prepare it again on this device)");
     const uint64_t ubase = user & ~uint64_t(15), pbase = wins[0].ptr & ~uint64_t(15);
     std::vector<uint64_t> key;
     key.reserve(4 + 3 * wins.size());

@@ -190,7 +190,9 @@ struct ddt_datatype {
     uint32_t opt_flags = 0;       // OPAL_DATATYPE_OPTIMIZED_RESTRICTED after commit (ddt_optimize.h)
     std::vector<uint64_t> opt_prefix;  // packed offset of each top-level opt node
     std::mutex plan_mu;
-    std::shared_ptr<ddt::Plan> plan;
+    // one plan per HIP device the type is moved on (index = device ordinal): a plan's descriptor
+    // sets, lists and tables live in that device's HBM
+    std::vector<std::shared_ptr<ddt::Plan>> plans;
     std::shared_ptr<ddt::ExtPlan> ext;   // external32 signature (lazy)
     int64_t extent() const { return ub - lb; }
 };

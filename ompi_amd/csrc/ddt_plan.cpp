@@ -231,10 +231,19 @@ void simplify(std::vector<LeafDim> &d, uint64_t *blen)
 
 std::shared_ptr<Plan> get_plan(ddt_datatype *t)
 {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) {   // no device here (CPU-side plan queries)
+        (void) hipGetLastError();
+        dev = -1;
+    }
+    const size_t slot = dev < 0 ? 0 : size_t(dev);
     std::lock_guard<std::mutex> g(t->plan_mu);
-    if (t->plan)
-        return t->plan;
+    if (t->plans.size() <= slot)
+        t->plans.resize(slot + 1);
+    if (t->plans[slot])
+        return t->plans[slot];
     auto P = std::make_shared<Plan>();
+    P->device = dev;
     std::vector<LeafDim> dims;
     collect(t->opt, dims, 0, P->leaves);
     P->dev.resize(P->leaves.size());
@@ -251,7 +260,7 @@ std::shared_ptr<Plan> get_plan(ddt_datatype *t)
         D.disp32 = span < (int64_t(1) << 31);
         D.disp_base = D.disp32 ? X.min_disp : 0;
     }
-    t->plan = P;
+    t->plans[slot] = P;
     return P;
 }
 
