@@ -25,9 +25,9 @@
 // merge of its blocks from a fresh start (sealed_opt_entries, O(blocks), cached), whose last
 // pending element stays pending so the next element can merge into it.  Only that greedy's
 // result is kept as a block range, never expanded.  Loops holding a list are neither unrolled,
-// expanded, compressed nor boundary-fused (none of the reference's limits lets a loop of more than
-// 2^20 items take those paths, except a boundary fusion of the list's last block with the next
-// iteration's first, the one case not reproduced: DESIGN.md §1).
+// expanded nor compressed (none of the reference's limits lets a loop of more than 2^20 items
+// take those paths); a loop-boundary fusion with the list as the body's first or last item takes
+// its first or last block and splits the range around it, as the reference's separate entries.
 #include "ddt_optimize.h"
 
 #include <algorithm>
@@ -249,6 +249,8 @@ private:
     bool fuse_tail_head(const DescEntry &tail, const DescEntry &head, int64_t delta, uint32_t rcount,
                         int64_t rextent, DescEntry &fused) const;
     void copy_range(size_t pos, uint32_t from, uint32_t to, int64_t delta);
+    DescEntry sealed_block(const DescEntry &s, uint32_t k) const;
+    void put_sealed(const DescEntry &s, uint32_t b0, uint32_t b1, int64_t delta);
     bool loop_boundary(size_t pos);
     void unrolled(size_t pos, uint32_t f);
 };
@@ -424,35 +426,91 @@ void Pass::copy_range(size_t pos, uint32_t from, uint32_t to, int64_t delta)   /
     }
 }
 
+// Block k of a sealed entry as the DATA element the reference holds for it (count 1).
+DescEntry Pass::sealed_block(const DescEntry &s, uint32_t k) const
+{
+    const IndexList &X = *lists_[size_t(s.sealed)];
+    const uint64_t len = X.len.empty() ? X.ulen : X.len[k];
+    DescEntry b;
+    b.flags = uint16_t(kept(s.flags));
+    b.type = s.type;
+    b.count = 1;
+    b.blen = len / uint64_t(esz(s.type));
+    b.extent = int64_t(len);
+    b.disp = s.disp + X.disp[k];
+    return b;
+}
+
+// A sealed entry restricted to blocks [b0, b1), shifted by delta (nothing when empty).
+void Pass::put_sealed(const DescEntry &s, uint32_t b0, uint32_t b1, int64_t delta)
+{
+    if (b0 >= b1)
+        return;
+    DescEntry e = s;
+    e.flags = uint16_t(kept(e.flags));
+    e.sb = b0;
+    e.se = b1;
+    e.disp += delta;
+    put(e);
+}
+
 bool Pass::loop_boundary(size_t pos)   // :799-888
 {
     const DescEntry &L = d_[pos], &E = d_[pos + L.count];
-    if (L.loops < 2 || L.count <= 2)
+    if (L.loops < 2)
         return false;
-    uint32_t last_item = 0, nitems = 0;
+    // the body's top-level items; a sealed list is se - sb items of the reference's
+    std::vector<uint32_t> items;
+    uint64_t ref_items = L.count, nitems = 0;
     for (uint32_t i = 1; i < L.count; i = next_item(pos, i)) {
         const DescEntry &e = d_[pos + i];
         if (!(e.type == kDescLoop && !is_data(e)) && !is_data(e))
             return false;
-        last_item = i;
-        ++nitems;
+        items.push_back(i);
+        nitems += (is_data(e) && e.sealed >= 0) ? uint64_t(e.se - e.sb) : 1;
     }
-    if (nitems < 2 || last_item == 0)
+    for (uint32_t i = 1; i < L.count; ++i)
+        if (d_[pos + i].sealed >= 0)
+            ref_items += uint64_t(d_[pos + i].se - d_[pos + i].sb) - 1;
+    if (ref_items <= 2 || nitems < 2 || items.empty())
         return false;
-    const uint32_t after_first = next_item(pos, 1);
+    const uint32_t fi = items.front(), li = items.back();
+    const DescEntry &F = d_[pos + fi], &T = d_[pos + li];
+    const bool fs = is_data(F) && F.sealed >= 0, ls = is_data(T) && T.sealed >= 0;
     DescEntry first, last, fused;
-    if (!as_elem(pos, 1, first) || !as_elem(pos, last_item, last))
+    if (fs)
+        first = sealed_block(F, F.sb);
+    else if (!as_elem(pos, fi, first))
+        return false;
+    if (ls)
+        last = sealed_block(T, T.se - 1);
+    else if (!as_elem(pos, li, last))
         return false;
     if (!fuse_tail_head(last, first, L.extent, L.loops - 1, L.extent, fused))
         return false;
-    copy_range(pos, 1, last_item, 0);
+    // the first iteration without its last item
+    if (fi == li) {
+        put_sealed(F, F.sb, F.se - 1, 0);
+    } else {
+        copy_range(pos, fi, li, 0);
+        if (ls)
+            put_sealed(T, T.sb, T.se - 1, 0);
+    }
     if (nitems == 2) {
         elem(fused.type, fused.flags, fused.blen, L.loops - 1, fused.disp, L.extent);
     } else {
-        const uint32_t steady = last_item - after_first + 2;
-        put(loop_entry(L.loops - 1, steady, L.extent, L.flags));
+        const size_t at = o_->size();
+        put(loop_entry(L.loops - 1, 0, L.extent, L.flags));
         elem(fused.type, fused.flags, fused.blen, 1, fused.disp, fused.extent);
-        copy_range(pos, after_first, last_item, L.extent);
+        if (fs)
+            put_sealed(F, F.sb + 1, fi == li ? F.se - 1 : F.se, L.extent);
+        if (fi != li) {
+            copy_range(pos, next_item(pos, fi), li, L.extent);
+            if (ls)
+                put_sealed(T, T.sb, T.se - 1, L.extent);
+        }
+        const uint32_t steady = uint32_t(o_->size() - at);   // body entries + the END_LOOP
+        (*o_)[at].count = steady;
         put(end_entry(steady, fused.disp, E.blen, L.flags));
     }
     elem(last.type, last.flags, last.blen, last.count, last.disp + int64_t(L.loops - 1) * L.extent,

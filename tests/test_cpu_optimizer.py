@@ -282,3 +282,23 @@ def test_sealed_list_boundaries_merge_like_separate_entries():
     full, got = b.o.raw(1, base, 0, 1 << 22)
     chunks, tot = engine_raw_all(b.engine(), 1, base, 1 << 22)
     assert tot == got == info["size"] and stitched(chunks) == full
+
+
+def test_sealed_list_in_a_loop_boundary_fusion():
+    """optimize_loop_boundary (:799-888) with a sealed list as the loop body's first and last
+    item: when the list's last block is byte-adjacent to the next iteration's first block, the
+    reference fuses them (a loop of count - 1 around the fused element); the engine splits the
+    list's range the same way.  Engine == oracle entry for entry."""
+    import numpy as np
+    rng = np.random.default_rng(11)
+    n = (1 << 20) + 17
+    d = (rng.permutation(8 * n)[:n] * 2 + 100).astype(np.int64)
+    if d[-1] < d[0]:
+        d[0], d[-1] = d[-1], d[0]
+    lst = ("hindexed_block", 1, (d * 4).tolist(), ("basic", FLOAT4))
+    f, last = int(d[0]) * 4, int(d[-1]) * 4
+    rec = ("contig", 3, ("resized", lst, 0, last + 4 - f))
+    b, eng, fl = _engine(rec)
+    o = b.o.opt_desc()
+    assert eng == o
+    assert any(e[1] == 0 and e[3] == 2 for e in o)   # the reference did fuse: a loop of 2

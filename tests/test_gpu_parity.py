@@ -120,6 +120,14 @@ def test_sealed_list_with_merged_ends(device):
     b = R.Built(both)
     _roundtrip(b, 1, device, 99)
     _roundtrip(b, 2, device, 98, frags=[4 << 20, 12, 4096])
+    # the list as a loop body whose last block abuts the next iteration's first (loop-boundary
+    # fusion splits the list's range around the fused block)
+    if d[-1] < d[0]:
+        d[0], d[-1] = d[-1], d[0]
+    lst = ("hindexed_block", 1, (d * 4).tolist(), ("basic", 15))
+    first, last = int(d[0]) * 4, int(d[-1]) * 4
+    _roundtrip(R.Built(("contig", 3, ("resized", lst, 0, last + 4 - first))), 1, device, 97,
+               frags=[8 << 20, 8, 100])
 
 
 def test_lb_ub_markers(device):
