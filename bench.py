@@ -806,8 +806,15 @@ def main():
             "all_gather_check": rccl,
             "kernel_ms": {"pack": round(tp * 1e3, 4), "unpack": round(tu * 1e3, 4)},
             "graph_replay_GiBs_per_gpu": (round(2.0 * S / graph_step / GiB, 3) if graph_step else None),
+            # achieved/frac: the step's pack + unpack launches together (traffic is per step too);
+            # dominant_kernel: the longer of the two alone, 2S over its own event time
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 2), "peak": 8000.0,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": None},
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
+                         "dominant_kernel": {
+                             "kernel": "unpack" if tu >= tp else "pack",
+                             "us": round(max(tp, tu) * 1e6, 2),
+                             "achieved": round(2.0 * S / max(tp, tu) / 1e9, 2),
+                             "frac": round(2.0 * S / max(tp, tu) / HBM_PEAK, 4)}},
             "floor_us": floor,
         }
         if copy and "GB_per_s" in copy:
