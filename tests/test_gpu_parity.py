@@ -51,8 +51,8 @@ def _roundtrip(b: R.Built, count: int, device, seed: int, frags=None, shift=0):
         return
     span, origin = R.layout(info, count)
     host = R.fill(span, seed)
-    pad = np.zeros(16, dtype=np.uint8)
-    user = _dev(np.concatenate([pad[:shift], host, pad]), device)
+    pad = np.zeros(max(16, shift), dtype=np.uint8)
+    user = _dev(np.concatenate([pad[:shift], host, pad[:16]]), device)
     uptr = user.data_ptr() + shift + origin
     e = b.engine()
     ref = np.frombuffer(b.o.pack(count, host, origin, 0, size, element_granular=False), dtype=np.uint8)
@@ -910,6 +910,32 @@ def test_sorted_list_engine(device, sorted_from, esz, count, density):
     _roundtrip(b, count, device, 5 + esz)
     st = b.engine().engine_info()
     assert st["sorted"] == 1 and st["chunks"] == (n + ch - 1) // ch, st
+
+
+@pytest.mark.parametrize("density,first,shift", [(4, 0, 0), (3, 0, 0), (4, 7, 28), (8, 0, 0), (2, 5, 20),
+                                                 (4, 0, 4), (4, 7, 0)])
+def test_sorted_list_engine_line_dense_pack(device, sorted_from, density, first, shift):
+    """ddt_tune sdense 1: pack 1 reads the chunk's span as 16-byte pieces of the touched 128-byte
+    lines (a kept bitmap, ranks by popcount) instead of one load per sorted offset; bit-exact both
+    ways.  The list's first element sits `first` elements into the datatype's origin and the
+    origin `shift - 4 * first` bytes past a 512-byte aligned allocation: the bitmap's lines are
+    the buffer's own when that is 0 (the dense pass runs), else the offset walk does."""
+    import ompi_amd
+    L = ompi_amd.lib()
+    sorted_from(1)
+    L.ddt_tune(b"sdense", 1)
+    try:
+        rng = np.random.default_rng(density * 10 + shift + first)
+        ch = (128 << 10) // 4
+        n = 3 * ch + 1237
+        disps = rng.permutation(density * n)[:n].astype(np.int64) + first + 1
+        disps[0] = first
+        b = R.Built(("indexed_block", 1, disps.tolist(), ("basic", 15)))
+        _roundtrip(b, 1, device, 31 + density, shift=shift)
+        _roundtrip(b, 2, device, 32 + density, shift=shift)
+        assert b.engine().engine_info()["sorted"] == 1
+    finally:
+        L.ddt_tune(b"sdense", 0)
 
 
 @pytest.mark.parametrize("seg", [64, 32])
