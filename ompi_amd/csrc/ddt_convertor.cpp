@@ -310,7 +310,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                                                          + i * uint64_t(t->extent()));
                 uint8_t *pk = reinterpret_cast<uint8_t *>(wins[0].ptr + i * uint64_t(t->size));
                 HIPCHK(SL->run(u, pk, dir, uint32_t(tuning().spol), stream, uint32_t(tuning().sunroll),
-                               uint32_t(tuning().s2unroll), tuning().sdense != 0));
+                               uint32_t(tuning().s2unroll)));
             }
             return DDT_SUCCESS;
         }
@@ -1680,8 +1680,6 @@ int ddt_tune(const char *key, long value)
         tuning().sunroll = value >= 16 ? 16 : (value >= 8 ? 8 : 4);
     else if (k == "sseg")
         tuning().sseg = (value == 128 || value == 32) ? value : 64;
-    else if (k == "sdense")
-        tuning().sdense = value;
     else if (k == "schunk")
         tuning().schunk = value == 2 ? 2 : 1;
     else if (k == "sorted_commit")

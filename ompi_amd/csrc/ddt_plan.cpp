@@ -396,16 +396,8 @@ SortedList *sorted_build(Plan &P, hipStream_t stream)
         auto S = std::make_unique<SortedList>();
         bool ok = false;
         try {
-            // the line-dense pack 1 reads whole 16-byte pieces of 128-byte lines: its bitmap is
-            // laid out on lines of a 128-byte aligned origin (a hipMalloc'd buffer's), element 0
-            // sitting (shift + min displacement) mod 128 bytes into its line; dense lists only
-            int32_t doff = -1;
-            if (tuning().sdense && esz == 4 && span_elems <= 8 * ne) {
-                const int64_t o = (L.list_shift + D.disp_base) % 128;
-                doff = int32_t(((o + 128) % 128) / 4);
-            }
             ok = S->build(ed, uint32_t(ne), uint32_t(esz), span_elems, uint32_t(segb), bs,
-                          uint32_t(tuning().schunk), doff);
+                          uint32_t(tuning().schunk));
         } catch (...) {
             pool_free(tmp);   // build() has drained its stream before throwing
             throw;

@@ -43,8 +43,6 @@ struct Tuning {
     long sunroll = 16;    // address-ordered engine: pack 1 elements per thread in flight (4, 8, 16)
     long s2unroll = 8;    // the same for its unpack pass 2' 
     long sseg = 64;       // address-ordered engine: U segment bytes (32, 64 or 128), read at plan build
-    long sdense = 0;      // address-ordered engine: line-dense pack 1 over a kept bitmap (4-byte
-                          // elements, lists touching >= 1 element in 8; read at plan build and run)
     long schunk = 1;      // address-ordered engine: 2 = half-size chunks, two pass-1 workgroups per
                           // CU (read at plan build)
     int sorted_commit = 1;   // build the address-ordered tables at commit / bridge import (1) or

@@ -32,11 +32,6 @@ struct SortedList {
     uint32_t *bstart = nullptr;  // [nb + 1] first U slot of bucket k
     uint16_t *upos = nullptr;    // [slots] position inside its bucket, 0xFFFF = padding
     void *U = nullptr;           // [slots] scratch elements
-    // line-dense pack 1 (4-byte elements, ddt_tune "sdense"): a bitmap of the touched elements
-    // over 128-byte lines and each word's rank prefix, `doff` elements before element 0 being the
-    // line start when the list's origin is 128-byte aligned plus 4 * doff
-    uint32_t *bm = nullptr, *wpre = nullptr;
-    uint32_t doff = 0;
     hipEvent_t done = nullptr;   // recorded after every run (U reuse across streams)
     hipStream_t last_stream = nullptr;
     bool used = false;
@@ -44,16 +39,13 @@ struct SortedList {
     ~SortedList();
     // hand the tables and U to `out` (the plan releases them behind its stream fences)
     void take_blocks(std::vector<void *> &out);
-    // dense_off >= 0: keep the bitmap for the line-dense pack 1, element 0 sitting dense_off
-    // elements into its 128-byte line
     bool build(const int32_t *disp, uint32_t n, uint32_t esz, uint64_t span_elems, uint32_t segb,
-               hipStream_t stream, uint32_t cdiv = 1, int32_t dense_off = -1);
+               hipStream_t stream, uint32_t cdiv = 1);
     // pol: access policy bits (POL_* in ddt_sorted.hip; ddt_tune "spol")
     // unroll: elements per thread in flight in pack 1's address-ordered gather (4, 8 or 16)
     // k2: the same for unpack pass 2' (4, 8 or 16)
-    // dense: the line-dense pack 1 when its bitmap was kept and the list's lines are aligned
     hipError_t run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol, hipStream_t stream,
-                   uint32_t unroll = 16, uint32_t k2 = 8, bool dense = false);
+                   uint32_t unroll = 16, uint32_t k2 = 8);
 };
 
 }  // namespace ddt

@@ -114,10 +114,10 @@ __device__ __forceinline__ uint32_t addr_at(const AddrList &L, uint32_t j, bool 
 
 // ------------------------------------------------------------------ plan build kernels
 __global__ __launch_bounds__(BT) void k_bitmap(const int32_t *__restrict__ disp, uint32_t n, uint32_t shift,
-                                               uint32_t off, uint32_t *__restrict__ bm, uint32_t *__restrict__ dup)
+                                               uint32_t *__restrict__ bm, uint32_t *__restrict__ dup)
 {
     for (uint32_t i = blockIdx.x * BT + threadIdx.x; i < n; i += gridDim.x * BT) {
-        const uint32_t a = (uint32_t(disp[i]) >> shift) + off;
+        const uint32_t a = uint32_t(disp[i]) >> shift;
         const uint32_t bit = 1u << (a & 31);
         const uint32_t old = atomicOr(&bm[a >> 5], bit);
         if (old & bit)
@@ -139,14 +139,13 @@ __device__ __forceinline__ uint32_t rank_of(uint32_t a, const uint32_t *bm, cons
 
 // A[j] = a; count (chunk, bucket) and remember each block's rank inside its run
 __global__ __launch_bounds__(BT) void k_rank(const int32_t *__restrict__ disp, uint32_t n, uint32_t shift,
-                                             uint32_t off, const uint32_t *__restrict__ bm,
-                                             const uint32_t *__restrict__ wpre, uint32_t ch, uint32_t rg,
-                                             uint32_t nb, uint32_t *__restrict__ A, uint32_t *__restrict__ cnt,
-                                             uint16_t *__restrict__ rr)
+                                             const uint32_t *__restrict__ bm, const uint32_t *__restrict__ wpre,
+                                             uint32_t ch, uint32_t rg, uint32_t nb, uint32_t *__restrict__ A,
+                                             uint32_t *__restrict__ cnt, uint16_t *__restrict__ rr)
 {
     for (uint32_t i = blockIdx.x * BT + threadIdx.x; i < n; i += gridDim.x * BT) {
         const uint32_t a = uint32_t(disp[i]) >> shift;
-        const uint32_t j = rank_of(a + off, bm, wpre);
+        const uint32_t j = rank_of(a, bm, wpre);
         A[j] = a;
         const uint32_t c = j / ch, k = i / rg;
         rr[i] = uint16_t(atomicAdd(&cnt[size_t(c) * nb + k], 1u));
@@ -220,15 +219,14 @@ __global__ __launch_bounds__(BT) void k_run_bases(const uint32_t *__restrict__ u
 }
 
 __global__ __launch_bounds__(BT) void k_assign(const int32_t *__restrict__ disp, uint32_t n, uint32_t shift,
-                                               uint32_t off, const uint32_t *__restrict__ bm,
-                                               const uint32_t *__restrict__ wpre, uint32_t ch, uint32_t rg,
-                                               uint32_t nb, const uint16_t *__restrict__ rr,
+                                               const uint32_t *__restrict__ bm, const uint32_t *__restrict__ wpre,
+                                               uint32_t ch, uint32_t rg, uint32_t nb, const uint16_t *__restrict__ rr,
                                                const uint16_t *__restrict__ off16, const uint32_t *__restrict__ ub,
                                                uint16_t *__restrict__ SL, uint16_t *__restrict__ upos)
 {
     for (uint32_t i = blockIdx.x * BT + threadIdx.x; i < n; i += gridDim.x * BT) {
         const uint32_t a = uint32_t(disp[i]) >> shift;
-        const uint32_t j = rank_of(a + off, bm, wpre);
+        const uint32_t j = rank_of(a, bm, wpre);
         const uint32_t c = j / ch, k = i / rg;
         const size_t ck = size_t(c) * nb + k;
         SL[j] = uint16_t(off16[ck] + rr[i]);
@@ -314,80 +312,6 @@ __global__ __launch_bounds__(PT / CDIV) void k_pack1(const uint8_t *__restrict__
     }
     __syncthreads();
     emit_runs<E, SEGB, NT>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, nts);
-}
-
-// pack pass 1, line-dense form (4-byte elements, a dense list: cfg4 touches one element in four):
-// instead of one load per element at its sorted offset, the chunk's address span is read as
-// 16-byte pieces, only those holding a touched element (a bitmap word per 128-byte line; a piece
-// with a touched element lies in that element's line, so nothing is read from a line the type map
-// does not touch), each element's rank coming from the word's prefix and a popcount.  Two
-// dependent rounds per piece (bitmap word, then data and slots) instead of the offset list's
-// 2-byte-per-element stream and its per-element requests.  `origin` is the list's line-aligned
-// origin (element 0 at origin + 4 * doff).
-template <int SEGB, int K>
-__global__ __launch_bounds__(PT) void k_pack1d(const uint8_t *__restrict__ origin, const AddrList al, uint32_t doff,
-                                               const uint32_t *__restrict__ bm, const uint32_t *__restrict__ wpre,
-                                               const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
-                                               const uint32_t *__restrict__ ub, uint8_t *__restrict__ U, uint32_t n,
-                                               uint32_t nb, uint32_t pol)
-{
-    constexpr uint32_t CH = LDS_BYTES / 4, SEG = SEGB / 4;
-    const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS, ntu = pol & POL_USER_NTL;
-    __shared__ uint32_t lds[CH + SEG];
-    __shared__ uint16_t toff[MAXNB + 1];
-    __shared__ uint32_t tub[MAXNB];
-    const uint32_t c = blockIdx.x, j0 = c * CH;
-    const uint32_t m = min(CH, n - j0);
-    stage_tables<PT>(off16, ub, c, nb, m, toff, tub);
-    // the chunk's span in 16-byte pieces (every lane reads the same two offsets)
-    const uint32_t p0 = (addr_at(al, j0, false) + doff) >> 2;
-    const uint32_t p1 = ((addr_at(al, j0 + m - 1, false) + doff) >> 2) + 1;
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(origin);
-    const uint32_t pe = (pol & POL_SKIP_USER) ? p0 : p1;
-    for (uint32_t pb = p0 + threadIdx.x; pb < pe; pb += PT * K) {
-        uint32_t bits[K], r0[K];
-#pragma unroll
-        for (int q = 0; q < K; ++q) {
-            const uint32_t p = pb + uint32_t(q) * PT;
-            bits[q] = 0;
-            r0[q] = 0;
-            if (p < pe) {
-                const uint32_t w = p >> 3, sh = (p & 7u) * 4u;
-                const uint32_t b = ldp(&bm[w], ntl);
-                bits[q] = (b >> sh) & 0xFu;
-                r0[q] = ldp(&wpre[w], ntl) + __popc(b & ((1u << sh) - 1u));
-            }
-        }
-        u32x4 v[K];
-        uint32_t s[K][4];
-#pragma unroll
-        for (int q = 0; q < K; ++q) {
-            if (!bits[q])
-                continue;
-            v[q] = ldp(&src[pb + uint32_t(q) * PT], ntu);
-            uint32_t r = r0[q];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                s[q][e] = 0xFFFFFFFFu;
-                if ((bits[q] >> e) & 1u) {
-                    if (r >= j0 && r < j0 + m)
-                        s[q][e] = ldp(&SL[r], ntl);
-                    ++r;
-                }
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < K; ++q) {
-            if (!bits[q])
-                continue;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (s[q][e] != 0xFFFFFFFFu)
-                    lds[s[q][e]] = v[q][e];
-        }
-    }
-    __syncthreads();
-    emit_runs<4, SEGB, PT>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, nts);
 }
 
 // pack pass 2: the bucket's runs scatter into LDS by destination, then stream out
@@ -600,7 +524,7 @@ T *dalloc(size_t n, uint64_t &bytes)
 void SortedList::take_blocks(std::vector<void *> &out)
 {
     for (void **p : {(void **) &A, (void **) &A16, (void **) &Abase, (void **) &SL, (void **) &off16,
-                     (void **) &ub, (void **) &bstart, (void **) &upos, &U, (void **) &bm, (void **) &wpre})
+                     (void **) &ub, (void **) &bstart, (void **) &upos, &U})
         if (*p) {
             out.push_back(*p);
             *p = nullptr;
@@ -623,7 +547,7 @@ SortedList::~SortedList()
 // list's minimum displacement, every value a multiple of esz).  Returns false (and leaves
 // nothing allocated) when the displacements repeat.
 bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t span_elems, uint32_t segb_,
-                       hipStream_t stream, uint32_t cdiv_, int32_t dense_off)
+                       hipStream_t stream, uint32_t cdiv_)
 {
     n = n_;
     esz = esz_;
@@ -637,23 +561,16 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
     uint32_t shift = 0;
     while ((1u << shift) < esz)
         ++shift;
-    const bool keep_bm = dense_off >= 0 && esz == 4 && cdiv == 1;
-    doff = keep_bm ? uint32_t(dense_off) & 31u : 0u;
-    const uint64_t words = (span_elems + doff + 31) / 32 + 1;
+    const uint64_t words = (span_elems + 31) / 32 + 1;
     const size_t runs = size_t(nc) * nb;
     uint64_t tmp_bytes = 0;
-    uint32_t *dup = nullptr, *cnt = nullptr, *padT = nullptr, *ubT = nullptr;
+    uint32_t *bm = nullptr, *wpre = nullptr, *dup = nullptr, *cnt = nullptr, *padT = nullptr, *ubT = nullptr;
     uint16_t *rr = nullptr;
     void *scan_tmp = nullptr;
-    // bm / wpre are the members: kept for the line-dense pack 1 (keep_bm), else temporaries
     auto release = [&] {   // the build's stream has been drained before every call
-        for (void *p : {(void *) dup, (void *) cnt, (void *) padT, (void *) ubT, (void *) rr, scan_tmp})
+        for (void *p : {(void *) bm, (void *) wpre, (void *) dup, (void *) cnt, (void *) padT, (void *) ubT,
+                        (void *) rr, scan_tmp})
             pool_free(p);
-        if (!keep_bm) {
-            pool_free(bm);
-            pool_free(wpre);
-            bm = wpre = nullptr;
-        }
     };
     try {
         bm = dalloc<uint32_t>(words, tmp_bytes);
@@ -666,7 +583,7 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
         HK(hipMemsetAsync(bm, 0, words * 4, stream));
         HK(hipMemsetAsync(dup, 0, 4, stream));
         HK(hipMemsetAsync(cnt, 0, runs * 4, stream));
-        hipLaunchKernelGGL(k_bitmap, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, doff, bm, dup);
+        hipLaunchKernelGGL(k_bitmap, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, bm, dup);
         hipLaunchKernelGGL(k_popc, dim3(grid_for(words, BT)), dim3(BT), 0, stream, bm, uint32_t(words), wpre);
         size_t tb = 0, tb2 = 0;
         HK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, wpre, wpre, int(words), stream));
@@ -678,9 +595,6 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
         HK(hipMemcpyAsync(&hdup, dup, 4, hipMemcpyDeviceToHost, stream));
         HK(hipStreamSynchronize(stream));
         if (hdup) {
-            pool_free(bm);
-            pool_free(wpre);
-            bm = wpre = nullptr;
             release();
             return false;
         }
@@ -690,8 +604,8 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
         off16 = dalloc<uint16_t>(runs, bytes);
         ub = dalloc<uint32_t>(runs, bytes);
         bstart = dalloc<uint32_t>(nb + 1, bytes);
-        hipLaunchKernelGGL(k_rank, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, doff, bm, wpre, ch,
-                           rg, nb, A, cnt, rr);
+        hipLaunchKernelGGL(k_rank, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, bm, wpre, ch, rg,
+                           nb, A, cnt, rr);
         {   // the 16-bit form of A, kept when every 64-element group spans < 64 Ki elements
             uint64_t cb = 0;
             A16 = dalloc<uint16_t>(n, cb);
@@ -724,12 +638,12 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
         upos = dalloc<uint16_t>(slots, bytes);
         U = dalloc<uint8_t>(size_t(slots) * esz, bytes);
         HK(hipMemsetAsync(upos, 0xFF, size_t(slots) * 2, stream));
-        hipLaunchKernelGGL(k_assign, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, doff, bm, wpre,
-                           ch, rg, nb, rr, off16, ub, SL, upos);
+        hipLaunchKernelGGL(k_assign, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, bm, wpre, ch, rg,
+                           nb, rr, off16, ub, SL, upos);
         HK(hipGetLastError());
         HK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
         HK(hipStreamSynchronize(stream));
-        dev_bytes = bytes + (keep_bm ? 2 * words * 4 : 0);
+        dev_bytes = bytes;
     } catch (...) {
         (void) hipStreamSynchronize(stream);   // queued build kernels may still use the temporaries
         release();
@@ -749,7 +663,7 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
 // A/B (profiles/r2_ab_sorted_unroll.log): pack 656 / 617 / 612 us; unpack 1' keeps 4 (its
 // scatter has one dependent load per element; 8 and 16 measured slower, 804 -> 818 / 842 us).
 hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol, hipStream_t stream,
-                           uint32_t unroll, uint32_t k2, bool dense)
+                           uint32_t unroll, uint32_t k2)
 {
     // U is one scratch per plan: a launch on another stream waits for the last one
     std::lock_guard<std::mutex> g(mu);
@@ -761,26 +675,6 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol
     const dim3 gc(nc), gb(nb), blk(PT), blk1(PT / cdiv);
     const AddrList al{A, A16, Abase};
     uint8_t *u8 = static_cast<uint8_t *>(U);
-    // the line-dense pack 1 needs the kept bitmap and element 0 at its line offset doff
-    const uint8_t *origin = user - size_t(doff) * 4;
-    if (dense && dir == 0 && bm && esz == 4 && cdiv == 1 && (uintptr_t(origin) & 127) == 0) {
-        if (segb == 128)
-            hipLaunchKernelGGL((k_pack1d<128, 4>), gc, blk, 0, stream, origin, al, doff, bm, wpre, SL, off16, ub, u8,
-                               n, nb, pol);
-        else if (segb == 32)
-            hipLaunchKernelGGL((k_pack1d<32, 4>), gc, blk, 0, stream, origin, al, doff, bm, wpre, SL, off16, ub, u8,
-                               n, nb, pol);
-        else
-            hipLaunchKernelGGL((k_pack1d<64, 4>), gc, blk, 0, stream, origin, al, doff, bm, wpre, SL, off16, ub, u8,
-                               n, nb, pol);
-        launch_pass2<4, 0>(gb, blk, stream, u8, upos, bstart, packed, n, pol, k2);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess)
-            return e;
-        used = true;
-        last_stream = stream;
-        return hipEventRecord(done, stream);
-    }
 #define DDT_SORTED_PASS1(E, SB, K, CD)                                                                          \
     if (dir == 0)                                                                                               \
         hipLaunchKernelGGL((k_pack1<E, SB, K, CD>), gc, blk1, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol); \

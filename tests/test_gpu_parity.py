@@ -912,32 +912,6 @@ def test_sorted_list_engine(device, sorted_from, esz, count, density):
     assert st["sorted"] == 1 and st["chunks"] == (n + ch - 1) // ch, st
 
 
-@pytest.mark.parametrize("density,first,shift", [(4, 0, 0), (3, 0, 0), (4, 7, 28), (8, 0, 0), (2, 5, 20),
-                                                 (4, 0, 4), (4, 7, 0)])
-def test_sorted_list_engine_line_dense_pack(device, sorted_from, density, first, shift):
-    """ddt_tune sdense 1: pack 1 reads the chunk's span as 16-byte pieces of the touched 128-byte
-    lines (a kept bitmap, ranks by popcount) instead of one load per sorted offset; bit-exact both
-    ways.  The list's first element sits `first` elements into the datatype's origin and the
-    origin `shift - 4 * first` bytes past a 512-byte aligned allocation: the bitmap's lines are
-    the buffer's own when that is 0 (the dense pass runs), else the offset walk does."""
-    import ompi_amd
-    L = ompi_amd.lib()
-    sorted_from(1)
-    L.ddt_tune(b"sdense", 1)
-    try:
-        rng = np.random.default_rng(density * 10 + shift + first)
-        ch = (128 << 10) // 4
-        n = 3 * ch + 1237
-        disps = rng.permutation(density * n)[:n].astype(np.int64) + first + 1
-        disps[0] = first
-        b = R.Built(("indexed_block", 1, disps.tolist(), ("basic", 15)))
-        _roundtrip(b, 1, device, 31 + density, shift=shift)
-        _roundtrip(b, 2, device, 32 + density, shift=shift)
-        assert b.engine().engine_info()["sorted"] == 1
-    finally:
-        L.ddt_tune(b"sdense", 0)
-
-
 @pytest.mark.parametrize("seg", [64, 32])
 @pytest.mark.parametrize("esz,count,density", [(4, 1, 4), (4, 2, 3), (8, 1, 5), (16, 1, 4), (4, 1, 64)])
 def test_sorted_list_engine_half_chunks(device, sorted_from, esz, count, density, seg):
