@@ -242,7 +242,7 @@ def test_sealed_list_exports_the_reference_opt_desc():
     distance, arithmetic runs extended, blocks the constructor already fused kept whole:
     opal_datatype_optimize.c:1146-1278), and the LOOPs around it count the expanded entries: the
     committed description equals the oracle's entry for entry, as config 4's 33.5 M pairs would
-    (SURVEY.md §8a a3).  Its boundary with a neighbouring element stays the documented deviation."""
+    (SURVEY.md §8a a3).  Boundaries with neighbouring elements: the next two tests."""
     import numpy as np
     rng = np.random.default_rng(5)
     n = (1 << 20) + 4099
