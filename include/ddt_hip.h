@@ -339,7 +339,8 @@ int ddt_debug_host_window(const void *p, size_t n, uint64_t *device_addr);
 /* Tuning knobs for A/B measurements (affect descriptor sets built afterwards):
  * "nt" = user-side non-temporal gathers (-1 auto = off since round 3, 0 off, 1 on); "task_kb" = packed KiB per
  * workgroup (0 adaptive); "policy" = task sizing (0 v0, 1 per-leaf passes); "interleave" =
- * reorder items in runs of this many tasks (0 off); "wt" = write-through stores (-1 auto,
+ * reorder a pack's items in runs of this many tasks (0 off, default); "uinterleave" = the same for
+ * an unpack (256 default, -1 as "interleave"); "wt" = write-through stores (-1 auto,
  * 0 off, 1 every sparse leaf, 2 all); "sorted" = address-ordered list engine (-1 auto from
  * 1 Mi blocks, 0 off, n > 0 from n blocks; read when a type's plan first runs);
  * "spol" = the address-ordered engine's

@@ -278,6 +278,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     key.push_back(count);
     key.push_back(user - ubase);
     key.push_back(same_layout ? 1 : 0);
+    key.push_back(uint64_t(same_layout ? interleave_of(0) : interleave_of(dir)));   // item order
     for (const Window &w : wins) {
         key.push_back(w.w0);
         key.push_back(w.w1);
@@ -337,7 +338,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         } catch (const std::exception &ex) {
             return fail(DDT_ERR_NOT_SUPPORTED, ex.what());
         }
-        assign_tasks(S->items);
+        assign_tasks(S->items, same_layout ? 0 : dir);
         S->ntasks = total_tasks(S->items);
         for (Item &it : S->items)
             it.slab = use_slab(it) ? (tuning().xchunk > 0 ? uint32_t(tuning().xchunk) : SLAB_FULL) : 0;
@@ -1652,6 +1653,8 @@ int ddt_tune(const char *key, long value)
         tuning().task_kb = value;
     else if (k == "interleave")
         tuning().interleave = value;
+    else if (k == "uinterleave")
+        tuning().uinterleave = value < 0 ? -1 : value;
     else if (k == "policy")
         tuning().policy = int(value);
     else if (k == "ptr")

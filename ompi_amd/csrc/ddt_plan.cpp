@@ -859,7 +859,12 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
     }
 }
 
-void assign_tasks(std::vector<Item> &items)
+long interleave_of(int dir)
+{
+    return dir == 1 && tuning().uinterleave >= 0 ? tuning().uinterleave : tuning().interleave;
+}
+
+void assign_tasks(std::vector<Item> &items, int dir)
 {
     uint64_t total = 0;
     for (const Item &it : items)
@@ -911,11 +916,14 @@ void assign_tasks(std::vector<Item> &items)
             it.units_per_task = u < THREADS ? THREADS : u;
         }
     }
-    const long chunk = tuning().interleave;
+    // Split items into runs of `chunk` tasks and order the runs by their fractional position
+    // inside their item, so that leaves of different access classes share the chip instead of
+    // running back to back.  Unpacks take 256 (round 4, profiles/r4_ab_interleave.jsonl: the
+    // halo's unpack 89.6 -> 86.5 us, cfg3's 85.7 -> 80.6 us, the partial-line writes of the sparse
+    // faces draining under the streaming faces); packs keep item order (the same split costs the
+    // halo's pack 75 -> 80 us: its sparse gathers are latency-bound and lose the streams' overlap).
+    const long chunk = interleave_of(dir);
     if (chunk > 0 && items.size() > 1) {
-        // Split items into runs of `chunk` tasks and order the runs by their fractional
-        // position inside their item, so gather-bound and streaming leaves share the chip
-        // instead of running back to back.
         struct Piece { double key; size_t seq; Item it; };
         std::vector<Piece> pieces;
         size_t seq = 0;

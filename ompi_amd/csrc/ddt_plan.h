@@ -16,7 +16,8 @@ namespace ddt {
 struct Tuning {
     int nt = -1;       // user-side non-temporal loads: -1 auto (off, use_nt), 0 off, 1 on
     long task_kb = 0;  // packed KiB per workgroup task: 0 = adaptive
-    long interleave = 0;  // >0: interleave items in runs of this many tasks
+    long interleave = 0;  // >0: interleave items in runs of this many tasks (pack, typed copy)
+    long uinterleave = 256;  // the same for an unpack (-1: as `interleave`); see assign_tasks
     int policy = 1;       // task sizing: 0 = v0 (~6 K tasks), 1 = per-leaf passes
     int wt = -1;          // write-through (sc1) stores: -1 auto, 0 off, 1 sparse user side, 2 all
     long sorted = -1;     // address-ordered list engine: -1 auto, 0 off, n > 0 from n blocks up
@@ -56,7 +57,9 @@ hipError_t private_stream(hipStream_t *out);
 
 void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t user, uint64_t pk,
                  uint64_t W0, uint64_t W1, bool same_layout, std::vector<Item> &items);
-void assign_tasks(std::vector<Item> &items);
+// Task sizes and order of a launch's items; dir 1 (unpack) interleaves by tuning().uinterleave.
+void assign_tasks(std::vector<Item> &items, int dir = 0);
+long interleave_of(int dir);
 // The address-ordered engine of plan P for a whole-message pack/unpack, built on first use;
 // null when the plan does not qualify (or `user` is misaligned for it).
 SortedList *sorted_plan(const ddt_datatype *t, Plan &P, uint64_t user, hipStream_t stream);
