@@ -339,6 +339,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             return fail(DDT_ERR_NOT_SUPPORTED, ex.what());
         }
         assign_tasks(S->items, same_layout ? 0 : dir);
+        stream_policy(S->items);
         S->ntasks = total_tasks(S->items);
         for (Item &it : S->items)
             it.slab = use_slab(it) ? (tuning().xchunk > 0 ? uint32_t(tuning().xchunk) : SLAB_FULL) : 0;
@@ -1588,6 +1589,7 @@ int ddt_debug_items(const ddt_datatype_t *t, size_t count, uint64_t user, uint64
         return fail(DDT_ERR_NOT_SUPPORTED, ex.what());
     }
     assign_tasks(items);
+    stream_policy(items);
     if (item_size)
         *item_size = sizeof(Item);
     if (nitems)
@@ -1690,7 +1692,7 @@ int ddt_tune(const char *key, long value)
     else if (k == "stage_mb")
         tuning().stage_mb = value < 1 ? 1 : value;
     else if (k == "snt")
-        tuning().snt = value < -1 ? -2 : (value < 0 ? -1 : (value >= 3 && value <= 5 ? int(value) : (value ? 1 : 0)));
+        tuning().snt = value < -2 ? -3 : (value < 0 ? int(value) : ((value >= 3 && value <= 5) || value == 7 ? int(value) : (value ? 1 : 0)));
     else if (k == "dfast")
         tuning().dfast = int(value & 3);
     else if (k == "dense")

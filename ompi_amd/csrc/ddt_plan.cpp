@@ -584,13 +584,14 @@ uint32_t use_wt(uint32_t U, uint64_t blen, const std::vector<LeafDim> *dims)
 //     directions (3) 0.795 against 0.778 for (5) (unpack 88.3 -> 84.6 us), and without the
 //     flush 0.785 against 0.789; stores non-temporal (1) 0.684.  So (3) for every stream.
 // The halo and cfg3 (x/dim-2 gathers in the same launch) move by <= 1 % either way.
-// ddt_tune("snt"): -1 this rule, -2 the first rule, 0 off, 1 / 3 / 4 / 5 forced.
+// ddt_tune("snt"): -1 this rule and stream_policy's, -3 this rule alone, -2 the first rule, 0 off,
+// 1 / 3 / 4 / 5 / 7 forced.
 uint32_t use_snt(uint32_t U, uint64_t blen)   // Item::nt of a streaming leaf, 0 = none
 {
     const int force = tuning().snt;
     if (U != 16)
         return 0;
-    if (force >= 0)   // 1 both, 3 loads only, 4 stores only, 5 pack loads only
+    if (force >= 0)   // 1 both, 3 loads only, 4 stores only, 5 pack loads only, 7 loads + pack stores
         return force && blen >= 256 ? (force == 1 ? 2u : uint32_t(force)) : 0u;
     if (force == -2)  // round-2 first rule: long runs every access non-temporal
         return blen >= (64u << 10) ? 2u : 0u;
@@ -862,6 +863,28 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
 long interleave_of(int dir)
 {
     return dir == 1 && tuning().uinterleave >= 0 ? tuning().uinterleave : tuning().interleave;
+}
+
+// A launch whose items mix streams with isolated narrow blocks (the halo's x faces, cfg3's
+// dim-2 face: one element per 128-byte line, Item::wt == 3) runs its streams with every load AND
+// store non-temporal (Item::nt 2): the sparse lines are what the Infinity Cache can save (an unpack's
+// partial-line writes merge there instead of in DRAM, a pack's gathers hit there), and plain
+// stream stores evict them: the halo's step (pair loop) 164.0 -> 158.9 us, its pack 77.5 -> 68.8
+// (the unpack before it no longer leaves 32 MiB of dirty stream lines), its unpack 86.6 -> 90.2;
+// cfg3, the x faces alone and the y / z faces alone unchanged (profiles/r4_ab_snt_mix.jsonl, r4q
+// rows).  Streams alone keep loads-only (3): the y / z faces lose 8-24 % with non-temporal stores
+// in every direction (r4o / r4p rows, snt 1 / 4 / 7).
+void stream_policy(std::vector<Item> &items)
+{
+    if (tuning().snt != -1)
+        return;
+    bool sparse = false;
+    for (const Item &it : items)
+        sparse = sparse || (it.kind == ITEM_AFFINE && it.wt == 3);
+    if (sparse)
+        for (Item &it : items)
+            if (it.kind == ITEM_AFFINE && it.nt == 3)
+                it.nt = 2;
 }
 
 void assign_tasks(std::vector<Item> &items, int dir)

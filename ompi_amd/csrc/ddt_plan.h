@@ -60,6 +60,8 @@ void build_items(const ddt_datatype *t, const Plan &P, uint64_t count, uint64_t 
 // Task sizes and order of a launch's items; dir 1 (unpack) interleaves by tuning().uinterleave.
 void assign_tasks(std::vector<Item> &items, int dir = 0);
 long interleave_of(int dir);
+// Launch-level cache policy of streaming items (see ddt_plan.cpp).
+void stream_policy(std::vector<Item> &items);
 // The address-ordered engine of plan P for a whole-message pack/unpack, built on first use;
 // null when the plan does not qualify (or `user` is misaligned for it).
 SortedList *sorted_plan(const ddt_datatype *t, Plan &P, uint64_t user, hipStream_t stream);
