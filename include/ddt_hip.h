@@ -350,7 +350,7 @@ int ddt_debug_host_window(const void *p, size_t n, uint64_t *device_addr);
  * gathers stay round-robin; 0: all round-robin; 1: all slabs); "xchunk" = tasks per XCD run for
  * slab items (0, default: one slab per XCD); "snt" = cache policy of streaming leaves (-1 auto:
  * non-temporal loads, and stores too in a launch with isolated narrow blocks; -3 loads only; else
- * an Item::nt mode 0-5, 7); "spass" = workgroup passes per streaming task; "stask" = bytes per
+ * an Item::nt mode 0-5); "spass" = workgroup passes per streaming task; "stask" = bytes per
  * streaming task (0, default: spass passes); "dense" = line-dense records moved through LDS
  * with whole-line accesses (-1 auto, 0 off, n chunks per task); "dsplit" = such an unpack runs
  * each task as two workgroups (1 default, 0 off); "dfast" = a large single-item line-dense launch

@@ -1692,7 +1692,7 @@ int ddt_tune(const char *key, long value)
     else if (k == "stage_mb")
         tuning().stage_mb = value < 1 ? 1 : value;
     else if (k == "snt")
-        tuning().snt = value < -2 ? -3 : (value < 0 ? int(value) : ((value >= 3 && value <= 5) || value == 7 ? int(value) : (value ? 1 : 0)));
+        tuning().snt = value < -2 ? -3 : (value < 0 ? int(value) : (value >= 3 && value <= 5 ? int(value) : (value ? 1 : 0)));
     else if (k == "dfast")
         tuning().dfast = int(value & 3);
     else if (k == "dense")

@@ -140,8 +140,7 @@ template <typename T, bool WT> __device__ __forceinline__ void st(T *p, T v)
 // NT: 0 plain; 1 non-temporal user-side loads (pack of sparse gathers, Item::nt == 1);
 // streaming leaves (Item::nt >= 2): 2 every load and store non-temporal, 3 loads only,
 // 4 stores only, 5 loads only and only when packing (the user-side rows); 6 non-temporal
-// user-side stores of an unpack (isolated narrow blocks, Item::wt == 3); 7 loads, and the
-// packed-side stores of a pack.
+// user-side stores of an unpack (isolated narrow blocks, Item::wt == 3).
 template <int U, int DIR, int ND, int NT, bool WT>
 __device__ __forceinline__ void run_affine(const Item *it, Bases bs, uint32_t ub, uint32_t ue)
 {
@@ -166,13 +165,13 @@ __device__ __forceinline__ void run_affine(const Item *it, Bases bs, uint32_t ub
                 nest_offsets32(n, blk, uo, po);
                 const T *src = reinterpret_cast<const T *>(DIR == 0 ? user + uo : packed + po);
                 dst[k] = reinterpret_cast<T *>(DIR == 0 ? packed + po : user + uo);
-                v[k] = ld<T, ((NT == 1 || NT == 5) && DIR == 0) || NT == 2 || NT == 3 || NT == 7>(src);
+                v[k] = ld<T, ((NT == 1 || NT == 5) && DIR == 0) || NT == 2 || NT == 3>(src);
             }
         }
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (dst[k]) {
-                if constexpr (NT == 2 || NT == 4 || NT == 6 || (NT == 7 && DIR == 0))
+                if constexpr (NT == 2 || NT == 4 || NT == 6)
                     __builtin_nontemporal_store(v[k], dst[k]);
                 else
                     st<T, WT>(dst[k], v[k]);
@@ -636,7 +635,6 @@ __device__ __forceinline__ void move_task(const Item *__restrict__ items, uint32
                 if (it->nt == 3) dispatch_affine_u<16, DIR, 3, false>(it, bs, uint32_t(ub), uint32_t(ue));
                 else if (it->nt == 4) dispatch_affine_u<16, DIR, 4, false>(it, bs, uint32_t(ub), uint32_t(ue));
                 else if (it->nt == 5) dispatch_affine_u<16, DIR, 5, false>(it, bs, uint32_t(ub), uint32_t(ue));
-                else if (it->nt == 7) dispatch_affine_u<16, DIR, 7, false>(it, bs, uint32_t(ub), uint32_t(ue));
                 else dispatch_affine_u<16, DIR, 2, false>(it, bs, uint32_t(ub), uint32_t(ue));
             } else if (DIR == 1 && it->wt == 3) {
                 dispatch_affine<DIR, 6, false>(it, bs, uint32_t(ub), uint32_t(ue));

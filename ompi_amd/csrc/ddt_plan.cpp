@@ -585,13 +585,13 @@ uint32_t use_wt(uint32_t U, uint64_t blen, const std::vector<LeafDim> *dims)
 //     flush 0.785 against 0.789; stores non-temporal (1) 0.684.  So (3) for every stream.
 // The halo and cfg3 (x/dim-2 gathers in the same launch) move by <= 1 % either way.
 // ddt_tune("snt"): -1 this rule and stream_policy's, -3 this rule alone, -2 the first rule, 0 off,
-// 1 / 3 / 4 / 5 / 7 forced.
+// 1 / 3 / 4 / 5 forced.
 uint32_t use_snt(uint32_t U, uint64_t blen)   // Item::nt of a streaming leaf, 0 = none
 {
     const int force = tuning().snt;
     if (U != 16)
         return 0;
-    if (force >= 0)   // 1 both, 3 loads only, 4 stores only, 5 pack loads only, 7 loads + pack stores
+    if (force >= 0)   // 1 both, 3 loads only, 4 stores only, 5 pack loads only
         return force && blen >= 256 ? (force == 1 ? 2u : uint32_t(force)) : 0u;
     if (force == -2)  // round-2 first rule: long runs every access non-temporal
         return blen >= (64u << 10) ? 2u : 0u;
@@ -873,7 +873,9 @@ long interleave_of(int dir)
 // (the unpack before it no longer leaves 32 MiB of dirty stream lines), its unpack 86.6 -> 90.2;
 // cfg3, the x faces alone and the y / z faces alone unchanged (profiles/r4_ab_snt_mix.jsonl, r4q
 // rows).  Streams alone keep loads-only (3): the y / z faces lose 8-24 % with non-temporal stores
-// in every direction (r4o / r4p rows, snt 1 / 4 / 7).
+// (r4o / r4p rows, snt 1 / 4 and a pack-stores-only mode).  In the mixed launch the unpack's
+// stream stores are what matter: non-temporal there alone ties (r4t rows, modes built for the
+// A/B and removed).
 void stream_policy(std::vector<Item> &items)
 {
     if (tuning().snt != -1)
