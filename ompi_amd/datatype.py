@@ -36,7 +36,7 @@ ORDER_FORTRAN = 1
 class Datatype:
     """A committed-or-not engine datatype (opaque ``ddt_datatype_t*``)."""
 
-    __slots__ = ("handle", "owned", "name")
+    __slots__ = ("handle", "owned", "name", "subtypes")
 
     def __init__(self, handle: int, owned: bool = True, name: str = "derived"):
         if not handle:
@@ -44,6 +44,7 @@ class Datatype:
         self.handle = ctypes.c_void_p(handle)
         self.owned = owned
         self.name = name
+        self.subtypes = ()   # recipe.build_committed: the sub-types it was built from
 
     # --- lifetime ---------------------------------------------------------
     def commit(self) -> "Datatype":

@@ -59,12 +59,9 @@ def build(recipe, memo=None):
 
 
 def build_committed(recipe):
-    """Build and commit; the returned type keeps its sub-types alive."""
+    """Build and commit; the returned type keeps its sub-types alive (and frees them with it)."""
     memo: dict = {}
     t = build(recipe, memo)
     t.commit()
-    _keepalive[id(t)] = memo
+    t.subtypes = tuple(v[0] for v in memo.values() if v[0] is not t)
     return t
-
-
-_keepalive: dict = {}
