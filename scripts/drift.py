@@ -30,7 +30,11 @@ def main():
     ap.add_argument("--pad-gb", type=float, default=0, help="cycles: allocate this much HBM first (placement probe)")
     ap.add_argument("--pad-after", action="store_true", help="allocate the pad after the user buffer, before the type")
     ap.add_argument("--pad-chunks", type=int, default=1, help="the pad as this many separate allocations")
+    ap.add_argument("--tune", default="", help="ddt_tune settings k=v;k=v before anything is built")
     args = ap.parse_args()
+    for kv in filter(None, args.tune.split(";")):
+        k, v = kv.split("=")
+        ompi_amd.lib().ddt_tune(k.encode(), int(v))
     if args.cycles:
         return cycles(args)
     dev = torch.device("cuda:0")
@@ -115,7 +119,7 @@ def cycles(args):
                 evs.append((a, b, c))
         torch.cuda.synchronize()
         L.ddt_pool_info(pool)
-        print(json.dumps({"config": args.config, "cycle": k, "pad_gb": args.pad_gb, "pad_after": args.pad_after,
+        print(json.dumps({"config": args.config, "cycle": k, "tune": args.tune, "pad_gb": args.pad_gb, "pad_after": args.pad_after,
                           "pad_chunks": args.pad_chunks,
                           "pack_us": round(statistics.median(a.elapsed_time(b) for a, b, _ in evs) * 1e3, 1),
                           "unpack_us": round(statistics.median(b.elapsed_time(c) for _, b, c in evs) * 1e3, 1),
