@@ -876,14 +876,21 @@ long interleave_of(int dir)
 // (r4o / r4p rows, snt 1 / 4 and a pack-stores-only mode).  In the mixed launch the unpack's
 // stream stores are what matter: non-temporal there alone ties (r4t rows, modes built for the
 // A/B and removed).
+// Only when the sparse lines overflow the L2s (8 XCDs x 4 MiB): below that the whole launch is
+// cache-resident and the plain stores win (the halo of 1 / 2 fields, 16 / 32 MiB of x lines:
+// 18.5 -> 19.6 / 22.6 -> 24.1 us with the rule; 3 fields, 48 MiB: 30.3 -> 29.4; 8: 70.8 -> 64.8;
+// 64: 700.9 -> 685.0; profiles/r4_ab_snt_mix.jsonl, r4z2 / r4z3 rows).
+constexpr uint64_t kL2Bytes = uint64_t(32) << 20;
+
 void stream_policy(std::vector<Item> &items)
 {
     if (tuning().snt != -1)
         return;
-    bool sparse = false;
+    uint64_t lines = 0;
     for (const Item &it : items)
-        sparse = sparse || (it.kind == ITEM_AFFINE && it.wt == 3);
-    if (sparse)
+        if (it.kind == ITEM_AFFINE && it.wt == 3)
+            lines += (it.u1 - it.u0) / (it.upb ? it.upb : 1);   // one block per line
+    if (lines * 128 > kL2Bytes)
         for (Item &it : items)
             if (it.kind == ITEM_AFFINE && it.nt == 3)
                 it.nt = 2;
