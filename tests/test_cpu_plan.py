@@ -177,6 +177,36 @@ def test_interleaved_task_order_matches_oracle(chunk):
         L.ddt_tune(b"task_kb", 0)
 
 
+def test_stream_policy_of_mixed_launches():
+    """ddt_plan.cpp:stream_policy: the halo's streaming faces (y, z: U = 16, nt 3 = non-temporal
+    loads) turn fully non-temporal (nt 2) beside isolated narrow blocks (the x faces, wt 3) only
+    when those blocks' lines overflow the L2s (32 MiB: 2 fields of x lines fill it exactly);
+    streams alone keep nt 3 at any size; snt -3 switches the rule off."""
+    import bench
+    from ompi_amd import lib
+    from ompi_amd import recipe as ER
+    halo, _ = bench.halo_recipe()
+    faces = bench.face_recipes()
+
+    def nts(recipe, count):
+        t = ER.build_committed(recipe)
+        its = E.items(t, count, 0, 0, 0, t.info()["size"] * count)
+        return ({it.nt for it in its if it.kind == E.ITEM_AFFINE and it.U == 16},
+                {it.wt for it in its if it.kind == E.ITEM_AFFINE and it.U == 8})
+
+    assert nts(halo, 16) == ({2}, {3})
+    assert nts(halo, 3) == ({2}, {3})
+    assert nts(halo, 2) == ({3}, {3})
+    assert nts(halo, 1) == ({3}, {3})
+    assert nts(faces["y"], 64)[0] == {3} and nts(faces["z"], 64)[0] == {3}
+    L = lib()
+    L.ddt_tune(b"snt", -3)
+    try:
+        assert nts(halo, 16)[0] == {3}
+    finally:
+        L.ddt_tune(b"snt", -1)
+
+
 def test_reference_resized_extent_bounds():
     """resized_extent.c:148-163 known answers, engine and oracle: resized(int, 0, 6) has
     lb 0 / extent 6 / true_lb 0 / true_extent 4; contiguous(3, it) keeps extent 18 (not the
