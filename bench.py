@@ -119,11 +119,17 @@ def make_workload(name):
     raise SystemExit(f"unknown config {name}")
 
 
-def layout(info, count):
+def layout(info, count, align=256):
+    """(span, origin): a buffer of `span` bytes whose byte `origin` is the type origin (the
+    array's base address; negative when the type touches nothing before true_lb).  The buffer
+    holds only the touched bytes, starting up to align - 1 bytes early so that the type origin
+    sits on an `align`-byte boundary, as an allocator places an array: without it cfg3's grid
+    (first touched byte at 2044) would start 4-byte aligned and its planes and rows with it."""
     ext = info["ub"] - info["lb"]
     lo = min(info["true_lb"], info["true_lb"] + (count - 1) * ext)
     hi = max(info["true_ub"], info["true_ub"] + (count - 1) * ext)
-    return hi - lo, -lo
+    pad = lo % align
+    return hi - lo + pad, pad - lo
 
 
 # ------------------------------------------------------------------ CPU baseline
