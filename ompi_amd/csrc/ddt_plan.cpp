@@ -871,8 +871,8 @@ long interleave_of(int dir)
 // partial-line writes merge there instead of in DRAM, a pack's gathers hit there), and plain
 // stream stores evict them: the halo's step (pair loop) 164.0 -> 158.9 us, its pack 77.5 -> 68.8
 // (the unpack before it no longer leaves 32 MiB of dirty stream lines), its unpack 86.6 -> 90.2;
-// cfg3, the x faces alone and the y / z faces alone unchanged (profiles/r4_ab_snt_mix.jsonl, r4q
-// rows).  Streams alone keep loads-only (3): the y / z faces lose 8-24 % with non-temporal stores
+// the x faces alone and the y / z faces alone unchanged (profiles/r4_ab_snt_mix.jsonl, r4q rows);
+// cfg3 on the aligned bench layout 152.5 -> 149.7 us (r4_ab_cfg3_tasks.jsonl, r4al rows).  Streams alone keep loads-only (3): the y / z faces lose 8-24 % with non-temporal stores
 // (r4o / r4p rows, snt 1 / 4 and a pack-stores-only mode).  In the mixed launch the unpack's
 // stream stores are what matter: non-temporal there alone ties (r4t rows, modes built for the
 // A/B and removed).
