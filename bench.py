@@ -281,6 +281,130 @@ def single_face_latency(dev, stream, user, origin, reps=200):
     return out
 
 
+# ------------------------------------------------------------------ back-to-back small launches
+HBM_MEASURED = 6.29e12     # float4 copy on MI355X (MI355X_MICROARCH.md, chip-level table)
+BOUNDARY_US = (1.45, 1.9)  # dependent kernel boundary, same stream (MI355X_MICROARCH.md "boundary")
+
+
+def back_to_back(dev, fields, K=200, faces=("x", "y", "z"), with_copy=True):
+    """Small-message throughput where halos live: K operations of ONE face type
+    over `fields` fields between ONE event pair -- no event pair per operation.
+
+      eager:  the K launches are enqueued while a sleep kernel holds the stream, so the events
+              time the device running them back to back (each launch's boundary + kernel), not
+              the host's enqueue rate;
+      host:   the same K launches from an idle stream (events around the whole loop): what a
+              host that enqueues one operation at a time sustains;
+      graph:  the K operations captured once into a HIP graph and replayed.
+    For every path: K packs, K unpacks, and K pack+unpack pairs (per operation = /2K).  Paths:
+    the engine (Convertor.prepare + pack/unpack), the face's bare kernel (ddt_floor.hip) and,
+    for the dense faces, a contiguous copy of the same bytes; an empty kernel prices the
+    boundary under the same protocol.  `hbm_us` = the operation's 2S bytes at the measured
+    6.29 TB/s; `model_us` = that + the guide's 1.45-1.9 us boundary."""
+    import ctypes
+    import torch
+    import ompi_amd
+    from ompi_amd import recipe as ER
+    recs = face_recipes()
+    field = 256 ** 3 * 8
+    user = torch.empty(fields * field, dtype=torch.uint8, device=dev)
+    user.fill_(0x5A)
+    stream = torch.cuda.current_stream(dev)
+    L, Part = floor_lib()
+    tiny = torch.zeros(1, device=dev)
+
+    def timed(fn, mode):
+        """per-operation us of K calls of fn(i) (i = call index) under `mode`"""
+        for i in range(4):
+            fn(i)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if mode == "graph":
+            gs = torch.cuda.Stream(dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=gs, capture_error_mode="relaxed"):
+                for i in range(K):
+                    fn(i, torch.cuda.current_stream(dev))
+            with torch.cuda.stream(gs):
+                g.replay()
+                torch.cuda.synchronize()
+                a.record(gs)
+                g.replay()
+                b.record(gs)
+            torch.cuda.synchronize()
+            del g
+        else:
+            if mode == "eager":
+                torch.cuda._sleep(int(3e8))   # hold the stream while the host enqueues the K calls
+            a.record(stream)
+            for i in range(K):
+                fn(i)
+            b.record(stream)
+            torch.cuda.synchronize()
+        return a.elapsed_time(b) * 1e3 / K
+
+    out = {"fields": fields, "K": K}
+    op = [0]
+
+    def empty(i, s=None):
+        tiny.add_(1)
+    out["empty_kernel_us"] = {m: round(timed(empty, m), 3) for m in ("eager", "host", "graph")}
+    for k in faces:
+        ft = ER.build_committed(recs[k])
+        S = ft.info()["size"] * fields
+        pk = torch.empty(S, dtype=torch.uint8, device=dev)
+        cv = ompi_amd.Convertor()
+        kind, es, ls, ss, base, lw = face_floor_part(k, fields)
+        part = Part(kind, es, ls[0], ls[1], ls[2], lw, ss[0], ss[1], ss[2], base, 0)
+
+        def engine(d):
+            def f(i, s=None):
+                dd = d if d < 2 else i & 1
+                cv.set_stream(s or stream, True)
+                if dd == 0:
+                    cv.prepare_for_send(ft, fields, user.data_ptr())
+                    cv.pack([(pk, S)])
+                else:
+                    cv.prepare_for_recv(ft, fields, user.data_ptr())
+                    cv.unpack([(pk, S)])
+            return f
+
+        def bare(d):
+            def f(i, s=None):
+                dd = d if d < 2 else i & 1
+                L.ddt_floor_launch(ctypes.c_void_p(user.data_ptr()), ctypes.c_void_p(pk.data_ptr()),
+                                   ctypes.byref(part), dd, ctypes.c_void_p((s or stream).cuda_stream))
+            return f
+        src = user[:S]
+
+        def copy(d):
+            def f(i, s=None):
+                dd = d if d < 2 else i & 1
+                (pk.copy_(src) if dd == 0 else src.copy_(pk))
+            return f
+        paths = [("engine", engine), ("bare", bare)] + ([("copy", copy)] if with_copy and k != "x" else [])
+        res = {"bytes": S, "hbm_us": round(2 * S / HBM_MEASURED * 1e6, 3)}
+        res["model_us"] = [round(res["hbm_us"] + x, 3) for x in BOUNDARY_US]
+        for name, mk in paths:
+            r = {}
+            for mode in ("eager", "host", "graph"):
+                r[mode] = {"pack": round(timed(mk(0), mode), 3), "unpack": round(timed(mk(1), mode), 3),
+                           "pair_per_op": round(timed(mk(2), mode), 3)}
+            res[name] = r
+        e = res["engine"]
+        # the bench line's keys: per-operation us of alternating pack/unpack pairs
+        res["back_to_back_us"] = e["eager"]["pair_per_op"]
+        res["graph_us"] = e["graph"]["pair_per_op"]
+        res["frac_back_to_back"] = round(2 * S / (e["eager"]["pair_per_op"] * 1e-6) / HBM_PEAK, 4)
+        res["frac_graph"] = round(2 * S / (e["graph"]["pair_per_op"] * 1e-6) / HBM_PEAK, 4)
+        out[k] = res
+        cv.set_stream(stream, True)
+        del pk, cv
+    del user
+    torch.cuda.empty_cache()
+    return out
+
+
 # ------------------------------------------------------------------ per-face throughput
 def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z"), flush="read"):
     """The north star's per-face figure: ONE face type of the 256^3
@@ -621,7 +745,11 @@ def main():
     local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # DDT_BENCH_PG=1 builds the process group (and runs the post-run RCCL gather) at world size 1
+    # too: a single-rank RCCL communicator on the one GPU executes the code the driver's 8-GPU
+    # run reaches (tests/test_gpu_rccl.py)
+    use_pg = world > 1 or os.environ.get("DDT_BENCH_PG") == "1"
+    if use_pg:
         # bind the RCCL communicator to this rank's GPU up front (no device guess in barrier())
         dist.init_process_group(backend=backend, **({"device_id": dev} if backend == "nccl" else {}))
 
@@ -780,7 +908,7 @@ def main():
     # whole packed stream on one device all-gathers the shards (backend "nccl" = RCCL over
     # xGMI); every rank checks that its slice of the gathered stream is its own shard.
     rccl = None
-    if world > 1 and not args.no_gather:
+    if use_pg and not args.no_gather:
         try:
             rccl = gather_check(packed, S, world, rank, dev, backend)
         except Exception as ex:   # the timed line stands on its own; report the failed check in it
@@ -858,6 +986,17 @@ def main():
         result["faces_unflushed"] = face_throughput(dev, args.face_fields, max(5, min(args.steps, 20)),
                                                     flush=None)
         result["faces_at_bench_fields"] = face_throughput(dev, count, max(5, min(args.steps, 20)))
+        # back-to-back operations between one event pair, eager and as a replayed graph: the
+        # per-operation cost without an event pair around every operation
+        for fields, key in ((count, "faces_at_bench_fields"), (1, "single_face_latency_us")):
+            if key not in result:
+                continue
+            bb = back_to_back(dev, fields)
+            result[key]["back_to_back"] = bb
+            for k in ("x", "y", "z"):
+                result[key].setdefault(k, {})
+                result[key][k]["back_to_back_us"] = bb[k]["back_to_back_us"]
+                result[key][k]["graph_us"] = bb[k]["graph_us"]
 
     if rank == 0 and base_sample is not None:
         srec, scount, what, host_user, gpu_prefix = base_sample
@@ -868,7 +1007,7 @@ def main():
     if rank == 0:
         sys.stdout.flush()
         os.write(result_fd, (json.dumps(result) + "\n").encode())
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

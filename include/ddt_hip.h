@@ -152,6 +152,12 @@ int ddt_type_get_true_extent(const ddt_datatype_t *type, ptrdiff_t *true_lb, ptr
 uint32_t ddt_type_flags(const ddt_datatype_t *type);
 /* out[0..7] = size, lb, ub, true_lb, true_ub, align, flags, nbElems */
 int ddt_type_info(const ddt_datatype_t *type, int64_t *out8);
+/* Committed metadata of opal_datatype_t (opal_datatype.h:172-212): out[0] = stack_depth (the
+ * deeper LOOP nesting of desc and opt_desc, opal_datatype_optimize.c:222-261, :1777), out[1] =
+ * bdt_used (predefined ids present, opal_datatype_add.c:163,175,306), out[2] = the optimizer's
+ * flags (OPAL_DATATYPE_OPTIMIZED_RESTRICTED), out[3] = 1 once committed.  What
+ * opt_desc_equiv.c:223-276 reads to recompute a corpus type's traits. */
+int ddt_type_commit_info(const ddt_datatype_t *type, int64_t *out4);
 
 /* Import a committed Open MPI description: `desc` is the opal_datatype_t::opt_desc
  * (or ::desc) array of `used` dt_elem_desc_t entries, 32 bytes each, layout of

@@ -9,6 +9,7 @@
 // DATA entry per block: 1 GiB of opt_desc for 64 M blocks).
 #pragma once
 
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <map>
@@ -169,7 +170,9 @@ struct Plan {
     bool captured = false;                            // a launch was enqueued inside a capture
     // address-ordered plan of a one-leaf single-element index list (ddt_sorted.hip):
     // 0 = not tried yet, 1 = built, -1 = not applicable
-    int sorted_state = 0;
+    // (atomic: the commit hook or a bridge import may build it on one thread while another
+    // thread's first move reads it)
+    std::atomic<int> sorted_state{0};
     std::unique_ptr<SortedList> sorted;
     ~Plan();
 };
@@ -184,6 +187,12 @@ struct ddt_datatype {
     int64_t true_lb = INT64_MAX, true_ub = INT64_MIN;
     int64_t align = 1;
     uint64_t nbElems = 0;
+    // opal_datatype_t::bdt_used (opal_datatype.h:175): one bit per predefined id the type map
+    // holds, LB / UB markers included (opal_datatype_add.c:163,175,306)
+    uint32_t bdt_used = 0;
+    // opal_datatype_t::stack_depth after commit: the deeper LOOP nesting of desc and opt_desc
+    // (opal_datatype_opt_update_stack_depth, opal_datatype_optimize.c:222-261, :1777)
+    uint32_t stack_depth = 0;
     std::vector<ddt::Node> desc;  // type map (uncommitted form)
     std::vector<ddt::Node> opt;   // committed + normalised form
     bool imported = false;        // desc is already a committed opt_desc (ddt_type_from_opal_desc)

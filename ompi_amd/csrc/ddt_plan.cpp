@@ -114,7 +114,17 @@ Plan::~Plan()
         sorted->take_blocks(blocks);
     std::vector<hipEvent_t> fences;
     bool unknown = false;
-    if (captured || !pool_fences(streams, fences, unknown)) {
+    // the fences are events of the plan's device (a destroy may run with another device
+    // current: an event of that device recorded on this device's streams would fail and mark the
+    // release unknown)
+    int cur = -1;
+    const bool other = device >= 0 && hipGetDevice(&cur) == hipSuccess && cur != device
+                       && hipSetDevice(device) == hipSuccess;
+    (void) hipGetLastError();
+    const bool fenced = !captured && pool_fences(streams, fences, unknown);
+    if (other)
+        (void) hipSetDevice(cur);
+    if (!fenced) {
         for (hipEvent_t e : fences)
             (void) hipEventDestroy(e);
         for (void *p : blocks)
@@ -457,16 +467,34 @@ int prebuild_device(ddt_datatype *t)
         if (P->device != dev)
             return DDT_SUCCESS;
     }
+    // The build allocates, uploads and waits for the private stream: calls a global-mode capture
+    // on ANOTHER thread forbids, and refusing them invalidates that capture
+    // (profiles/r3_probe_capture.log).  A commit or an import may run while some thread captures
+    // (the bridge imports at the first attach).  So: no build while the legacy stream
+    // captures or cannot be queried (it fails while a global capture is under way), and the
+    // build runs with this thread in relaxed capture mode, where those calls are this thread's
+    // own business (r5_probe_capture.log).  A skipped build happens at the first move instead.
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(nullptr, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+        (void) hipGetLastError();
+        return DDT_SUCCESS;
+    }
     hipStream_t bs = nullptr;
     if (private_stream(&bs) != hipSuccess)
         return DDT_ERR_HIP;
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    const bool swapped = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
+    (void) hipGetLastError();
+    int rc = DDT_SUCCESS;
     try {
         ensure_device_lists(*P);
         (void) sorted_build(*P, bs);
     } catch (const std::exception &) {
-        return DDT_ERR_OUT_OF_RESOURCE;
+        rc = DDT_ERR_OUT_OF_RESOURCE;
     }
-    return DDT_SUCCESS;
+    if (swapped)
+        (void) hipThreadExchangeStreamCaptureMode(&mode);
+    return rc;
 }
 
 // ------------------------------------------------------------------ items for one call

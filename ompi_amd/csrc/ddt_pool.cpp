@@ -82,15 +82,28 @@ void reap(Pool &P)   // P.mu held
 // that could take no fence (destroyed before the plan or convertor) are settled by one device
 // synchronisation, and the largest cached blocks go back to HIP until the cache is within
 // kCacheCap.
+// A device synchronisation settles only the current device's work, so only releases whose
+// blocks all live on `dev` settle here; another device's settle at its own next
+// hipMalloc.
+bool on_device(const Pool &P, const Pending &r, int dev)   // P.mu held
+{
+    for (void *p : r.blocks) {
+        auto it = P.blocks.find(p);
+        if (it == P.blocks.end() || it->second.device != dev)
+            return false;
+    }
+    return true;
+}
+
 void settle_and_cap(Pool &P, int dev)   // P.mu held
 {
     bool unknown = false;
     for (const Pending &r : P.pending)
-        unknown |= r.unknown;
+        unknown |= r.unknown && on_device(P, r, dev);
     if (unknown && hipDeviceSynchronize() == hipSuccess) {
         for (size_t i = 0; i < P.pending.size();) {
             Pending &r = P.pending[i];
-            if (!r.unknown) {
+            if (!r.unknown || !on_device(P, r, dev)) {
                 ++i;
                 continue;
             }

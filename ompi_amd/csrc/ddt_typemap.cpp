@@ -38,6 +38,7 @@ void init_predefined()
         t.align = 0;
         t.nbElems = 1;
         t.flags = F_PREDEFINED;
+        t.bdt_used = 1u << id;   // OPAL_DATATYPE_INIT_BASIC_TYPE (opal_datatype_constructors.h:77-85)
     }
     for (int id = 4; id <= 27; ++id) {
         ddt_datatype &t = g_predef[id];
@@ -49,6 +50,7 @@ void init_predefined()
         t.true_ub = kSize[id];
         t.align = kAlign[id];
         t.nbElems = 1;
+        t.bdt_used = 1u << id;   // OPAL_DATATYPE_INIT_BASIC_DATATYPE (:87-96)
         t.flags = F_PREDEFINED | F_CONTIGUOUS | F_NO_GAPS | F_DATA | F_COMMITTED;
         Node n;
         n.kind = Node::DATA;
@@ -103,6 +105,7 @@ AddState add_bounds(ddt_datatype *base, const ddt_datatype *add, uint64_t count,
     if (add->id == 2 || add->id == 3) {
         // the LB / UB markers (:158-186): move the bound to disp, nothing is appended; the id
         // survives a dup (opal_datatype_clone.c:74), so a duplicated marker is one too
+        base->bdt_used |= 1u << add->id;   // (:163, :175)
         if (add->id == 2) {
             base->lb = (base->flags & F_USER_LB) ? std::min(base->lb, disp) : disp;
             base->flags |= F_USER_LB;
@@ -162,6 +165,7 @@ AddState add_bounds(ddt_datatype *base, const ddt_datatype *add, uint64_t count,
     if (add->size == 0)
         return st;
     base->size += int64_t(count) * add->size;
+    base->bdt_used |= add->bdt_used;   // (:306)
     st.old_true_ub = (base->nbElems == 0) ? disp : base->true_ub;
     base->true_lb = std::min(true_lb, base->true_lb);
     base->true_ub = std::max(true_ub, base->true_ub);
@@ -284,6 +288,7 @@ ddt_datatype *clone_type(const ddt_datatype *o)
     t->true_ub = o->true_ub;
     t->align = o->align;
     t->nbElems = o->nbElems;
+    t->bdt_used = o->bdt_used;
     t->desc = o->desc;
     return t;
 }
@@ -586,17 +591,44 @@ bool opt_desc_of(const ddt_datatype *t, DescForm &out)
 // fragments and send positions stop on the reference's opt_desc elements.  An imported
 // description already is an opt_desc; a type map whose description the 32-byte form cannot hold
 // (a count beyond 32 bits) keeps its own elements.
+// opal_datatype_opt_loop_nesting_depth (opal_datatype_optimize.c:222-241): the deepest LOOP
+// nesting of a description; sibling loops do not add depth
+uint32_t loop_depth(const DescForm &d)
+{
+    uint32_t depth = 0, mx = 0;
+    for (size_t i = 0; i < d.used; ++i) {
+        if (d.e[i].type == kDescLoop)
+            mx = std::max(mx, ++depth);
+        else if (d.e[i].type == kDescEndLoop && depth > 0)
+            --depth;
+    }
+    return mx;
+}
+
+// the same on the tree (an imported opt_desc, or a type map the 32-byte form cannot hold)
+uint32_t loop_depth(const std::vector<Node> &nodes)
+{
+    uint32_t mx = 0;
+    for (const Node &n : nodes)
+        if (n.kind == Node::LOOP)
+            mx = std::max(mx, 1 + loop_depth(n.body));
+    return mx;
+}
+
 int commit(ddt_datatype *t)
 {
     if (t->flags & F_COMMITTED)
         return DDT_SUCCESS;
     bool optimized = false;
+    t->stack_depth = loop_depth(t->desc);
     if (!t->imported) {
         DescForm in, out;
         std::vector<Node> nodes;
         if (build_opal_desc(t->desc, t->size, in)) {
             uint32_t flags = 0;
             optimize_desc(in, t->size, out, &flags);
+            // opal_datatype_opt_update_stack_depth (:248-261): max over desc and opt_desc
+            t->stack_depth = std::max(loop_depth(in), loop_depth(out));
             if (nodes_from_desc(out, nodes)) {
                 t->opt = std::move(nodes);
                 t->opt_flags = flags;
@@ -1245,6 +1277,17 @@ int ddt_get_elements(const ddt_datatype_t *t, size_t ucount, size_t *count)
     return DDT_SUCCESS;
 }
 
+int ddt_type_commit_info(const ddt_datatype_t *t, int64_t *o)
+{
+    if (!t || !o)
+        return DDT_ERR_BAD_PARAM;
+    o[0] = int64_t(t->stack_depth);
+    o[1] = int64_t(t->bdt_used);
+    o[2] = int64_t(t->opt_flags);
+    o[3] = (t->flags & F_COMMITTED) ? 1 : 0;
+    return DDT_SUCCESS;
+}
+
 int ddt_type_info(const ddt_datatype_t *t, int64_t *o)
 {
     if (!t || !o)
@@ -1336,6 +1379,10 @@ struct Fold {
     void flush(std::vector<Node> &out)
     {
         if (L) {
+            // the reservation assumed the run continues to the level's end; a run that ended
+            // early hands the unused part back (other entries after a short run)
+            if (L->disp.capacity() > L->disp.size() + L->disp.size() / 4)
+                L->disp.shrink_to_fit();
             if (uni) {
                 L->ulen = ulen;
                 L->len.clear();
@@ -1578,6 +1625,17 @@ int64_t ddt_type_to_opal_opt_desc(const ddt_datatype_t *t, void *out, size_t cap
     return int64_t(used);
 }
 
+namespace {
+// bdt_used of an imported description: its DATA entries' predefined ids
+uint32_t bdt_of(const std::vector<Node> &nodes)
+{
+    uint32_t m = 0;
+    for (const Node &n : nodes)
+        m |= n.kind == Node::LOOP ? bdt_of(n.body) : (n.tid ? 1u << n.tid : 0u);
+    return m;
+}
+}  // namespace
+
 int ddt_type_from_opal_desc(const void *desc, size_t used, size_t size, ptrdiff_t lb, ptrdiff_t ub,
                             ptrdiff_t true_lb, ptrdiff_t true_ub, ddt_datatype_t **out)
 {
@@ -1596,6 +1654,7 @@ int ddt_type_from_opal_desc(const void *desc, size_t used, size_t size, ptrdiff_
     t->flags = F_DATA;
     t->nbElems = 0;
     t->imported = true;
+    t->bdt_used = bdt_of(t->desc);
     uint64_t s = 0;
     for (const Node &n : t->desc)
         s += n.packed_bytes();

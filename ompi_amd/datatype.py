@@ -71,6 +71,13 @@ class Datatype:
         keys = ("size", "lb", "ub", "true_lb", "true_ub", "align", "flags", "nbElems")
         return dict(zip(keys, list(out)))
 
+    def commit_info(self) -> dict:
+        """opal_datatype_t's committed stack_depth and bdt_used (opal_datatype.h:175-187), the
+        optimizer flags and whether the type is committed (ddt_type_commit_info)."""
+        out = (ctypes.c_int64 * 4)()
+        check(lib().ddt_type_commit_info(self.handle, out), "ddt_type_commit_info")
+        return dict(zip(("stack_depth", "bdt_used", "opt_flags", "committed"), list(out)))
+
     @property
     def size(self) -> int:
         return self.info()["size"]

@@ -74,6 +74,7 @@ typedef struct ort_type {
     int64_t size, lb, ub, true_lb, true_ub;
     int64_t align;
     int64_t nbElems;
+    uint32_t bdt_used; /* opal_datatype_t::bdt_used (opal_datatype.h:175) */
     ort_run *runs;
     int64_t nruns, cap;
     int64_t *pref; /* packed offset of each run (built lazily at first pack) */
@@ -188,6 +189,7 @@ ort_type *ort_basic(int id)
         m->align = 0;
         m->nbElems = 1;
         m->flags = ORT_FLAG_PREDEFINED;
+        m->bdt_used = 1u << id; /* OPAL_DATATYPE_INIT_BASIC_TYPE (:77-85) */
         return m;
     }
     if (id < 4 || id > 27 || ort_basic_size[id] == 0)
@@ -201,6 +203,7 @@ ort_type *ort_basic(int id)
     t->true_ub = t->size;
     t->align = ort_basic_align[id];
     t->nbElems = 1;
+    t->bdt_used = 1u << id; /* OPAL_DATATYPE_INIT_BASIC_DATATYPE (:87-96) */
     t->flags = ORT_FLAG_PREDEFINED | ORT_FLAG_CONTIGUOUS | ORT_FLAG_NO_GAPS | ORT_FLAG_DATA;
     ort_push_run(t, 0, t->size, t->size, id);
     /* desc[0] of a predefined type (opal_datatype_module.c:418-426) */
@@ -345,6 +348,7 @@ static void ort_add(ort_type *base, const ort_type *add, int64_t count, int64_t 
     if (extent == -1)
         extent = add->ub - add->lb;
     if (add->id == 2) {   /* OPAL_DATATYPE_LB (:161-172) */
+        base->bdt_used |= 1u << 2;
         base->lb = (base->flags & ORT_FLAG_USER_LB) ? lmin(base->lb, disp) : disp;
         base->flags |= ORT_FLAG_USER_LB;
         if ((int64_t) ((uint64_t) base->ub - (uint64_t) base->lb) != base->size)
@@ -352,6 +356,7 @@ static void ort_add(ort_type *base, const ort_type *add, int64_t count, int64_t 
         return;
     }
     if (add->id == 3) {   /* OPAL_DATATYPE_UB (:173-184) */
+        base->bdt_used |= 1u << 3;
         base->ub = (base->flags & ORT_FLAG_USER_UB) ? lmax(base->ub, disp) : disp;
         base->flags |= ORT_FLAG_USER_UB;
         if ((int64_t) ((uint64_t) base->ub - (uint64_t) base->lb) != base->size)
@@ -407,6 +412,7 @@ static void ort_add(ort_type *base, const ort_type *add, int64_t count, int64_t 
     old_true_ub = (0 == base->nbElems) ? disp : base->true_ub;
     base->true_lb = lmin(true_lb, base->true_lb);
     base->true_ub = lmax(true_ub, base->true_ub);
+    base->bdt_used |= add->bdt_used; /* (:306) */
     if (!(add->flags & ORT_FLAG_PREDEFINED)) {
         base->flags |= (add->flags & ORT_FLAG_USER_LB);
         base->flags |= (add->flags & ORT_FLAG_USER_UB);
@@ -1404,6 +1410,18 @@ void ort_commit(ort_type *t)
         acc += t->oruns[r].len;
     }
     t->opref[t->noruns] = acc;
+}
+
+/* The committed metadata opt_desc_equiv.c:223-276 reads: out[0] = stack_depth, the deeper LOOP
+ * nesting of desc and opt_desc (opal_datatype_opt_update_stack_depth, :248-261, set at :1777);
+ * out[1] = bdt_used; out[2] = desc.used; out[3] = opt_desc.used. */
+void ort_commit_info(ort_type *t, int64_t *out)
+{
+    ort_commit(t);
+    out[0] = lmax(ox_depth(&t->desc), ox_depth(&t->opt));
+    out[1] = t->bdt_used;
+    out[2] = t->desc.used;
+    out[3] = t->opt.used;
 }
 
 /* opt_desc entry i (i == used: the END_LOOP sentinel): flags, type, count|items, loops,

@@ -3,7 +3,9 @@
 // without invalidating that capture?  Round 3: grounds the engine's non-blocking datatype
 // destruction (ddt_pool.cpp).  For each call: thread B begins a global-mode capture and
 // enqueues a kernel, thread A makes the call, then B enqueues another kernel and ends the
-// capture.  Prints A's return code and B's end-capture result.  Not part of the product.
+// capture.  Prints A's return code and B's end-capture result.  Round 5: the same calls again
+// with thread A switched to hipStreamCaptureModeRelaxed (hipThreadExchangeStreamCaptureMode),
+// the mode the engine's attach-time table build runs under.  Not part of the product.
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>
@@ -64,6 +66,7 @@ int main()
         {"hipFree", [] { void *p = nullptr; (void) hipMalloc(&p, 1 << 20); return hipFree(p); }},
         {"hipDeviceSynchronize", [] { return hipDeviceSynchronize(); }},
     };
+    for (int relaxed = 0; relaxed < 2; ++relaxed)
     for (Case &c : cases) {
         Gate g;
         hipError_t ra = hipSuccess, rb = hipSuccess, rl = hipSuccess;
@@ -81,13 +84,18 @@ int main()
         });
         std::thread a([&] {
             g.wait(1);
+            hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+            if (relaxed)
+                (void) hipThreadExchangeStreamCaptureMode(&mode);
             ra = c.call();
+            if (relaxed)
+                (void) hipThreadExchangeStreamCaptureMode(&mode);
             (void) hipGetLastError();
             g.set(2);
         });
         a.join();
         b.join();
-        printf("%-32s A: %-36s  B's capture: %s%s\n", c.name, hipGetErrorName(ra), hipGetErrorName(rb),
+        printf("%s%-32s A: %-36s  B's capture: %s%s\n", relaxed ? "[A relaxed] " : "", c.name, hipGetErrorName(ra), hipGetErrorName(rb),
                rl != hipSuccess ? " (launch after the call failed)" : "");
         if (graph)
             (void) hipGraphDestroy(graph);

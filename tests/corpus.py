@@ -397,6 +397,23 @@ def contig():
     return B(INT), lambda count: [(0, 4 * count)]
 
 
+# The receive types of the three PAIR entries (datatype_corpus.c:626-789): the same packed stream
+# into dense storage (lammps: a struct of contiguous runs at the send type's field offsets;
+# specfem3d_mt: one contiguous run of floats).
+def _lammps_recv(D, N, nfields):
+    offs = [0] + [3 * D * 8 + k * D * 8 for k in range(nfields - 1)]
+    ext = offs[-1] + D * 8
+    types = [("contig", 3 * N, B(DOUBLE))] + [("contig", N, B(DOUBLE))] * (nfields - 1)
+    return ("resized", ("struct", [1] * nfields, offs, types), 0, ext)
+
+
+PAIR_RECV = {
+    "ddtbench_lammps_full": _lammps_recv(LAMMPS_FULL_DIM, LAMMPS_FULL_ICOUNT, 6),        # :662-672
+    "ddtbench_lammps_atomic": _lammps_recv(LAMMPS_ATOMIC_DIM, LAMMPS_ATOMIC_ICOUNT, 4),  # :712-722
+    "ddtbench_specfem3d_mt": ("contig", SPEC_MT[2] * SPEC_MT[0], B(FLOAT)),              # :786-788
+}
+
+
 CORPUS = {
     "contig": contig,
     "indexed_gap": indexed_gap,

@@ -57,6 +57,7 @@ def lib():
             "ort_opt_used": (i64, [vp]), "ort_opt_at": (None, [vp, i64, vp]),
             "ort_opt_flags": (ctypes.c_uint32, [vp]),
             "ort_desc_used": (i64, [vp]), "ort_desc_at": (None, [vp, i64, vp]),
+            "ort_commit_info": (None, [vp, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -126,6 +127,13 @@ class OType:
             lib().ort_opt_at(self.h, i, out)
             res.append(tuple(out))
         return res
+
+    def commit_info(self) -> dict:
+        """stack_depth / bdt_used after commit (opal_datatype_optimize.c:1777,
+        opal_datatype_add.c:306) and the two descriptions' lengths."""
+        out = (ctypes.c_int64 * 4)()
+        lib().ort_commit_info(self.h, out)
+        return dict(zip(("stack_depth", "bdt_used", "desc_used", "opt_used"), list(out)))
 
     def restricted(self) -> bool:
         """OPAL_DATATYPE_OPTIMIZED_RESTRICTED after commit (a mixed-type region was re-typed)."""

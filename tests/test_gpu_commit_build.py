@@ -106,3 +106,58 @@ def test_bridge_import_builds_the_tables(device, disps, hook):
     np.testing.assert_array_equal(packed.cpu().numpy(), _want(user.cpu().numpy(), disps))
     assert host_s < 1e-3, f"first asynchronous bridge pack took {host_s * 1e3:.2f} ms of host time"
     ot.destruct()
+
+
+@pytest.mark.parametrize("mode", ["global", "relaxed"])
+def test_commit_during_foreign_capture(device, disps, mode):
+    """a commit (or the bridge's first-attach import) of a table-building type while
+    ANOTHER thread captures a graph (`mode` capture).  The table build allocates and waits on the
+    library's private stream; it runs with the committing thread in relaxed capture mode and is
+    skipped while the legacy stream reports a capture, so the foreign capture must end intact and
+    its graph replay correctly; the type then packs bit-exactly (tables built now or at first
+    move)."""
+    import threading
+    import torch
+    import ompi_amd
+    from ompi_amd import datatype as D
+    x = torch.zeros(1024, device=device)
+    sb = torch.cuda.Stream(device)
+    g = torch.cuda.CUDAGraph()
+    started, committed = threading.Event(), threading.Event()
+    errors, types = [], []
+
+    def capture():
+        try:
+            with torch.cuda.graph(g, stream=sb, capture_error_mode=mode):
+                x.add_(1)
+                started.set()
+                committed.wait(120)
+                x.add_(1)
+        except Exception as ex:   # noqa: BLE001 -- reported below
+            errors.append(repr(ex))
+            started.set()
+
+    def commit():
+        try:
+            started.wait(60)
+            t = D.create_indexed_block(1, disps, D.predefined(15)).commit()
+            types.append(t)
+        except Exception as ex:   # noqa: BLE001
+            errors.append(repr(ex))
+        finally:
+            committed.set()
+
+    tb, ta = threading.Thread(target=capture), threading.Thread(target=commit)
+    tb.start()
+    ta.start()
+    ta.join(180)
+    tb.join(180)
+    assert not errors, errors
+    g.replay()
+    torch.cuda.synchronize()
+    assert float(x[0].item()) == 2.0
+    user = torch.randint(1, 255, (SPAN_FLOATS * 4,), dtype=torch.uint8, device=device)
+    packed = torch.zeros(N * 4, dtype=torch.uint8, device=device)
+    assert ompi_amd.pack(user.data_ptr(), 1, types[0], packed, N * 4, 0) == N * 4
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(packed.cpu().numpy(), _want(user.cpu().numpy(), disps))

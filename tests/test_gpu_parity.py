@@ -394,6 +394,10 @@ def test_corpus_on_gpu(device, name):
     host = R.fill(span, 0x5A)
     user = _dev(host, device)
     e = b.engine()
+    # the type packed here carries the reference's trait tags (opt_desc_equiv.c:223-290)
+    from .test_cpu_traits import TRAITS, observed
+    ec = e.commit_info()
+    assert observed(e.info(), ec["stack_depth"], ec["bdt_used"], name in _corpus.PAIR_RECV) == TRAITS[name]
     packed = torch.zeros(size, dtype=torch.uint8, device=device)
     assert ompi_amd.pack(user.data_ptr() + origin, count, e, packed, size, 0) == size
     assert _hashlib.sha256(_host(packed).tobytes()).hexdigest() == g["sha256"]
