@@ -14,8 +14,10 @@
 //                               lowers the copy-range count (:406-435), growth <= 10x
 //   promoted_type (:581-611)    carrier of a mixed region: widest UINT8/4/2 that tiles it and
 //                               is aligned at disp (and extent when count > 1), else UINT1
-// with the run-time defaults of opal_datatype_module.c:85-88 (max_desc_growth 10, unroll 8 items
-// of <= 128 bytes, preserve_type on).  COUNT_OPTIMIZABLE (:385-401) is a hint no mover reads and
+// with the reference's run-time parameters (opal_datatype_module.c:85-90, registered :347-383),
+// read at commit: defaults max_desc_growth 10, unroll 8 items of <= 128 bytes, preserve_type on;
+// set by ddt_tune("opt_growth" / "opt_unroll_items" / "opt_unroll_bytes" / "opt_preserve") or
+// their MCA environment form OMPI_MCA_opal_datatype_optimize_*.  COUNT_OPTIMIZABLE (:385-401) is a hint no mover reads and
 // is not computed.
 //
 // Sealed lists (engine extension): an index list of more than kSealBlocks blocks (64 Mi for
@@ -29,6 +31,7 @@
 // take those paths); a loop-boundary fusion with the list as the body's first or last item takes
 // its first or last block and splits the range around it, as the reference's separate entries.
 #include "ddt_optimize.h"
+#include "ddt_plan.h"
 
 #include <algorithm>
 #include <cstring>
@@ -42,9 +45,10 @@ constexpr uint32_t kData = F_DATA;
 constexpr uint32_t kContig = F_CONTIGUOUS;
 constexpr uint32_t kElemMask = 0x01FFu;                                  // OPAL_DATATYPE_FLAG_ELEM_MASK
 constexpr uint32_t kBasic = F_PREDEFINED | F_CONTIGUOUS | F_NO_GAPS | F_DATA | F_COMMITTED;
-constexpr uint64_t kUnrollItems = 8, kUnrollBytes = 128;
 constexpr uint64_t kInlineBlocklen = 8;   // OPAL_DATATYPE_PREDEFINED_MAX_INLINE_BLOCKLEN
-constexpr int64_t kGrowth = 10;
+// opal_datatype_config.optimize (opal_datatype_module.c:85-90), read at commit (ddt_plan.h Tuning)
+inline uint64_t unroll_items() { return uint64_t(tuning().opt_unroll_items); }
+inline uint64_t unroll_bytes() { return uint64_t(tuning().opt_unroll_bytes); }
 constexpr uint16_t kNoType = 0xFFFF;
 
 inline int64_t esz(uint16_t t) { return kOpalSize[t]; }
@@ -268,8 +272,10 @@ void collapse(DescEntry &e)
 // opal_datatype_opt_promoted_type + set_mixed_region (:581-630)
 void mixed_region(DescEntry &e, int64_t bytes, uint32_t count, int64_t disp, int64_t extent)
 {
-    uint16_t type = 9;   // UINT1
+    uint16_t type = 9;   // UINT1 (always when preserve_type is off, :586-588)
     for (uint16_t c : {uint16_t(12), uint16_t(11), uint16_t(10)}) {   // UINT8, UINT4, UINT2
+        if (!tuning().opt_preserve)
+            break;
         const uint64_t sz = uint64_t(esz(c)), al = uint64_t(kOpalAlign[c]);
         if (uint64_t(bytes) % sz || (uint64_t(disp) & (al - 1)) || (count > 1 && (uint64_t(extent) & (al - 1))))
             continue;
@@ -291,17 +297,17 @@ uint32_t Pass::unroll_factor(size_t pos) const   // :72-110
     if (L.loops < 4 || L.count < 2 || (L.flags & kContig) || E.type != kDescEndLoop || is_data(E))
         return 1;
     const uint32_t body = L.count - 1;
-    if (kUnrollItems < body)
+    if (unroll_items() < body)
         return 1;
     for (uint32_t k = 0; k < body; ++k) {
         const DescEntry &e = d_[pos + k + 1];
         if (!is_data(e) || e.sealed >= 0)
             return 1;
         const uint64_t ts = uint64_t(esz(e.type));
-        if (!ts || !e.blen || e.blen > kUnrollBytes / ts || e.count > kUnrollBytes / (e.blen * ts))
+        if (!ts || !e.blen || e.blen > unroll_bytes() / ts || e.count > unroll_bytes() / (e.blen * ts))
             return 1;
     }
-    const uint32_t f = std::min<uint32_t>(uint32_t(kUnrollItems / body), L.loops / 2);
+    const uint32_t f = std::min<uint32_t>(uint32_t(std::min<uint64_t>(unroll_items() / body, UINT32_MAX)), L.loops / 2);
     return f > 1 ? f : 1;
 }
 
@@ -781,7 +787,8 @@ uint64_t ranges(const std::vector<DescEntry> &d, const std::vector<std::shared_p
 void optimize_desc(const DescForm &in, int64_t size, DescForm &out, uint32_t *flags)
 {
     // opal_datatype_optimize_short_restart (:1347-1478) from opal_datatype_commit (:1765-1777)
-    const int64_t limit = int64_t(in.used) * kGrowth;
+    const int64_t growth = tuning().opt_growth;   // clamped to 1024 (opal_datatype_module.c:370-372)
+    const int64_t limit = int64_t(in.used) * growth;
     const uint32_t init = *flags;
     // The growth cap counts entries as the reference holds them: a sealed list is nblk entries in
     // `desc` and its optimized entries (sealed_opt_entries) after a pass.  In sealed-as-one units a
@@ -812,7 +819,7 @@ void optimize_desc(const DescForm &in, int64_t size, DescForm &out, uint32_t *fl
             }
             extra += it->second - 1;
         }
-        return int64_t(f.used) + extra > (int64_t(in.used) + in_extra) * kGrowth;
+        return int64_t(f.used) + extra > (int64_t(in.used) + in_extra) * growth;
     };
     auto short_pass = [&](const std::vector<DescEntry> &src, DescForm &dst, bool boundary, bool *expanded,
                           bool *reevaluate) {

@@ -34,6 +34,25 @@ Tuning &tuning()
             v.wt = std::atoi(e);
         if (const char *e = std::getenv("DDT_XCD"))
             v.xcd = std::atoi(e) < 0 ? -1 : (std::atoi(e) ? 1 : 0);
+        // the reference's MCA variables in their environment form (mca_base_var: OMPI_MCA_<name>)
+        const char *pre = "OMPI_MCA_opal_datatype_optimize_";
+        auto mca = [&](const char *name, long &dst) {
+            if (const char *e = std::getenv((std::string(pre) + name).c_str()))
+                dst = std::atol(e);
+        };
+        long preserve = v.opt_preserve;
+        mca("max_desc_growth", v.opt_growth);
+        mca("loop_unroll_max_items", v.opt_unroll_items);
+        mca("loop_unroll_max_data_bytes", v.opt_unroll_bytes);
+        if (const char *e = std::getenv("OMPI_MCA_opal_datatype_optimize_preserve_type")) {
+            // an MCA bool: 0/1, true/false, yes/no
+            const std::string b(e);
+            preserve = (b == "0" || b == "false" || b == "no" || b == "f" || b == "n") ? 0 : 1;
+        }
+        v.opt_preserve = int(preserve);
+        v.opt_growth = std::clamp<long>(v.opt_growth, 0, 1024);
+        v.opt_unroll_items = std::max<long>(v.opt_unroll_items, 0);
+        v.opt_unroll_bytes = std::max<long>(v.opt_unroll_bytes, 0);
         return v;
     }();
     return t;

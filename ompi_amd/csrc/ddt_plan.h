@@ -48,6 +48,14 @@ struct Tuning {
                           // CU (read at plan build)
     int sorted_commit = 1;   // build the address-ordered tables at commit / bridge import (1) or
                              // at the first whole-message move (0)
+    // The commit optimizer's run-time parameters, read at commit like the reference's MCA
+    // variables opal_datatype_optimize_{max_desc_growth, loop_unroll_max_items,
+    // loop_unroll_max_data_bytes, preserve_type} (opal_datatype_module.c:85-90, :347-383); their
+    // environment form OMPI_MCA_opal_datatype_optimize_* sets the initial values
+    long opt_growth = 10;         // clamped to 1024 (OPAL_DATATYPE_OPTIMIZE_MAX_DESC_GROWTH_CAP)
+    long opt_unroll_items = 8;
+    long opt_unroll_bytes = 128;
+    int opt_preserve = 1;         // 0: fused mixed-type regions travel as UINT1 (:586-588)
 };
 Tuning &tuning();
 // Synchronous host -> device copy on a library-private stream (capture-safe).

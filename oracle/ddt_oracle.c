@@ -812,9 +812,25 @@ void ort_run_at(const ort_type *t, int64_t i, int64_t *out)
  * (opal_datatype_position.c:167-367 walks opt_desc): a fused mixed-type region is re-typed to
  * the widest UINT8/4/2 carrier that tiles it, or UINT1.
  * ===================================================================================== */
-#define OX_UNROLL_ITEMS 8u
-#define OX_UNROLL_BYTES 128u
-#define OX_GROWTH 10
+/* opal_datatype_config.optimize (opal_datatype_module.c:85-90): the MCA variables
+ * opal_datatype_optimize_{max_desc_growth, loop_unroll_max_items, loop_unroll_max_data_bytes,
+ * preserve_type}, defaults 10 / 8 / 128 / true, set by ort_optimize_config before a commit. */
+static uint64_t ox_unroll_items = 8, ox_unroll_bytes = 128;
+static int64_t ox_growth = 10;
+static int ox_preserve = 1;
+
+void ort_optimize_config(int64_t growth, int64_t unroll_items, int64_t unroll_bytes, int preserve_type)
+{
+    /* max_desc_growth is clamped to OPAL_DATATYPE_OPTIMIZE_MAX_DESC_GROWTH_CAP = 1024
+     * (opal_datatype_module.c:370-372, opal_datatype_internal.h:385) */
+    ox_growth = growth < 0 ? 0 : (growth > 1024 ? 1024 : growth);
+    ox_unroll_items = unroll_items < 0 ? 0 : (uint64_t) unroll_items;
+    ox_unroll_bytes = unroll_bytes < 0 ? 0 : (uint64_t) unroll_bytes;
+    ox_preserve = preserve_type != 0;
+}
+#define OX_UNROLL_ITEMS ox_unroll_items
+#define OX_UNROLL_BYTES ox_unroll_bytes
+#define OX_GROWTH ox_growth
 #define OX_INLINE_BLOCKLEN 8u   /* OPAL_DATATYPE_PREDEFINED_MAX_INLINE_BLOCKLEN (_internal.h:103) */
 #define OX_UNAVAILABLE 0xFFFFu
 
@@ -861,7 +877,8 @@ static uint32_t ox_unroll_factor(const ort_elem *d, int64_t pos)
         if (e->count > OX_UNROLL_BYTES / (e->blocklen * ts))
             return 1;
     }
-    uint32_t f = OX_UNROLL_ITEMS / body, lf = L->loops / 2;
+    uint64_t fw = OX_UNROLL_ITEMS / body;
+    uint32_t f = fw > UINT32_MAX ? UINT32_MAX : (uint32_t) fw, lf = L->loops / 2;
     f = f < lf ? f : lf;
     return f > 1 ? f : 1;
 }
@@ -911,6 +928,8 @@ static void ox_collapse(ort_elem *e)
 static uint16_t ox_carrier(int64_t disp, int64_t extent, uint32_t count, int64_t bytes)
 {
     static const uint16_t cand[3] = {12, 11, 10};
+    if (!ox_preserve) /* (:586-588) */
+        return 9;
     for (int k = 0; k < 3; k++) {
         const uint64_t sz = (uint64_t) ort_basic_size[cand[k]], al = (uint64_t) ort_basic_align[cand[k]];
         if ((uint64_t) bytes % sz)

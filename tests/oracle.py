@@ -58,6 +58,7 @@ def lib():
             "ort_opt_flags": (ctypes.c_uint32, [vp]),
             "ort_desc_used": (i64, [vp]), "ort_desc_at": (None, [vp, i64, vp]),
             "ort_commit_info": (None, [vp, vp]),
+            "ort_optimize_config": (None, [i64, i64, i64, i]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -272,3 +273,9 @@ def resized(old, lb, extent):
 
 def dup(old):
     return OType(lib().ort_dup(old.h))
+
+
+def optimize_config(growth: int = 10, unroll_items: int = 8, unroll_bytes: int = 128,
+                    preserve_type: bool = True) -> None:
+    """The optimizer's MCA parameters for later commits (opal_datatype_module.c:85-90)."""
+    lib().ort_optimize_config(growth, unroll_items, unroll_bytes, int(bool(preserve_type)))

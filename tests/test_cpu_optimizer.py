@@ -214,6 +214,81 @@ def test_engine_and_oracle_optimizers_agree(kind, seed):
         assert restricted > 150
 
 
+# the reference's optimizer MCA variables (opal_datatype_module.c:85-90, :347-383) away from
+# their defaults: (max_desc_growth, loop_unroll_max_items, loop_unroll_max_data_bytes, preserve_type)
+NONDEFAULT = {
+    "no_preserve": (10, 8, 128, False),        # every fused mixed region a UINT1 carrier (:586-588)
+    "unroll_2x32": (10, 2, 32, True),
+    "unroll_32x1024": (10, 32, 1024, True),
+    "growth_1": (1, 8, 128, True),
+    "growth_0_no_unroll": (0, 0, 0, True),
+}
+
+
+def _configure(growth, items, nbytes, preserve):
+    from ompi_amd._lib import lib
+    O.optimize_config(growth, items, nbytes, preserve)
+    for k, v in (("opt_growth", growth), ("opt_unroll_items", items), ("opt_unroll_bytes", nbytes),
+                 ("opt_preserve", int(preserve))):
+        assert lib().ddt_tune(k.encode(), v) == 0
+
+
+@pytest.mark.parametrize("name", sorted(NONDEFAULT))
+def test_optimizers_agree_under_nondefault_parameters(name):
+    """The 2,500-recipe agreement (desc, opt_desc, RESTRICTED, engine == oracle) under the
+    reference's optimizer parameters set away from their defaults, through the engine's ABI
+    (ddt_tune opt_*) and the oracle's ort_optimize_config: 500 recipes each, half mixed-type."""
+    growth, items, nbytes, preserve = NONDEFAULT[name]
+    rng = random.Random(4700 + sorted(NONDEFAULT).index(name))
+    _configure(growth, items, nbytes, preserve)
+    n = wide = 0
+    try:
+        for i in range(500):
+            rec = R.random_mixed_recipe(rng) if i % 2 else R.random_recipe(rng)
+            b = R.Built(rec)
+            if b.o.info()["size"] == 0:
+                continue
+            e = b.engine()
+            oo = b.o.opt_desc()
+            raw, fl = e.to_opal_opt_desc()
+            eo = S.unpack_entries(raw)
+            assert S.unpack_entries(e.to_opal_desc()) == b.o.desc(), rec
+            assert eo == oo, (name, rec)
+            assert bool(fl & 0x10000) == b.o.restricted(), rec
+            if len(oo) < 4000:
+                assert _flatten(oo) == _flatten(b.o.desc()), rec
+            changed = [x for x in oo if x[0] & CHANGED]
+            if not preserve:
+                assert all(x[1] == UINT1 for x in changed), rec
+            wide += any(x[1] in (10, 11, 12) for x in changed)
+            n += 1
+    finally:
+        _configure(10, 8, 128, True)
+    assert n > 300
+    if not preserve:
+        assert wide == 0
+    # the defaults are back: struct{double,int[3]} is UINT4 x 5 again (SURVEY App. A)
+    o, eng, _, _ = _both(("struct", [1, 3], [0, 8], [("basic", FLOAT8), ("basic", INT4)]))
+    assert [_data(x) for x in eng] == [(UINT4, 1, 5, 20, 0)] and o == eng
+
+
+def test_preserve_type_off_makes_byte_carriers_and_positions():
+    """preserve_type = false (MCA opal_datatype_optimize_preserve_type): struct{double,int[3]}
+    commits as UINT1 x 20 in both restatements, so a send position may stop on any byte of it
+    (position.c's 113-byte fragments are no longer snapped to 112)."""
+    st = ("struct", [1, 3], [0, 8], [("basic", FLOAT8), ("basic", INT4)])
+    _configure(10, 8, 128, False)
+    try:
+        o, e, ro, re_ = _both(st)
+        assert [_data(x) for x in e] == [(UINT1, 1, 20, 20, 0)] and o == e and ro and re_
+        b = R.Built(st)
+        eng = b.engine()
+        for p in (1, 7, 13, 39):
+            assert eng.snap_position(p) == p == b.o.set_position(3, p, send=True)
+    finally:
+        _configure(10, 8, 128, True)
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_engine_snap_follows_carriers_on_mixed_types(seed):
     """Send positions on mixed-type recipes: the engine's snap (its committed opt_desc) ==
