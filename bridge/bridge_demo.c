@@ -3,7 +3,7 @@
  * convertor: an opal_datatype_t with a committed opt_desc, an opal_convertor_t prepared as
  * OPAL_CONVERTOR_PREPARE + opal_convertor_prepare_for_{send,recv} leave it
  * (opal_convertor.c:526-696), the movers swapped by opal_hip_bridge_attach() (the
- * pack_description_sweep.c:896-965 precedent), then opal_convertor_pack/unpack's call into
+ * pack_description_sweep.c:877-965 precedent), then opal_convertor_pack/unpack's call into
  * conv->fAdvance (:255-349) in BTL-sized fragments, with opal_convertor_set_position
  * (opal_convertor.h:357-394) for out-of-order receives.
  *

@@ -4,7 +4,7 @@
  * What the maintainer's copy of this file does inside opal/datatype/ (INTEGRATION.md §1):
  *   - opal_hip_bridge_attach() runs right after OPAL_CONVERTOR_PREPARE in
  *     opal_convertor_prepare_for_{send,recv} (opal_convertor.c:616-696) for accelerator
- *     convertors and installs fAdvance / fPosition, the way pack_description_sweep.c:896-965
+ *     convertors and installs fAdvance / fPosition, the way pack_description_sweep.c:877-965
  *     swaps the movers of a prepared convertor;
  *   - each committed opal_datatype_t is imported once (ddt_type_from_opal_desc on the
  *     convertor's use_desc, opal_convertor.c:533) into a cache keyed by the datatype

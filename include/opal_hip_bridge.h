@@ -5,7 +5,7 @@
  * Open MPI has no component framework for datatype engines; the accelerator movers are
  * hard-wired in opal_convertor_prepare_for_{recv,send} (opal_convertor.c:633-635,
  * :677-679) when check_addr reports a device buffer (:593-608).  The reference's own
- * precedent for replacing them after prepare is pack_description_sweep.c:877-960, which
+ * precedent for replacing them after prepare is pack_description_sweep.c:877-965, which
  * overrides convertor->fAdvance.  This bridge does the same: after prepare,
  * opal_hip_bridge_attach() points fAdvance at opal_pack_hip / opal_unpack_hip and
  * fPosition at opal_position_hip.  INTEGRATION.md §1 shows the three-line patch.

@@ -12,7 +12,7 @@ movers.  Test infrastructure only.
   OPAL_CONVERTOR_PREPARE + opal_convertor_prepare_for_{send,recv}
   (opal_convertor.c:526-591, :616-696), opal_convertor_pack / _unpack (:255-349) and
   opal_convertor_set_position (opal_convertor.h:357-394).  Like
-  pack_description_sweep.c:896-965, the movers are swapped after prepare
+  pack_description_sweep.c:877-965, the movers are swapped after prepare
   (opal_hip_bridge_attach).
 """
 from __future__ import annotations
@@ -299,7 +299,7 @@ class Convertor:
             return OPAL_SUCCESS   # NO_OP: opal_convertor_pack copies it with cbmemcpy
         c.flags &= ~CONVERTOR_NO_OP
         # dispatch (:633-635, :677-679) chose the accelerator movers; swap them like
-        # pack_description_sweep.c:896-965 does
+        # pack_description_sweep.c:877-965 does
         return bridge_lib().opal_hip_bridge_attach(self.ptr)
 
     # opal_convertor_pack / opal_convertor_unpack (opal_convertor.c:255-349)

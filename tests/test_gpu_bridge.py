@@ -1,7 +1,7 @@
 """The drop-in boundary on the GPU: opal-shaped convertors (tests/opal_shapes.py builds
 opal_datatype_t / opal_convertor_t as Open MPI lays them out and prepares them the way
 opal_convertor_prepare_for_{send,recv} does) whose fAdvance / fPosition were swapped for
-the bridge after prepare, as pack_description_sweep.c:896-965 swaps the reference's
+the bridge after prepare, as pack_description_sweep.c:877-965 swaps the reference's
 movers.  Every byte is checked against the reference's known answers (golden digests of
 the corpus by-hand packers, unpack_ooo.c's expected struct contents, ddt_raw2.c's
 description walked literally) or the CPU oracle.
