@@ -541,6 +541,19 @@ def floor_parts(name):
                 ("dim2 elements", 0, 4, (18, 3, 0), (row, field, 0), (n - 1) * e, 0)]
     if name == "cfg1":
         return [("elements", 0, 8, (10, 11, 0), (16, 16376, 0), 0, 0)]
+    if name == "cfg5":
+        # 128 Mi records of 20 bytes at a 32-byte pitch: the r3 bare LDS kernels (pack: whole-line
+        # span loads; unpack: plain dwordx4 + dword record stores)
+        return [("records", 2, 20, (27, 0, 0), (32, 0, 0), 0, 0)]
+    if name == "cfg4":
+        # the address-ordered design's passes: (1) every touched line read once in
+        # address order into a compact stream / the masked scatter of every element in address
+        # order, with a 4-byte index per element; (2) the permutation pass between that stream
+        # and the packed order, priced as a contiguous copy of its bytes between two scratch
+        # buffers (no user or packed bytes; the engine permutes through LDS)
+        n = 64 << 20
+        return [("address-ordered elements", 3, 4, (0, 0, 0), (0, 0, 0), 0, 0, {"count": n, "list": True}),
+                ("permutation stream", 1, 0, (14, 0, 0), (16384, 0, 0), 0, 10, {"scratch": 4 * n})]
     return None
 
 
@@ -557,7 +570,8 @@ def floor_lib():
             _fields_ = [("kind", ctypes.c_int32), ("esize", ctypes.c_int32), ("l0", ctypes.c_uint32),
                         ("l1", ctypes.c_uint32), ("l2", ctypes.c_uint32), ("lw", ctypes.c_uint32),
                         ("s0", ctypes.c_int64), ("s1", ctypes.c_int64), ("s2", ctypes.c_int64),
-                        ("base", ctypes.c_int64), ("poff", ctypes.c_int64)]
+                        ("base", ctypes.c_int64), ("poff", ctypes.c_int64), ("list", ctypes.c_uint64),
+                        ("count", ctypes.c_uint64), ("ubuf", ctypes.c_uint64), ("pbuf", ctypes.c_uint64)]
         L = ctypes.CDLL(os.path.join(ROOT, "ompi_amd", "libddt_floor.so"))
         L.ddt_floor_run.restype = ctypes.c_int
         L.ddt_floor_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
@@ -580,9 +594,12 @@ def face_floor_part(face, fields, n=256, e=8):
             "z": (1, 0, (lf, 0, 0), (field, 0, 0), 0, 15)}[face]
 
 
-def floor_run(name, user_ptr, packed_ptr, reps=10):
+def floor_run(name, user_ptr, packed_ptr, reps=10, recipe=None, dev=None):
     """Each part of the workload by its bare kernel, pack then unpack, in the same run and on
-    the same buffers as the engine; returns per-part medians (us) or None."""
+    the same buffers as the engine; returns per-part medians (us) or None.  Parts with extras:
+    "list" = the workload's element indices in ascending order uploaded for the part (config 4:
+    from `recipe`'s displacements), "scratch" = a pass between two scratch buffers of that many
+    bytes (not counted in the packed bytes the parts cover)."""
     import ctypes
     parts = floor_parts(name)
     if parts is None:
@@ -590,12 +607,28 @@ def floor_run(name, user_ptr, packed_ptr, reps=10):
     L, Part = floor_lib()
     arr = (Part * len(parts))()
     poff = 0
-    for i, (_, kind, es, ls, ss, base, lw) in enumerate(parts):
+    keep = []
+    for i, (_, kind, es, ls, ss, base, lw, *ex) in enumerate(parts):
+        ex = ex[0] if ex else {}
         arr[i] = Part(kind, es, ls[0], ls[1], ls[2], lw, ss[0], ss[1], ss[2], base, poff)
-        npos = 1 << sum(ls)
-        poff += npos * (es if kind == 0 else 16 << lw)
+        if ex.get("list"):
+            import torch
+            idx = np.sort(np.asarray(recipe[2], dtype=np.int64))
+            assert len(idx) == ex["count"] and idx[0] >= 0 and idx[-1] < (1 << 32)
+            t = torch.from_numpy(idx.astype(np.uint32).view(np.int32)).to(dev)
+            keep.append(t)
+            arr[i].list, arr[i].count = t.data_ptr(), ex["count"]
+        if ex.get("scratch"):
+            import torch
+            bufs = [torch.empty(ex["scratch"], dtype=torch.uint8, device=dev) for _ in range(2)]
+            keep += bufs
+            arr[i].ubuf, arr[i].pbuf, arr[i].poff = bufs[0].data_ptr(), bufs[1].data_ptr(), 0
+            continue
+        npos = ex["count"] if "count" in ex else 1 << sum(ls)
+        poff += npos * (es if kind in (0, 2, 3) else 16 << lw)
     out = (ctypes.c_float * (2 * len(parts)))()
     rc = L.ddt_floor_run(ctypes.c_void_p(user_ptr), ctypes.c_void_p(packed_ptr), arr, len(parts), reps, out)
+    del keep
     if rc != 0:
         return {"error": f"hip error {rc}"}
     res = {label: {"pack_us": round(out[2 * i], 2), "unpack_us": round(out[2 * i + 1], 2)}
@@ -631,6 +664,160 @@ def copy_ceiling(dev, nbytes=1 << 30, reps=10):
     return {"bytes": nbytes, "copy_us": [round(out[0], 2), round(out[1], 2)],
             "GB_per_s": round(sum(gbs) / 2, 1),
             "source": "ompi_amd/csrc/ddt_floor.hip copy_blocks, 1 GiB each way, median of 10"}
+
+
+# ------------------------------------------------------------------ end to end (host packed stream)
+def end_to_end(dev, config, pageable=False, reps=10, tune="", hostdirect=-1, stage_mb=0):
+    """End-to-end rate with a HOST-resident packed stream (SURVEY.md §8d "End-to-end"; the north
+    star's "copies to and from the GPU"): pack e2e = pack kernel + D2H into host memory, unpack
+    e2e = H2D from host memory + unpack kernel, the user buffer device-resident.  Schedules:
+      serialized -- whole-message kernel into an HBM buffer, then one copy (and reverse);
+      overlapped -- the convertor's own host-iovec path (pinned: the kernel moves the host bytes
+                    itself over PCIe; pageable: chunks double-buffered through HBM staging).
+    Beside them the bare pinned copies (the PCIe ceiling).  Wall-clock medians of `reps` calls;
+    `stream_us` = the stream time alone, `host_call_us` = the host time of one call.  Outside the
+    bench's timed region; never `value`."""
+    import statistics
+    import torch
+    import ompi_amd
+    from ompi_amd import recipe as ER
+    if hostdirect >= 0:
+        ompi_amd.lib().ddt_tune(b"hostdirect", hostdirect)
+    if stage_mb:
+        ompi_amd.lib().ddt_tune(b"stage_mb", stage_mb)
+    for kv in filter(None, tune.split(";")):
+        k, v = kv.split("=")
+        ompi_amd.lib().ddt_tune(k.encode(), int(v))
+    recipe, count, desc = make_workload(config)
+    dt = ER.build_committed(recipe)
+    info = dt.info()
+    S = info["size"] * count
+    span, origin = layout(info, count)
+    user = torch.randint(1, 255, (span,), dtype=torch.uint8, device=dev)
+    uptr = user.data_ptr() + origin
+    dpk = torch.empty(S, dtype=torch.uint8, device=dev)
+    hpk = torch.empty(S, dtype=torch.uint8, pin_memory=not pageable)
+    st = torch.cuda.current_stream(dev)
+    cp, cu = ompi_amd.Convertor(), ompi_amd.Convertor()
+    for c in (cp, cu):
+        c.set_stream(st, True)
+
+    def pack_dev():
+        cp.prepare_for_send(dt, count, uptr)
+        cp.pack([(dpk, S)])
+
+    def unpack_dev():
+        cu.prepare_for_recv(dt, count, uptr)
+        cu.unpack([(dpk, S)])
+
+    def pack_ser():
+        pack_dev()
+        hpk.copy_(dpk, non_blocking=True)
+
+    def unpack_ser():
+        dpk.copy_(hpk, non_blocking=True)
+        unpack_dev()
+
+    def pack_ovl():
+        cp.prepare_for_send(dt, count, uptr)
+        cp.pack([(hpk.data_ptr(), S)])
+
+    def unpack_ovl():
+        cu.prepare_for_recv(dt, count, uptr)
+        cu.unpack([(hpk.data_ptr(), S)])
+
+    def gpu_time(fn, reps):
+        """stream time of fn alone: a sleep kernel holds the stream while the host enqueues,
+        so host-side call overhead is not counted (the wall-clock rows count it)"""
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(2_000_000)
+            e0.record(st)
+            fn()
+            e1.record(st)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / 1e3)
+        return statistics.median(ts)
+
+    def host_time(fn, reps):
+        """host time of one call (the stream is held by a sleep kernel: nothing waits)"""
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            torch.cuda._sleep(2_000_000)
+            a = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - a)
+            torch.cuda.synchronize()
+        return statistics.median(ts)
+
+    r = reps
+
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts)
+    h = {k: host_time(f, r) for k, f in (("pack_device", pack_dev), ("pack_overlapped", pack_ovl),
+                                         ("unpack_overlapped", unpack_ovl),
+                                         ("d2h_copy", lambda: hpk.copy_(dpk, non_blocking=True)))}
+    g = {k: gpu_time(f, r) for k, f in (("pack_overlapped", pack_ovl), ("unpack_overlapped", unpack_ovl),
+                                        ("d2h_copy", lambda: hpk.copy_(dpk, non_blocking=True)),
+                                        ("h2d_copy", lambda: dpk.copy_(hpk, non_blocking=True)))}
+    t = {k: timed(f, r) for k, f in (("pack_kernel", pack_dev), ("unpack_kernel", unpack_dev),
+                                     ("pack_serialized", pack_ser), ("unpack_serialized", unpack_ser),
+                                     ("pack_overlapped", pack_ovl), ("unpack_overlapped", unpack_ovl),
+                                     ("d2h_copy", lambda: hpk.copy_(dpk, non_blocking=True)),
+                                     ("h2d_copy", lambda: dpk.copy_(hpk, non_blocking=True)))}
+    # the overlapped path must produce the same stream as the device path
+    pack_dev()
+    ref = dpk.clone()
+    pack_ovl()
+    torch.cuda.synchronize()
+    same = bool(torch.equal(ref.cpu(), hpk))
+    # and the overlapped unpack must restore what the device path restores
+    keep = user.clone()
+    user.fill_(0xA5)
+    unpack_ovl()
+    torch.cuda.synchronize()
+    got_o = user.clone()
+    user.fill_(0xA5)
+    dpk.copy_(hpk)
+    unpack_dev()
+    torch.cuda.synchronize()
+    same_u = bool(torch.equal(got_o, user))
+    user.copy_(keep)
+    out = {"config": config, "workload": desc["workload"], "packed_bytes": S,
+           "host_memory": "pageable" if pageable else "pinned",
+           "hostdirect": int(hostdirect), "stage_mb": stage_mb, "tune": tune,
+           "overlapped_matches_device_path": same, "overlapped_unpack_matches": same_u,
+           "GiBs": {k: round(S / v / GiB, 2) for k, v in t.items()},
+           "overlapped_vs_bare_copy": {"pack": round(t["d2h_copy"] / t["pack_overlapped"], 3),
+                                       "unpack": round(t["h2d_copy"] / t["unpack_overlapped"], 3)},
+           "us": {k: round(v * 1e6, 1) for k, v in t.items()},
+           "stream_us": {k: round(v * 1e6, 1) for k, v in g.items()},
+           "host_call_us": {k: round(v * 1e6, 1) for k, v in h.items()},
+           "stream_overlapped_vs_bare_copy": {"pack": round(g["d2h_copy"] / g["pack_overlapped"], 3),
+                                              "unpack": round(g["h2d_copy"] / g["unpack_overlapped"], 3)},
+           "pack+unpack_GiBs": {
+               "device_resident": round(2 * S / (t["pack_kernel"] + t["unpack_kernel"]) / GiB, 2),
+               "serialized": round(2 * S / (t["pack_serialized"] + t["unpack_serialized"]) / GiB, 2),
+               "overlapped": round(2 * S / (t["pack_overlapped"] + t["unpack_overlapped"]) / GiB, 2)}}
+    del user, dpk, hpk
+    torch.cuda.empty_cache()
+    return out
+
+
 
 
 # ------------------------------------------------------------------ multi-rank harness
@@ -714,6 +901,10 @@ def main():
     ap.add_argument("--no-floor", action="store_true", help="skip the bare-kernel floor of the workload")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-face latency probe (profiling runs: one workload per trace)")
+    ap.add_argument("--e2e", action="store_true",
+                    help="after the line's measurements: end-to-end rates with a host-resident packed "
+                         "stream (cfg1, cfg2, cfg5; pinned and pageable), outside the timed region")
+    ap.add_argument("--no-cold", action="store_true", help="skip the cold-unpack step (cold_step)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -874,13 +1065,45 @@ def main():
         torch.cuda.synchronize()
         graph_step = g0.elapsed_time(g1) / 1e3 / args.steps
 
+    # The cold-unpack step, outside the timed region: the same pack + unpack
+    # with the 1 GiB read flush of face_throughput before the pack and again between pack and
+    # unpack (outside the events), so the unpack finds none of the lines the pack just read in
+    # the Infinity Cache -- what the headline owes to the stream policy's cache merge.
+    cold = None
+    if rank == 0 and world == 1 and not args.no_cold:
+        scribble = torch.full((1 << 27,), 3, dtype=torch.int64, device=dev)
+        cev = []
+        for i in range(8):
+            a, b_, c_, d_ = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+            scribble.sum()
+            a.record(stream)
+            pack()
+            b_.record(stream)
+            scribble.sum()
+            c_.record(stream)
+            unpack()
+            d_.record(stream)
+            if i >= 2:
+                cev.append((a, b_, c_, d_))
+        torch.cuda.synchronize()
+        cp_ = float(np.median([a.elapsed_time(b_) for a, b_, _, _ in cev])) * 1e3
+        cu_ = float(np.median([c_.elapsed_time(d_) for _, _, c_, d_ in cev])) * 1e3
+        cold = {"pack_us": round(cp_, 2), "unpack_us": round(cu_, 2), "step_us": round(cp_ + cu_, 2),
+                "frac": round(4.0 * S / ((cp_ + cu_) * 1e-6) / HBM_PEAK, 4),
+                "GiBs": round(2.0 * S / ((cp_ + cu_) * 1e-6) / GiB, 2),
+                "warm_step_us": round((tp + tu) * 1e6, 2),
+                "flush": "1 GiB read (a reduction) before the pack and between pack and unpack, outside "
+                         "the events: cold and clean caches for each operation"}
+        del scribble
+        torch.cuda.empty_cache()
+
     # The floor of this workload on this box, outside the timed region: each of its parts moved
     # by a bare kernel (ompi_amd/csrc/ddt_floor.hip) on the same buffers, in the same pack-then-
     # unpack order.  frac_of_floor = floor / the engine's own event time (1.0 = at the floor).
     floor = None
     if rank == 0 and world == 1 and not args.no_floor and not split:
         try:
-            fl = floor_run(args.config, uptr, packed.data_ptr())
+            fl = floor_run(args.config, uptr, packed.data_ptr(), recipe=recipe, dev=dev)
         except OSError as ex:   # the measurement library is missing: report, never fail the line
             fl = {"error": f"{type(ex).__name__}: {ex}"[:200]}
         if fl and "error" not in fl:
@@ -894,6 +1117,7 @@ def main():
                                        "step": round(step_floor / ((tp + tu) * 1e6), 4)}
                 fl["source"] = ("ompi_amd/csrc/ddt_floor.hip: element gathers (plain loads), element "
                                 "scatters (non-temporal stores), 16 KiB block copies (non-temporal loads), "
+                                "records through LDS (cfg5), listed elements in address order (cfg4), "
                                 "median of 10 rounds; floor = sum of the parts")
         floor = fl
         torch.cuda.synchronize()
@@ -950,6 +1174,7 @@ def main():
                              "achieved": round(2.0 * S / max(tp, tu) / 1e9, 2),
                              "frac": round(2.0 * S / max(tp, tu) / HBM_PEAK, 4)}},
             "floor_us": floor,
+            "cold_step": cold,
         }
         if copy and "GB_per_s" in copy:
             copy["engine_frac_of_copy"] = round(achieved / 1e9 / copy["GB_per_s"], 4)
@@ -997,6 +1222,14 @@ def main():
                 result[key].setdefault(k, {})
                 result[key][k]["back_to_back_us"] = bb[k]["back_to_back_us"]
                 result[key][k]["graph_us"] = bb[k]["graph_us"]
+
+    if rank == 0 and world == 1 and args.e2e:
+        # the path starts and ends in host memory (north star): the copies to and from the GPU
+        # included, for the small, the default and the largest config, pinned and pageable
+        del user, packed
+        torch.cuda.empty_cache()
+        result["e2e"] = [end_to_end(dev, c, pageable=pg, reps=5)
+                         for c in ("cfg1", "cfg2", "cfg5") for pg in (False, True)]
 
     if rank == 0 and base_sample is not None:
         srec, scount, what, host_user, gpu_prefix = base_sample

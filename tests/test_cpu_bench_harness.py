@@ -105,6 +105,28 @@ def test_floor_parts_move_exactly_the_workloads_bytes(cfg):
     np.testing.assert_array_equal(elements(want, wlen), elements(got, glen))
 
 
+def test_floor_parts_of_cfg4_and_cfg5():
+    """The floors of BASELINE configs 4 and 5: config 5's record part is the
+    hvector's type map (128 Mi records of 20 bytes at a 32-byte pitch, S packed bytes); config 4's
+    listed part moves every element of the indexed type once (its 64 Mi displacements, S bytes)
+    and its permutation pass runs between scratch buffers of S bytes, outside the packed count."""
+    rec5, count5, _ = bench.make_workload("cfg5")
+    (label, kind, es, ls, ss, base, lw), = bench.floor_parts("cfg5")
+    n = 1 << sum(ls)
+    assert kind == 2 and (n, es, ss[0], base) == (rec5[1], 20, rec5[3], 0)
+    from ompi_amd import recipe as ER
+    i5 = ER.build_committed(("hvector", 64, 1, 32, rec5[4])).info()
+    assert i5["size"] == 64 * 20 and n * es * count5 == (128 << 20) * 20
+    rec4, count4, _ = bench.make_workload("cfg4")
+    parts = bench.floor_parts("cfg4")
+    lst = [p for p in parts if len(p) > 7 and p[7].get("list")]
+    scr = [p for p in parts if len(p) > 7 and p[7].get("scratch")]
+    assert len(lst) == 1 and len(scr) == 1
+    assert lst[0][7]["count"] == len(rec4[2]) and lst[0][2] == 4 and rec4[1] == 1
+    S = len(rec4[2]) * 4
+    assert scr[0][7]["scratch"] == S == (1 << sum(scr[0][3])) * (16 << scr[0][6])
+
+
 def test_strong_cfg3_over_eight_ranks_covers_all_64_fields():
     """The driver's 8-GPU strong run of BASELINE config 3 (`--gpus 8 --strong --config cfg3`): the
     self-launch command is one rank per GPU with the same arguments, and the eight ranks' splits
