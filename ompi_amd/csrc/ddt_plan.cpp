@@ -492,7 +492,8 @@ int prebuild_device(ddt_datatype *t)
     // (the bridge imports at the first attach).  So: no build while the legacy stream
     // captures or cannot be queried (it fails while a global capture is under way), and the
     // build runs with this thread in relaxed capture mode, where those calls are this thread's
-    // own business (r5_probe_capture.log).  A skipped build happens at the first move instead.
+    // own business -- all but a device synchronisation, which the pool then does not make
+    // (profiles/r5_probe_capture.log).  A skipped build happens at the first move instead.
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(nullptr, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
         (void) hipGetLastError();
@@ -505,6 +506,7 @@ int prebuild_device(ddt_datatype *t)
     const bool swapped = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
     (void) hipGetLastError();
     int rc = DDT_SUCCESS;
+    PoolNoDeviceSync no_sync;   // allocation, upload and stream waits only: no device-wide wait
     try {
         ensure_device_lists(*P);
         (void) sorted_build(*P, bs);

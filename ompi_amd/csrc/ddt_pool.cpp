@@ -35,6 +35,8 @@ struct Pool {
     std::vector<Pending> pending;
 };
 
+thread_local int t_no_device_sync = 0;
+
 Pool &pool()
 {
     static Pool *p = new Pool();   // never destroyed: blocks may be released at exit
@@ -99,7 +101,7 @@ void settle_and_cap(Pool &P, int dev)   // P.mu held
 {
     bool unknown = false;
     for (const Pending &r : P.pending)
-        unknown |= r.unknown && on_device(P, r, dev);
+        unknown |= r.unknown && on_device(P, r, dev) && !t_no_device_sync;
     if (unknown && hipDeviceSynchronize() == hipSuccess) {
         for (size_t i = 0; i < P.pending.size();) {
             Pending &r = P.pending[i];
@@ -141,6 +143,9 @@ void *take_free(Pool &P, int dev, size_t bytes)   // P.mu held
 }
 
 }  // namespace
+
+PoolNoDeviceSync::PoolNoDeviceSync() { ++t_no_device_sync; }
+PoolNoDeviceSync::~PoolNoDeviceSync() { --t_no_device_sync; }
 
 void *pool_alloc(size_t bytes)
 {

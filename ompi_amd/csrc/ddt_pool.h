@@ -45,6 +45,15 @@ void pool_keep(void *p);
 bool pool_fences(const std::vector<hipStream_t> &streams, std::vector<hipEvent_t> &fences, bool &unknown);
 // ddt_trim: synchronise the device, hand every reusable and fenced block back to HIP.
 int pool_trim();
+// While one lives on a thread, that thread's allocations never settle unknown releases by a
+// device synchronisation (the one call a relaxed-mode thread still may not make during another
+// thread's capture, profiles/r5_probe_capture.log): table builds at commit / import run under it.
+struct PoolNoDeviceSync {
+    PoolNoDeviceSync();
+    ~PoolNoDeviceSync();
+    PoolNoDeviceSync(const PoolNoDeviceSync &) = delete;
+    PoolNoDeviceSync &operator=(const PoolNoDeviceSync &) = delete;
+};
 // out[0..5] = blocks cached free, bytes cached free, blocks waiting on fences, bytes waiting,
 // blocks kept for captured graphs, blocks in use.  Fences are checked only by pool_alloc (an
 // event query invalidates another thread's global-mode capture; so does any allocation).

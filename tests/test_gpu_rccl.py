@@ -61,7 +61,7 @@ def test_rccl_gather_packed_single_rank(device):
     r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert r["backend"] == "nccl" and r["ok_full"]
     assert r["check"]["ok"] and r["check"]["backend"] == "nccl"
-    assert r["gathered"] == r["check"]["gathered_bytes"] == 2 * 3 * 512 * 1024
+    assert r["gathered"] == r["check"]["gathered_bytes"] == 2 * 6 * 512 * 1024   # 2 fields x 6 faces
 
 
 def test_bench_line_with_rccl_process_group(device):
