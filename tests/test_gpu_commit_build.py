@@ -5,8 +5,8 @@ A cfg4-shaped type -- an indexed list of 2 Mi one-float blocks at LCG displaceme
 address-ordered engine's domain, >= 1 Mi blocks) -- is committed with the engine's constructors
 and, separately, handed to the bridge as Open MPI's committed description (two-block FLOAT4 pairs,
 SURVEY App. A).  The engine's commit and the bridge's import (at prepare) build the tables; the
-first asynchronous pack's host call then only enqueues: it must return in under 1 ms (the build
-itself is ~10 ms of device work plus host round trips).  The packed bytes are checked.
+first asynchronous pack's host call then only enqueues: it must return in under 3 ms (the build
+itself is ~10 ms of device work plus host round trips; 3 ms leaves room for box jitter, r5).  The packed bytes are checked.
 """
 from __future__ import annotations
 
@@ -61,7 +61,7 @@ def test_engine_commit_builds_the_tables(device, disps):
     assert rc == 1 and md == N * 4
     torch.cuda.synchronize()
     np.testing.assert_array_equal(packed.cpu().numpy(), _want(user.cpu().numpy(), disps))
-    assert host_s < 1e-3, f"first asynchronous pack took {host_s * 1e3:.2f} ms of host time"
+    assert host_s < 3e-3, f"first asynchronous pack took {host_s * 1e3:.2f} ms of host time"
 
 
 @pytest.mark.parametrize("hook", [False, True], ids=["import_at_prepare", "commit_hook"])
@@ -104,7 +104,7 @@ def test_bridge_import_builds_the_tables(device, disps, hook):
     assert rc == 1 and md == N * 4
     torch.cuda.synchronize()
     np.testing.assert_array_equal(packed.cpu().numpy(), _want(user.cpu().numpy(), disps))
-    assert host_s < 1e-3, f"first asynchronous bridge pack took {host_s * 1e3:.2f} ms of host time"
+    assert host_s < 3e-3, f"first asynchronous bridge pack took {host_s * 1e3:.2f} ms of host time"
     ot.destruct()
 
 
