@@ -21,6 +21,11 @@
 //   7 scatter8        one plain 8-B store per sparse line
 //   8 scatter4_nt     one non-temporal 4-B store per sparse line
 //   9 gather8_dense   one 8-B load per line, lines adjacent (128-B pitch)
+//  10 gather8_nt      pattern 2 with non-temporal loads
+//  11 coop8           8 lanes per sparse line, each a 16-B load of its part (the whole line is
+//                     read, like a stream); the lane holding the element writes it compactly
+//  12 coop8_nt        pattern 11 with non-temporal loads
+//  13 gather16        one 16-B load per sparse line (the element's 16-B part), 8 B written
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -38,9 +43,10 @@
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int NPAT = 10;
+constexpr int NPAT = 14;
 constexpr const char *kNames[NPAT] = {"stream_read", "stream_write", "gather8", "gather4", "gather8_pair64",
-                                      "gather8_pair8", "scatter8_nt", "scatter8", "scatter4_nt", "gather8_dense"};
+                                      "gather8_pair8", "scatter8_nt", "scatter8", "scatter4_nt", "gather8_dense",
+                                      "gather8_nt", "coop8", "coop8_nt", "gather16"};
 constexpr size_t PITCH = 2048;
 
 __global__ __launch_bounds__(256) void cal_flush(const u32x4 *__restrict__ p, size_t n, uint32_t *sink)
@@ -73,6 +79,16 @@ __global__ __launch_bounds__(256) void cal(uint8_t *__restrict__ big, uint8_t *_
         }
         return;
     }
+    if (P == 11 || P == 12) {
+        if (t >= L * 8)
+            return;
+        const size_t ln = t >> 3, part = t & 7;
+        const u32x4 *q = reinterpret_cast<const u32x4 *>(big + ln * PITCH) + part;
+        const u32x4 v = P == 12 ? __builtin_nontemporal_load(q) : *q;
+        if (part == 0)
+            reinterpret_cast<uint64_t *>(compact)[ln] = uint64_t(v.x) | (uint64_t(v.y) << 32);
+        return;
+    }
     if (t >= L)
         return;
     uint8_t *line = big + t * (P == 9 ? 128 : PITCH);
@@ -102,6 +118,14 @@ __global__ __launch_bounds__(256) void cal(uint8_t *__restrict__ big, uint8_t *_
     case 8:
         __builtin_nontemporal_store(uint32_t(t) * 3 + RUN, reinterpret_cast<uint32_t *>(line));
         break;
+    case 10:
+        c8[t] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(line));
+        break;
+    case 13: {
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(line);
+        c8[t] = uint64_t(v.x) | (uint64_t(v.y) << 32);
+        break;
+    }
     default:
         break;
     }
@@ -110,7 +134,7 @@ __global__ __launch_bounds__(256) void cal(uint8_t *__restrict__ big, uint8_t *_
 template <int P, int RUN>
 void launch(uint8_t *big, uint8_t *compact, size_t L, uint32_t *sink)
 {
-    const size_t threads = (P == 0 || P == 1) ? L * 8 : L;
+    const size_t threads = (P == 0 || P == 1 || P == 11 || P == 12) ? L * 8 : L;
     hipLaunchKernelGGL((cal<P, RUN>), dim3(uint32_t((threads + 255) / 256)), dim3(256), 0, nullptr, big, compact, L,
                        sink);
 }
@@ -161,6 +185,10 @@ int main(int argc, char **argv)
     run_pattern<7>(big, compact, L, flush, nflush, sink, ev, ms[7]);
     run_pattern<8>(big, compact, L, flush, nflush, sink, ev, ms[8]);
     run_pattern<9>(big, compact, L, flush, nflush, sink, ev, ms[9]);
+    run_pattern<10>(big, compact, L, flush, nflush, sink, ev, ms[10]);
+    run_pattern<11>(big, compact, L, flush, nflush, sink, ev, ms[11]);
+    run_pattern<12>(big, compact, L, flush, nflush, sink, ev, ms[12]);
+    run_pattern<13>(big, compact, L, flush, nflush, sink, ev, ms[13]);
     CHK(hipDeviceSynchronize());
     for (int p = 0; p < NPAT; ++p)
         for (int r = 0; r < 2; ++r)

@@ -21,11 +21,13 @@ import re
 import sys
 
 NAMES = ["stream_read", "stream_write", "gather8", "gather4", "gather8_pair64", "gather8_pair8",
-         "scatter8_nt", "scatter8", "scatter4_nt", "gather8_dense"]
+         "scatter8_nt", "scatter8", "scatter4_nt", "gather8_dense", "gather8_nt", "coop8", "coop8_nt",
+         "gather16"]
 # useful bytes read / written per line by each pattern (streams: one 128-B line = 8 lanes x 16 B)
 USEFUL = {"stream_read": (128, 0), "stream_write": (0, 128), "gather8": (8, 8), "gather4": (4, 4),
           "gather8_pair64": (16, 16), "gather8_pair8": (16, 16), "scatter8_nt": (0, 8),
-          "scatter8": (0, 8), "scatter4_nt": (0, 4), "gather8_dense": (8, 8)}
+          "scatter8": (0, 8), "scatter4_nt": (0, 4), "gather8_dense": (8, 8), "gather8_nt": (8, 8),
+          "coop8": (8, 8), "coop8_nt": (8, 8), "gather16": (8, 8)}
 KIB = {"FETCH_SIZE", "WRITE_SIZE"}
 
 
