@@ -446,15 +446,11 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     }
     if (!d_items && S->has_lists)
         note_stream(P, stream);   // an inline launch of index lists reads the plan's lists
-    // an unpack may walk its tasks last to first (ddt_tune "urev", move_body): the whole-grid
-    // kernels only (no dense launch, no capped grid)
-    const uint32_t ntasks = S->ntasks | (dir == 1 && tuning().urev && !S->all_dense && !grid_cap
-                                         && S->ntasks < TASKS_REVERSED ? TASKS_REVERSED : 0u);
     if (!d_items)
-        HIPCHK(launch_move_inline(S->blk, ntasks, dir, S->has_lists, ubase, pbase, stream, grid_cap,
+        HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, ubase, pbase, stream, grid_cap,
                                   S->all_dense));
     else
-        HIPCHK(launch_move(d_items, uint32_t(S->items.size()), ntasks, dir, S->has_lists, ubase, pbase,
+        HIPCHK(launch_move(d_items, uint32_t(S->items.size()), S->ntasks, dir, S->has_lists, ubase, pbase,
                            stream, grid_cap, S->all_dense));
     return DDT_SUCCESS;
 }
@@ -1705,8 +1701,6 @@ int ddt_tune(const char *key, long value)
         tuning().stask = value < 0 ? 0 : value;
     else if (k == "spass")
         tuning().spass = value < 1 ? 1 : value;
-    else if (k == "urev")
-        tuning().urev = value ? 1 : 0;
     else if (k == "opt_growth")
         tuning().opt_growth = value < 0 ? 0 : (value > 1024 ? 1024 : value);
     else if (k == "opt_unroll_items")

@@ -15,7 +15,6 @@ namespace ddt {
 constexpr int MAXD = 8;             // affine dims per item, instance dim included
 constexpr int THREADS = 256;        // workgroup size (4 wave64)
 constexpr uint32_t SLAB_FULL = 0xffffffffu;
-constexpr uint32_t TASKS_REVERSED = 0x80000000u;   // launch's task count flag (move_body)
 // units each thread loads before storing, per pass of the affine loop
 constexpr int unroll_of(uint32_t U) { return U >= 16 ? 4 : 8; }
 // user-span bytes a workgroup stages in LDS per task of the line-dense path (run_dense)

@@ -114,8 +114,6 @@ bool launch_single_item(const Item &it, int dir, uint64_t ubase, uint64_t pbase,
 hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bool lists, uint64_t ubase,
                               uint64_t pbase, hipStream_t stream, uint32_t grid_cap, bool dense)
 {
-    const uint32_t rev = ntasks & TASKS_REVERSED;
-    ntasks &= ~TASKS_REVERSED;
     if (ntasks == 0 || blk.n == 0)
         return hipSuccess;
     const uint32_t g = grid_cap && grid_cap < ntasks ? grid_cap : ntasks;
@@ -126,17 +124,15 @@ hipError_t launch_move_inline(const ItemBlock &blk, uint32_t ntasks, int dir, bo
                         : launch_dense_inline_u0(blk, ntasks, gs, ubase, pbase, stream, sp);
     }
     if (dir == 0)
-        return lists ? launch_move_inline_p1(blk, ntasks | rev, g, ubase, pbase, stream)
-                     : launch_move_inline_p0(blk, ntasks | rev, g, ubase, pbase, stream);
-    return lists ? launch_move_inline_u1(blk, ntasks | rev, g, ubase, pbase, stream)
-                 : launch_move_inline_u0(blk, ntasks | rev, g, ubase, pbase, stream);
+        return lists ? launch_move_inline_p1(blk, ntasks, g, ubase, pbase, stream)
+                     : launch_move_inline_p0(blk, ntasks, g, ubase, pbase, stream);
+    return lists ? launch_move_inline_u1(blk, ntasks, g, ubase, pbase, stream)
+                 : launch_move_inline_u0(blk, ntasks, g, ubase, pbase, stream);
 }
 
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
                        uint64_t ubase, uint64_t pbase, hipStream_t stream, uint32_t grid_cap, bool dense)
 {
-    const uint32_t rev = ntasks & TASKS_REVERSED;
-    ntasks &= ~TASKS_REVERSED;
     if (ntasks == 0 || nitems == 0)
         return hipSuccess;
     const uint32_t g = grid_cap && grid_cap < ntasks ? grid_cap : ntasks;
@@ -147,10 +143,10 @@ hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, in
                         : launch_dense_u0(d_items, nitems, ntasks, gs, ubase, pbase, stream, sp);
     }
     if (dir == 0)
-        return lists ? launch_move_p1(d_items, nitems, ntasks | rev, g, ubase, pbase, stream)
-                     : launch_move_p0(d_items, nitems, ntasks | rev, g, ubase, pbase, stream);
-    return lists ? launch_move_u1(d_items, nitems, ntasks | rev, g, ubase, pbase, stream)
-                 : launch_move_u0(d_items, nitems, ntasks | rev, g, ubase, pbase, stream);
+        return lists ? launch_move_p1(d_items, nitems, ntasks, g, ubase, pbase, stream)
+                     : launch_move_p0(d_items, nitems, ntasks, g, ubase, pbase, stream);
+    return lists ? launch_move_u1(d_items, nitems, ntasks, g, ubase, pbase, stream)
+                 : launch_move_u0(d_items, nitems, ntasks, g, ubase, pbase, stream);
 }
 
 // ---------------------------------------------------------------- external32

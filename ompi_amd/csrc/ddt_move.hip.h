@@ -804,18 +804,13 @@ __global__ __launch_bounds__(THREADS) void ddt_dense1_kernel(ItemArgs args)
 // workgroups keep it full, thousands of them contend for it, scripts/ubench_pcie.hip) --
 // a grid-stride loop over the tasks.  A cap that is a multiple of 8 keeps every task on
 // the XCD the slab mapping chose for it.
-// Bit 31 of `ntasks` (TASKS_REVERSED, an unpack only): workgroup b runs task ntasks - 1 - b, so
-// the launch walks its tasks last to first -- the pack's most recent lines, still in the Infinity
-// Cache, are written first (ddt_tune "urev").
 template <int DIR, bool LISTS>
 __device__ __forceinline__ void move_body(const Item *__restrict__ items, uint32_t nitems, Bases bs, uint32_t ntasks)
 {
-    const bool rev = (ntasks & TASKS_REVERSED) != 0;
-    ntasks &= ~TASKS_REVERSED;
     for (uint32_t b = blockIdx.x; b < ntasks; b += gridDim.x) {
         if (b != blockIdx.x)
             __syncthreads();   // LDS of the previous task (list scans) is free again
-        move_task<DIR, LISTS>(items, nitems, bs, rev ? ntasks - 1 - b : b);
+        move_task<DIR, LISTS>(items, nitems, bs, b);
     }
 }
 

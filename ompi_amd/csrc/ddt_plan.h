@@ -46,7 +46,6 @@ struct Tuning {
     long sseg = 64;       // address-ordered engine: U segment bytes (32, 64 or 128), read at plan build
     long schunk = 1;      // address-ordered engine: 2 = half-size chunks, two pass-1 workgroups per
                           // CU (read at plan build)
-    int urev = 0;         // an unpack launch walks its tasks last to first (move_body)
     int sorted_commit = 1;   // build the address-ordered tables at commit / bridge import (1) or
                              // at the first whole-message move (0)
     // The commit optimizer's run-time parameters, read at commit like the reference's MCA
