@@ -638,6 +638,45 @@ def floor_run(name, user_ptr, packed_ptr, reps=10, recipe=None, dev=None):
             "unpack_us": round(sum(v["unpack_us"] for v in res.values()), 2)}
 
 
+def touched_lines(dt, count, max_iov=8 << 20):
+    """128-byte lines of user memory the type map of `count` instances touches (the engine's raw
+    iovec export, opal_convertor_raw semantics, on a NULL base: offsets only), or None beyond
+    `max_iov` iovecs.  The memory side moves whole lines (r5 calibration: one 128-B read request
+    per touched line for every access pattern the engine has)."""
+    import ctypes
+    import ompi_amd
+    from ompi_amd._lib import IOVec, lib
+    conv = ompi_amd.Convertor().prepare_for_raw(dt, count, 0)
+    chunk = 1 << 20
+    arr = (IOVec * chunk)()
+    firsts, lasts, total = [], [], 0
+    while True:
+        n = ctypes.c_uint32(chunk)
+        ln = ctypes.c_size_t(0)
+        rc = lib().ddt_convertor_raw(conv.h, arr, ctypes.byref(n), ctypes.byref(ln))
+        if rc < 0:
+            return None
+        v = np.frombuffer(arr, dtype=np.int64, count=2 * n.value).reshape(-1, 2)
+        v = v[v[:, 1] > 0]
+        firsts.append(v[:, 0] >> 7)
+        lasts.append((v[:, 0] + v[:, 1] - 1) >> 7)
+        total += n.value
+        if rc == 1 or n.value == 0:
+            break
+        if total > max_iov:
+            return None
+    f, l_ = np.concatenate(firsts), np.concatenate(lasts)
+    o = np.argsort(f, kind="stable")
+    f, l_ = f[o], l_[o]
+    # union of the [first, last] line ranges
+    reach = np.maximum.accumulate(l_)
+    new = np.ones(len(f), dtype=bool)
+    new[1:] = f[1:] > reach[:-1]
+    starts = f[new]
+    ends = np.maximum.reduceat(l_, np.flatnonzero(new))
+    return int((ends - starts + 1).sum())
+
+
 def copy_ceiling(dev, nbytes=1 << 30, reps=10):
     """"also report against a measured contiguous D2D copy ceiling".  One
     contiguous GiB copied each way by the floor library's block-copy kernel (16 KiB per
@@ -1179,6 +1218,24 @@ def main():
         if copy and "GB_per_s" in copy:
             copy["engine_frac_of_copy"] = round(achieved / 1e9 / copy["GB_per_s"], 4)
         result["copy_ceiling"] = copy
+        # The step at the memory's own granularity (r5): the pack reads every touched 128-B user
+        # line and writes S, the unpack reads S and writes every touched line back -- the least
+        # the memory side can move, since a gather costs its whole line and a partial write
+        # completes as one (r5_counter_calibration.json) -- priced at this run's copy ceiling.
+        if world == 1 and not split and not args.no_floor:
+            try:
+                lines = touched_lines(dt, count)
+            except (OSError, RuntimeError) as ex:
+                lines, result["line_floor_error"] = None, f"{type(ex).__name__}: {ex}"[:200]
+            if lines:
+                lb = 2 * (lines * 128 + S)
+                rate = copy["GB_per_s"] * 1e9 if copy and "GB_per_s" in copy else HBM_MEASURED
+                result["line_floor"] = {
+                    "touched_lines": lines, "bytes_per_step": lb, "rate_GBs": round(rate / 1e9, 1),
+                    "step_us": round(lb / rate * 1e6, 2),
+                    "frac": round(lb / rate / (tp + tu), 4),
+                    "rule": "2 x (touched 128-B user lines x 128 + packed bytes) per pack + unpack, "
+                            "at the copy ceiling measured in this run"}
         # the committed PMC passes were measured on the config's default (weak) message; a
         # --strong message of another size does not inherit them
         tfile = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")

@@ -7,10 +7,10 @@ export TMPDIR=/tmp
 CFG=${CFG:-cfg2}
 TAG=${TAG:-r1}
 run() { local name=$1; shift; echo "== $name"; timeout -k 10 400 "$@" > gpurun_out/$name.log 2>&1; local rc=$?; echo "rc=$rc"; tail -n 2 gpurun_out/$name.log; [ $rc -eq 0 ] || exit $rc; }
-run trace_$CFG rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$CFG -o trace -- python3 bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-graph --no-latency --no-faces
-run fetch_$CFG rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf_$CFG -o pmc -- python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --no-graph --no-latency --no-faces
-run write_$CFG rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw_$CFG -o pmc -- python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --no-graph --no-latency --no-faces
-run req_$CFG rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d gpurun_out/pmcr_$CFG -o pmc -- python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --no-graph --no-latency --no-faces
+run trace_$CFG rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$CFG -o trace -- python3 bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-graph --no-latency --no-faces --no-floor --no-cold
+run fetch_$CFG rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf_$CFG -o pmc -- python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --no-graph --no-latency --no-faces --no-floor --no-cold
+run write_$CFG rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw_$CFG -o pmc -- python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --no-graph --no-latency --no-faces --no-floor --no-cold
+run req_$CFG rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d gpurun_out/pmcr_$CFG -o pmc -- python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --no-graph --no-latency --no-faces --no-floor --no-cold
 python3 scripts/traffic.py $(find gpurun_out/pmcf_$CFG -name '*counter_collection.csv') $(find gpurun_out/pmcw_$CFG -name '*counter_collection.csv') $CFG > gpurun_out/traffic_$CFG.json
 python3 scripts/requests.py $(find gpurun_out/pmcr_$CFG -name '*counter_collection.csv') $CFG > gpurun_out/requests_$CFG.json
 python3 scripts/kstats.py $(find gpurun_out/prof_$CFG -name "*kernel_stats.csv") > gpurun_out/kstats_$CFG.txt; head -8 gpurun_out/kstats_$CFG.txt

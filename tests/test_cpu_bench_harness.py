@@ -163,3 +163,25 @@ def test_gather_packed_equal_shards_skip_padding():
         assert torch.equal(shard.gather_packed(x), x)
     finally:
         dist.destroy_process_group()
+
+
+def test_touched_lines_counts_128_byte_lines():
+    """bench.line_floor's line count (the engine's raw iovec export on a NULL base): known answers
+    -- a 300-byte contiguous run from 0 touches 3 lines; vector(4,1,32) of double (one element per
+    256 bytes) 4; vector(4,2,8) of double (16 B every 64 B, 256 B span) 2; two instances of a
+    type whose extent is half a line share lines; cfg2's halo: 2 x-face lines per row plus the y
+    rows and z planes, shared edge lines counted once."""
+    from ompi_amd import recipe as ER
+    D = ("basic", 16)
+    cases = [(("contig", 300, ("basic", 4)), 1, 3),
+             (("vector", 4, 1, 32, D), 1, 4),
+             (("vector", 4, 2, 8, D), 1, 2),
+             (("resized", ("contig", 8, D), 0, 64), 4, 2)]
+    for rec, count, want in cases:
+        assert bench.touched_lines(ER.build_committed(rec), count) == want, rec
+    rec, count, _ = bench.make_workload("cfg2")
+    n, lpr = 256, 256 * 8 // 128                    # 16 lines per 2 KiB row
+    x, y, z = 2 * n * n, 2 * n * lpr, 2 * n * lpr     # x: a line per row; y: 2 x 256 rows; z: 2 planes
+    xy, xz, yz, xyz = 2 * n * 2, 2 * n * 2, 2 * 2 * lpr, 2 * 2 * 2   # lines the faces share
+    per_field = x + y + z - xy - xz - yz + xyz        # inclusion-exclusion: 145,352
+    assert bench.touched_lines(ER.build_committed(rec), count) == count * per_field
