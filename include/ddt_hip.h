@@ -158,6 +158,15 @@ int ddt_type_info(const ddt_datatype_t *type, int64_t *out8);
  * flags (OPAL_DATATYPE_OPTIMIZED_RESTRICTED), out[3] = 1 once committed.  What
  * opt_desc_equiv.c:223-276 reads to recompute a corpus type's traits. */
 int ddt_type_commit_info(const ddt_datatype_t *type, int64_t *out4);
+/* MPI_Pack / MPI_Unpack count consolidation: ompi_datatype_consolidate_create
+ * (ompi/datatype/ompi_datatype_create_contiguous.c:119-180).  For count >= the threshold (MCA
+ * ompi_datatype_consolidate_threshold, default 250; ddt_tune("consolidate")) and a type with gaps,
+ * *out = contiguous(count, old) whose opt_desc is ONE loop of count over old's opt_desc,
+ * re-optimized on that loop only (opal_datatype_optimize_from_contiguous,
+ * opal_datatype_optimize.c:1480-1573) -- committed, owned by the caller; *out = NULL where the
+ * reference keeps (count, old).  Same packed bytes; its element boundaries (send positions, pack
+ * fragments) are the consolidated description's, as in MPI_Pack. */
+int ddt_type_consolidate(const ddt_datatype_t *old, size_t count, ddt_datatype_t **out);
 
 /* Import a committed Open MPI description: `desc` is the opal_datatype_t::opt_desc
  * (or ::desc) array of `used` dt_elem_desc_t entries, 32 bytes each, layout of

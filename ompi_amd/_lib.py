@@ -52,6 +52,7 @@ SIGNATURES = {
     "ddt_type_flags": (c_uint32, [c_void_p]),
     "ddt_type_info": (c_int, [c_void_p, P(c_int64)]),
     "ddt_type_commit_info": (c_int, [c_void_p, P(c_int64)]),
+    "ddt_type_consolidate": (c_int, [c_void_p, c_size_t, P(c_void_p)]),
     "ddt_type_from_opal_desc": (c_int, [c_void_p, c_size_t, c_size_t, c_ssize_t, c_ssize_t,
                                         c_ssize_t, c_ssize_t, P(c_void_p)]),
     "ddt_type_to_opal_desc": (c_int64, [c_void_p, c_void_p, c_size_t]),

@@ -1701,6 +1701,8 @@ int ddt_tune(const char *key, long value)
         tuning().stask = value < 0 ? 0 : value;
     else if (k == "spass")
         tuning().spass = value < 1 ? 1 : value;
+    else if (k == "consolidate")
+        tuning().consolidate = value;
     else if (k == "opt_growth")
         tuning().opt_growth = value < 0 ? 0 : (value > 1024 ? 1024 : value);
     else if (k == "opt_unroll_items")

@@ -203,6 +203,9 @@ struct ddt_datatype {
     // sets, lists and tables live in that device's HBM
     std::vector<std::shared_ptr<ddt::Plan>> plans;
     std::shared_ptr<ddt::ExtPlan> ext;   // external32 signature (lazy)
+    // a consolidated type (ddt_type_consolidate): its opt_desc, built from the old type's
+    // (opal_datatype_optimize_from_contiguous) rather than from its own desc
+    std::shared_ptr<const ddt::DescForm> opt_form;
     int64_t extent() const { return ub - lb; }
 };
 

@@ -183,8 +183,9 @@ using Lists = std::vector<std::shared_ptr<const IndexList>>;
 
 class Pass {
 public:
-    Pass(const std::vector<DescEntry> &d, uint32_t *flags, const Lists &lists, SealedCache &cache)
-        : d_(d), flags_(flags), lists_(lists), cache_(cache)
+    Pass(const std::vector<DescEntry> &d, uint32_t *flags, const Lists &lists, SealedCache &cache,
+         uint32_t mask = kOptimizeAll, bool top_only = false)
+        : d_(d), flags_(flags), lists_(lists), cache_(cache), mask_(mask), top_only_(top_only)
     {
     }
 
@@ -196,6 +197,8 @@ private:
     uint32_t *flags_;
     const Lists &lists_;
     SealedCache &cache_;
+    const uint32_t mask_;   // optimization_mask (opal_datatype.h:148-151)
+    const bool top_only_;   // top_loop_boundary_only: boundary expansion of top-level loops only
     std::vector<DescEntry> *o_ = nullptr;
     bool *reeval_ = nullptr;
     // the pending element is the fresh-start tail of the sealed entry at o_[tail_at_] (blocks up
@@ -564,7 +567,8 @@ bool Pass::absorb(DescEntry &last, const DescEntry &cur, bool inner)
     }
     const bool inline_pair = last.count > 1 && cur.count > 1 && last.blen <= kInlineBlocklen
                              && cur.blen <= kInlineBlocklen;
-    if (!inline_pair && last.disp + int64_t(last.count - 1) * last.extent + lbs == cur.disp) {
+    if (!inline_pair && (mask_ & kOptimizeFusion)   // (:1220-1223)
+        && last.disp + int64_t(last.count - 1) * last.extent + lbs == cur.disp) {
         // fuse the last block of `last` with the first block of `cur`
         const bool shrinks = last.count == 1 && cur.count == 1;
         const int64_t fext = last.extent + cur.extent;
@@ -719,13 +723,14 @@ void Pass::run(std::vector<DescEntry> &o, size_t &used, bool boundary, bool *exp
                     pos += L.count + 1;
                     continue;
                 }
-                if (boundary && loop_boundary(pos)) {
+                if (boundary && (mask_ & kOptimizeBoundary) && (!top_only_ || open.size() == 1)
+                    && loop_boundary(pos)) {   // (:1091-1101)
                     if (expanded)
                         *expanded = true;
                     pos += L.count + 1;
                     continue;
                 }
-                const uint32_t f = unroll_factor(pos);
+                const uint32_t f = (mask_ & kOptimizeUnroll) ? unroll_factor(pos) : 1;   // (:1112-1115)
                 if (f > 1) {
                     unrolled(pos, f);
                     pos += L.count + 1;
@@ -784,7 +789,38 @@ uint64_t ranges(const std::vector<DescEntry> &d, const std::vector<std::shared_p
 
 }  // namespace
 
-void optimize_desc(const DescForm &in, int64_t size, DescForm &out, uint32_t *flags)
+// ompi_datatype_desc_has_small_blocks (ompi_datatype_create_contiguous.c:52-70): a DATA entry of
+// blocklen < 9 (with count > 1 when `counted`); a sealed list stands for its optimized entries
+bool desc_has_small_blocks(const DescForm &d, bool counted)
+{
+    for (size_t i = 0; i < d.used; ++i) {
+        const DescEntry &e = d.e[i];
+        if (!is_data(e))
+            continue;
+        if (e.sealed >= 0) {
+            bool hit = false;
+            sealed_opt_entries(*d.lists[size_t(e.sealed)], e.type, e.flags, 0, e.sb, e.se,
+                               [&](const DescEntry &x) { hit |= x.blen < 9 && (!counted || x.count > 1); });
+            if (hit)
+                return true;
+        } else if (e.blen < 9 && (!counted || e.count > 1)) {
+            return true;
+        }
+    }
+    return false;
+}
+
+DescEntry loop_desc_entry(uint32_t loops, uint32_t items, int64_t extent, uint32_t flags)
+{
+    return loop_entry(loops, items, extent, flags);
+}
+
+DescEntry end_desc_entry(uint32_t items, int64_t first, uint64_t size, uint32_t flags)
+{
+    return end_entry(items, first, size, flags);
+}
+
+void optimize_desc(const DescForm &in, int64_t size, DescForm &out, uint32_t *flags, uint32_t mask, bool top_only)
 {
     // opal_datatype_optimize_short_restart (:1347-1478) from opal_datatype_commit (:1765-1777)
     const int64_t growth = tuning().opt_growth;   // clamped to 1024 (opal_datatype_module.c:370-372)
@@ -823,7 +859,7 @@ void optimize_desc(const DescForm &in, int64_t size, DescForm &out, uint32_t *fl
     };
     auto short_pass = [&](const std::vector<DescEntry> &src, DescForm &dst, bool boundary, bool *expanded,
                           bool *reevaluate) {
-        Pass p(src, flags, in.lists, cache);
+        Pass p(src, flags, in.lists, cache, mask, top_only);
         p.run(dst.e, dst.used, boundary, expanded, reevaluate);
         dst.lists = in.lists;
     };

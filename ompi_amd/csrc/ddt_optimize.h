@@ -55,7 +55,19 @@ bool build_opal_desc(const std::vector<Node> &nodes, int64_t size, DescForm &out
 // opal_datatype_commit's optimizer (opal_datatype_optimize_short_restart with
 // OPAL_DATATYPE_OPTIMIZE_ALL and the default tunables); *flags gets kRestricted when a region
 // was re-typed.  `out` shares `in`'s sealed lists.
-void optimize_desc(const DescForm &in, int64_t size, DescForm &out, uint32_t *flags);
+// optimization_mask bits (opal_datatype.h:148-151)
+constexpr uint32_t kOptimizeFusion = 0x1u, kOptimizeBoundary = 0x2u, kOptimizeUnroll = 0x4u;
+constexpr uint32_t kOptimizeAll = 0xFFFFFFFFu;
+// opal_datatype_optimize_short_restart (opal_datatype_optimize.c:1347-1478): `mask` removes
+// transforms, `top_only` limits loop-boundary expansion to top-level loops (the consolidation
+// path, opal_datatype_optimize_from_contiguous :1480-1573)
+void optimize_desc(const DescForm &in, int64_t size, DescForm &out, uint32_t *flags, uint32_t mask = kOptimizeAll,
+                   bool top_only = false);
+// ompi_datatype_consolidate_create (ompi_datatype_create_contiguous.c:119-180) -- see ddt_hip.h
+ddt_datatype *consolidate(const ddt_datatype *old, uint64_t count, int64_t threshold);
+bool desc_has_small_blocks(const DescForm &d, bool counted);
+DescEntry loop_desc_entry(uint32_t loops, uint32_t items, int64_t extent, uint32_t flags);
+DescEntry end_desc_entry(uint32_t items, int64_t first, uint64_t size, uint32_t flags);
 
 // Node tree of a committed description (the bridge's import, sealed lists passed through).
 bool nodes_from_desc(const DescForm &d, std::vector<Node> &out);

@@ -50,6 +50,8 @@ Tuning &tuning()
             preserve = (b == "0" || b == "false" || b == "no" || b == "f" || b == "n") ? 0 : 1;
         }
         v.opt_preserve = int(preserve);
+        if (const char *e = std::getenv("OMPI_MCA_datatype_consolidate_threshold"))
+            v.consolidate = std::atol(e);
         v.opt_growth = std::clamp<long>(v.opt_growth, 0, 1024);
         v.opt_unroll_items = std::max<long>(v.opt_unroll_items, 0);
         v.opt_unroll_bytes = std::max<long>(v.opt_unroll_bytes, 0);

@@ -56,6 +56,10 @@ struct Tuning {
     long opt_unroll_items = 8;
     long opt_unroll_bytes = 128;
     int opt_preserve = 1;         // 0: fused mixed-type regions travel as UINT1 (:586-588)
+    // MCA ompi_datatype_consolidate_threshold (ompi_datatype_module.c:527-532; environment
+    // OMPI_MCA_datatype_consolidate_threshold): the count from which ddt_type_consolidate builds
+    // the MPI_Pack / MPI_Unpack consolidated type (pack.c.in:118-125)
+    long consolidate = 250;
 };
 Tuning &tuning();
 // Synchronous host -> device copy on a library-private stream (capture-safe).

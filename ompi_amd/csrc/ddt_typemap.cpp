@@ -12,6 +12,7 @@
 #include "ddt_core.h"
 #include "ddt_hip.h"
 #include "ddt_optimize.h"
+#include "ddt_plan.h"
 
 using namespace ddt;
 
@@ -705,6 +706,83 @@ uint64_t snap_down_to_element(const ddt_datatype *t, uint64_t p)
 }  // namespace ddt
 
 // ================================================================ C ABI: construction
+namespace ddt {
+namespace {
+// GET_FIRST_NON_LOOP's displacement (opal_datatype_internal.h:282-294)
+int64_t first_elem_disp(const DescForm &d)
+{
+    for (size_t i = 0; i < d.used; ++i) {
+        const DescEntry &e = d.e[i];
+        if (e.flags & F_DATA)
+            return e.sealed >= 0 ? e.disp + d.lists[size_t(e.sealed)]->disp[e.sb] : e.disp;
+    }
+    return 0;
+}
+}  // namespace
+
+// ompi_datatype_consolidate_create (ompi_datatype_create_contiguous.c:119-180) and
+// opal_datatype_optimize_from_contiguous (opal_datatype_optimize.c:1480-1573)
+ddt_datatype *consolidate(const ddt_datatype *old, uint64_t count, int64_t threshold)
+{
+    if (count == 0 || int64_t(count) < threshold || count > uint64_t(INT64_MAX))
+        return nullptr;
+    if ((old->flags & F_NO_GAPS) || old->size == 0)
+        return nullptr;   // already contiguous across counts / nothing to move
+    if ((old->flags & F_CONTIGUOUS) && old->size == old->extent())
+        return nullptr;
+    // the old type's committed opt_desc (its desc when imported: that already is one)
+    DescForm body;
+    if (old->opt_form)
+        body = *old->opt_form;
+    else if (old->imported ? !build_opal_desc(old->desc, old->size, body) : !opt_desc_of(old, body))
+        return nullptr;
+    // ompi_datatype_consolidate_optimization_mask (:72-100)
+    uint32_t mask = kOptimizeAll;
+    if (body.used && desc_has_small_blocks(body, false)) {
+        mask &= ~kOptimizeBoundary;
+        if (desc_has_small_blocks(body, true))
+            mask &= ~kOptimizeFusion;
+    }
+    // the wrapping loop's count is 32 bits (:1504-1507); an empty body leaves the type as is
+    if (count < 2 || count > 0xffffffffull || body.used == 0)
+        return nullptr;
+    ddt_datatype_t *t = nullptr;
+    if (ddt_type_create_contiguous(size_t(count), old, &t) != DDT_SUCCESS || !t)
+        return nullptr;
+    const uint32_t loop_flags = (old->flags & 0x01FFu) & ~F_COMMITTED;
+    DescForm in;
+    in.lists = body.lists;
+    in.e.reserve(body.used + 3);
+    in.e.push_back(loop_desc_entry(uint32_t(count), uint32_t(body.used + 1), old->extent(), loop_flags));
+    in.e.insert(in.e.end(), body.e.begin(), body.e.begin() + long(body.used));
+    in.used = in.e.size();   // before the END_LOOP below: first_elem_disp skips the LOOP
+    const int64_t first = first_elem_disp(in);
+    in.e.push_back(end_desc_entry(uint32_t(body.used + 1), first, uint64_t(old->size), loop_flags));
+    in.used = in.e.size();
+    DescEntry fake = end_desc_entry(uint32_t(in.used), first, uint64_t(t->size), 0);
+    fake.flags = 0;
+    in.e.push_back(fake);   // opal_datatype_opt_set_fake_end_loop (:454-465)
+    auto out = std::make_shared<DescForm>();
+    uint32_t flags = 0;
+    optimize_desc(in, t->size, *out, &flags, mask, true);
+    t->opt_flags = flags | (old->opt_flags & kRestricted);
+    std::vector<Node> nodes;
+    if (nodes_from_desc(*out, nodes))
+        t->opt = std::move(nodes);
+    else
+        t->opt = t->desc;
+    normalize(t->opt);
+    t->opt_prefix.assign(1, 0);
+    for (const Node &n : t->opt)
+        t->opt_prefix.push_back(t->opt_prefix.back() + n.packed_bytes());
+    // opal_datatype_commit_description: committed, stack depth over desc and opt_desc
+    t->stack_depth = std::max(loop_depth(t->desc), loop_depth(*out));
+    t->flags |= F_COMMITTED;
+    t->opt_form = std::move(out);
+    return t;
+}
+}  // namespace ddt
+
 extern "C" {
 
 const ddt_datatype_t *ddt_predefined(int id)
@@ -1277,6 +1355,21 @@ int ddt_get_elements(const ddt_datatype_t *t, size_t ucount, size_t *count)
     return DDT_SUCCESS;
 }
 
+int ddt_type_consolidate(const ddt_datatype_t *old, size_t count, ddt_datatype_t **out)
+{
+    if (!old || !out)
+        return DDT_ERR_BAD_PARAM;
+    *out = nullptr;
+    if (!(old->flags & F_COMMITTED))
+        return DDT_ERR_NOT_COMMITTED;
+    try {
+        *out = consolidate(old, count, tuning().consolidate);
+    } catch (const std::bad_alloc &) {
+        return DDT_ERR_OUT_OF_RESOURCE;
+    }
+    return DDT_SUCCESS;
+}
+
 int ddt_type_commit_info(const ddt_datatype_t *t, int64_t *o)
 {
     if (!t || !o)
@@ -1604,7 +1697,9 @@ int64_t ddt_type_to_opal_opt_desc(const ddt_datatype_t *t, void *out, size_t cap
         return DDT_ERR_BAD_PARAM;
     std::vector<unsigned char> buf;
     uint32_t fl = t->opt_flags;
-    if (t->imported) {
+    if (t->opt_form) {
+        encode_desc(*t->opt_form, buf, true);
+    } else if (t->imported) {
         if (!export_nodes(t->desc, buf))
             return DDT_ERR_NOT_SUPPORTED;
     } else {

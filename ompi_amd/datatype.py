@@ -7,7 +7,7 @@ Function names and argument meaning follow ``ompi/datatype/ompi_datatype.h:217-2
 from __future__ import annotations
 
 import ctypes
-from typing import Sequence
+from typing import Optional, Sequence
 
 import numpy as np
 
@@ -77,6 +77,13 @@ class Datatype:
         out = (ctypes.c_int64 * 4)()
         check(lib().ddt_type_commit_info(self.handle, out), "ddt_type_commit_info")
         return dict(zip(("stack_depth", "bdt_used", "opt_flags", "committed"), list(out)))
+
+    def consolidate(self, count: int) -> "Optional[Datatype]":
+        """ompi_datatype_consolidate_create: contiguous(count, self) with the opt_desc of
+        opal_datatype_optimize_from_contiguous, committed; None where MPI_Pack keeps (count, self)."""
+        out = ctypes.c_void_p()
+        check(lib().ddt_type_consolidate(self.handle, count, ctypes.byref(out)), "ddt_type_consolidate")
+        return Datatype(out.value, owned=True, name=f"consolidated({count})") if out.value else None
 
     @property
     def size(self) -> int:

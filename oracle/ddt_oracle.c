@@ -1115,8 +1115,14 @@ static int64_t ox_depth(const ort_desc *d)
 }
 
 /* opal_datatype_optimize_short (:890-1295) on `in` (END_LOOP sentinel at in->e[in->used]) */
+/* optimization_mask bits (opal_datatype.h:148-151) */
+#define OX_ADJACENT_FUSION 0x1u
+#define OX_LOOP_BOUNDARY 0x2u
+#define OX_LOOP_UNROLL 0x4u
+#define OX_ALL 0xFFFFFFFFu
+
 static void ox_short(uint32_t *dflags, const ort_desc *in, ort_desc *o, int enable_boundary,
-                     int top_only, int *expanded, int *reevaluate)
+                     int top_only, uint32_t mask, int *expanded, int *reevaluate)
 {
     const ort_elem *d = in->e;
     const int64_t depth = ox_depth(in) + 2;
@@ -1175,14 +1181,15 @@ static void ox_short(uint32_t *dflags, const ort_desc *in, ort_desc *o, int enab
                 pos += L->count + 1;
                 continue;
             }
-            if (enable_boundary && (!top_only || sp == 0) && ox_loop_boundary(dflags, d, pos, o)) {
+            if (enable_boundary && (mask & OX_LOOP_BOUNDARY) && (!top_only || sp == 0)
+                && ox_loop_boundary(dflags, d, pos, o)) {   /* (:1091-1101) */
                 if (expanded)
                     *expanded = 1;
                 pos += L->count + 1;
                 continue;
             }
             {
-                const uint32_t f = ox_unroll_factor(d, pos);
+                const uint32_t f = (mask & OX_LOOP_UNROLL) ? ox_unroll_factor(d, pos) : 1;   /* (:1112-1115) */
                 if (f > 1) {
                     ox_emit_unrolled(o, d, pos, f);
                     pos += L->count + 1;
@@ -1241,7 +1248,8 @@ static void ox_short(uint32_t *dflags, const ort_desc *in, ort_desc *o, int enab
             /* fuse the last block of `last` with the first of `cur` (:1208-1268) */
             const int inline_pair = last.count > 1 && cur.count > 1 && last.blocklen <= OX_INLINE_BLOCKLEN
                                     && cur.blocklen <= OX_INLINE_BLOCKLEN;
-            if (!inline_pair && (last.disp + (int64_t) (last.count - 1) * last.extent + lbs) == cur.disp) {
+            if (!inline_pair && (mask & OX_ADJACENT_FUSION)   /* (:1220-1223) */
+                && (last.disp + (int64_t) (last.count - 1) * last.extent + lbs) == cur.disp) {
                 const int shrinks = last.count == 1 && cur.count == 1;
                 const int64_t fext = last.extent + cur.extent;
                 if (shrinks && reevaluate && inner[sp])
@@ -1306,14 +1314,14 @@ static void ox_free(ort_desc *d)
 }
 
 /* opal_datatype_optimize_short_restart (:1347-1478) */
-static void ox_restart(uint32_t *dflags, const ort_desc *in, ort_desc *out)
+static void ox_restart(uint32_t *dflags, const ort_desc *in, ort_desc *out, uint32_t mask, int top_only)
 {
     const int64_t limit = in->used * OX_GROWTH;
     const uint32_t init = *dflags;
     ort_desc cand, next, base;
     int expanded = 0, reeval = 0, any_expanded;
     *dflags = init;
-    ox_short(dflags, in, &cand, 1, 0, &expanded, &reeval);
+    ox_short(dflags, in, &cand, 1, top_only, mask, &expanded, &reeval);
     uint32_t cand_flags = *dflags;
     any_expanded = expanded;
     if (!expanded && !reeval) {
@@ -1326,7 +1334,7 @@ static void ox_restart(uint32_t *dflags, const ort_desc *in, ort_desc *out)
         if (cand.used > limit)
             break;
         *dflags = init | (cand_flags & ORT_RESTRICTED);
-        ox_short(dflags, &cand, &next, 1, 0, &nexp, &nre);
+        ox_short(dflags, &cand, &next, 1, top_only, mask, &nexp, &nre);
         const uint64_t nr = ox_ranges(next.e, 0, next.used);
         if (next.used > limit || (nexp && nr >= cand_ranges)) {
             ox_free(&next);
@@ -1347,12 +1355,12 @@ static void ox_restart(uint32_t *dflags, const ort_desc *in, ort_desc *out)
     }
     *dflags = init;
     reeval = 0;
-    ox_short(dflags, in, &base, 0, 0, NULL, &reeval);
+    ox_short(dflags, in, &base, 0, top_only, mask, NULL, &reeval);
     uint32_t base_flags = *dflags;
     while (reeval) {
         int nre = 0;
         *dflags = init | (base_flags & ORT_RESTRICTED);
-        ox_short(dflags, &base, &next, 0, 0, NULL, &nre);
+        ox_short(dflags, &base, &next, 0, top_only, mask, NULL, &nre);
         if (next.used > limit) {
             ox_free(&next);
             break;
@@ -1395,6 +1403,8 @@ static void ox_flatten(ort_type *t, const ort_elem *d, int64_t begin, int64_t en
     }
 }
 
+static void ort_finish_commit(ort_type *t);
+
 /* opal_datatype_commit (:1739-1782), then the carrier runs of opt_desc */
 void ort_commit(ort_type *t)
 {
@@ -1414,14 +1424,21 @@ void ort_commit(ort_type *t)
         memcpy(in.e, t->desc.e, (size_t) in.used * sizeof(ort_elem));
         in.e[in.used] = oe_end((uint32_t) in.used, first, (uint64_t) t->size, 0);
         in.e[in.used].flags = 0;
-        ox_restart(&t->opt_flags, &in, &t->opt);
+        ox_restart(&t->opt_flags, &in, &t->opt, OX_ALL, 0);
         free(in.e);
         if (t->opt.used) {
             ort_elem *s = &t->opt.e[t->opt.used];
             *s = oe_end((uint32_t) t->opt.used, first, (uint64_t) t->size, 0);
         }
-        ox_flatten(t, t->opt.e, 0, t->opt.used, 0);
     }
+    ort_finish_commit(t);
+}
+
+/* the carrier runs of opt_desc and their packed offsets */
+static void ort_finish_commit(ort_type *t)
+{
+    if (t->opt.used)
+        ox_flatten(t, t->opt.e, 0, t->opt.used, 0);
     t->opref = (int64_t *) malloc((size_t) (t->noruns + 1) * sizeof(int64_t));
     int64_t acc = 0;
     for (int64_t r = 0; r < t->noruns; r++) {
@@ -1441,6 +1458,68 @@ void ort_commit_info(ort_type *t, int64_t *out)
     out[1] = t->bdt_used;
     out[2] = t->desc.used;
     out[3] = t->opt.used;
+}
+
+/* ompi_datatype_consolidate_create (ompi/datatype/ompi_datatype_create_contiguous.c:119-180):
+ * MPI_Pack / MPI_Unpack of (count, old) with count >= threshold (ompi_datatype_consolidate_threshold,
+ * default 250) run on contiguous(count, old), whose opt_desc opal_datatype_optimize_from_contiguous
+ * (opal_datatype_optimize.c:1480-1573) builds as ONE loop of count over old's committed opt_desc,
+ * re-optimized with loop-boundary expansion on that outer loop only and the transforms
+ * ompi_datatype_consolidate_optimization_mask (:63-100) keeps.  NULL when the reference keeps old. */
+static int ox_small_blocks(const ort_desc *d, int counted)   /* ompi_datatype_desc_has_small_blocks (:52-70) */
+{
+    for (int64_t i = 0; i < d->used; i++)
+        if ((d->e[i].flags & ORT_FLAG_DATA) && d->e[i].blocklen < 9 && (!counted || d->e[i].count > 1))
+            return 1;
+    return 0;
+}
+
+ort_type *ort_consolidate(ort_type *old, int64_t count, int64_t threshold)
+{
+    if (count <= 0 || count < threshold)
+        return NULL;
+    if (old->flags & ORT_FLAG_NO_GAPS)
+        return NULL;
+    if (old->size == 0)
+        return NULL;
+    if ((old->flags & ORT_FLAG_CONTIGUOUS) && old->size == old->ub - old->lb)
+        return NULL;
+    ort_commit(old);
+    const ort_desc *body = old->opt.used ? &old->opt : &old->desc;
+    uint32_t mask = OX_ALL;
+    if (body->used && ox_small_blocks(body, 0)) {
+        mask &= ~OX_LOOP_BOUNDARY;
+        if (ox_small_blocks(body, 1))
+            mask &= ~OX_ADJACENT_FUSION;
+    }
+    /* opal_datatype_optimize_from_contiguous: a loop count must fit 32 bits */
+    if (count < 2 || count > (int64_t) UINT32_MAX || body->used == 0)
+        return NULL;
+    ort_type *t = ort_contiguous(count, old);
+    const int64_t extent = old->ub - old->lb;
+    const uint32_t loop_flags = (old->flags & ORT_ELEM_MASK) & ~ORT_FLAG_COMMITTED;
+    ort_desc in = {0};
+    in.used = body->used + 2;
+    in.cap = in.used + 1;
+    in.e = (ort_elem *) malloc((size_t) in.cap * sizeof(ort_elem));
+    in.e[0] = oe_loop((uint32_t) count, (uint32_t) (body->used + 1), extent, loop_flags);
+    memcpy(&in.e[1], body->e, (size_t) body->used * sizeof(ort_elem));
+    int64_t first = 0, k = 0;
+    while (in.e[k].type == OE_LOOP)   /* GET_FIRST_NON_LOOP */
+        k++;
+    first = in.e[k].disp;
+    in.e[in.used - 1] = oe_end((uint32_t) (body->used + 1), first, (uint64_t) old->size, loop_flags);
+    in.e[in.used] = oe_end((uint32_t) in.used, first, (uint64_t) t->size, 0);
+    in.e[in.used].flags = 0;
+    t->committed = 1;
+    t->opt_flags = 0;
+    ox_restart(&t->opt_flags, &in, &t->opt, mask, 1);
+    free(in.e);
+    t->opt_flags |= old->opt_flags & ORT_RESTRICTED;
+    if (t->opt.used)
+        t->opt.e[t->opt.used] = oe_end((uint32_t) t->opt.used, first, (uint64_t) t->size, 0);
+    ort_finish_commit(t);
+    return t;
 }
 
 /* opt_desc entry i (i == used: the END_LOOP sentinel): flags, type, count|items, loops,

@@ -59,6 +59,7 @@ def lib():
             "ort_desc_used": (i64, [vp]), "ort_desc_at": (None, [vp, i64, vp]),
             "ort_commit_info": (None, [vp, vp]),
             "ort_optimize_config": (None, [i64, i64, i64, i]),
+            "ort_consolidate": (vp, [vp, i64, i64]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -213,6 +214,13 @@ def basic(type_id: int) -> OType:
 
 def contiguous(count, old):
     return OType(lib().ort_contiguous(count, old.h))
+
+
+def consolidate(old, count, threshold=250):
+    """ompi_datatype_consolidate_create: contiguous(count, old) with the opt_desc of
+    opal_datatype_optimize_from_contiguous, or None where the reference keeps (count, old)."""
+    h = lib().ort_consolidate(old.h, count, threshold)
+    return OType(h) if h else None
 
 
 def vector(count, blen, stride, old):

@@ -1431,3 +1431,47 @@ def test_xcd_task_mappings(device, xcd, xchunk):
             _roundtrip(R.Built(rec), 3, device, 77 + i)
     finally:
         L.ddt_tune(b"reset", 0)
+
+
+# ---------------------------------------------------------------- MPI_Pack count consolidation
+@pytest.mark.parametrize("rec,count", [
+    (("vector", 1024, 1, 2, ("basic", 16)), 2048),                                         # App. A cfg1
+    (("resized", ("struct", [1, 3], [0, 8], [("basic", 16), ("basic", 6)]), 0, 32), 4096),  # cfg5's record
+    (("hvector", 3, 2, 40, ("contig", 2, ("basic", 15))), 300),
+])
+def test_consolidated_type_packs_the_same_stream(device, rec, count):
+    """ompi_datatype_consolidate_create (ompi_datatype_create_contiguous.c:119-180): MPI_Pack of
+    (count, type) runs (1, consolidated); the GPU packs and unpacks both to the same bytes, and
+    fragments of the consolidated type stop on its own description's elements (oracle)."""
+    import torch
+    import ompi_amd
+    from . import oracle as O
+    b = R.Built(rec)
+    e = b.engine()
+    c = e.consolidate(count)
+    assert c is not None
+    info = b.o.info()
+    size = count * info["size"]
+    span, origin = R.layout(info, count)
+    host = R.fill(span, 0x33)
+    user = _dev(host, device)
+    p1 = torch.zeros(size, dtype=torch.uint8, device=device)
+    p2 = torch.zeros(size, dtype=torch.uint8, device=device)
+    assert ompi_amd.pack(user.data_ptr() + origin, count, e, p1, size, 0) == size
+    assert ompi_amd.pack(user.data_ptr() + origin, 1, c, p2, size, 0) == size
+    assert torch.equal(p1, p2)
+    oc = O.consolidate(b.o, count)
+    conv = ompi_amd.Convertor().prepare_for_send(c, 1, user.data_ptr() + origin)
+    pos, rc, frag = 0, 0, 4099
+    p2.zero_()
+    while rc == 0:
+        rc, _, md = conv.pack([(p2.data_ptr() + pos, min(frag, size - pos))])
+        assert pos + md == oc.set_position(1, min(pos + frag, size), send=True) or pos + md == size
+        pos += md
+    assert pos == size and torch.equal(p1, p2)
+    out = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
+    ompi_amd.unpack(p1, size, 0, out.data_ptr() + origin, 1, c)
+    ref = torch.full((span,), 0xA5, dtype=torch.uint8, device=device)
+    ompi_amd.unpack(p1, size, 0, ref.data_ptr() + origin, count, e)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
