@@ -720,6 +720,9 @@ int64_t first_elem_disp(const DescForm &d)
 }
 }  // namespace
 
+void consolidate_into(ddt_datatype *t, const ddt_datatype *old, const DescForm &body, uint64_t count,
+                      uint32_t mask);
+
 // ompi_datatype_consolidate_create (ompi_datatype_create_contiguous.c:119-180) and
 // opal_datatype_optimize_from_contiguous (opal_datatype_optimize.c:1480-1573)
 ddt_datatype *consolidate(const ddt_datatype *old, uint64_t count, int64_t threshold)
@@ -749,6 +752,18 @@ ddt_datatype *consolidate(const ddt_datatype *old, uint64_t count, int64_t thres
     ddt_datatype_t *t = nullptr;
     if (ddt_type_create_contiguous(size_t(count), old, &t) != DDT_SUCCESS || !t)
         return nullptr;
+    try {
+        consolidate_into(t, old, body, count, mask);
+    } catch (...) {
+        (void) ddt_type_destroy(&t);   // the new type is the caller's only once complete
+        throw;
+    }
+    return t;
+}
+
+void consolidate_into(ddt_datatype *t, const ddt_datatype *old, const DescForm &body, uint64_t count,
+                      uint32_t mask)
+{
     const uint32_t loop_flags = (old->flags & 0x01FFu) & ~F_COMMITTED;
     DescForm in;
     in.lists = body.lists;
@@ -779,7 +794,6 @@ ddt_datatype *consolidate(const ddt_datatype *old, uint64_t count, int64_t thres
     t->stack_depth = std::max(loop_depth(t->desc), loop_depth(*out));
     t->flags |= F_COMMITTED;
     t->opt_form = std::move(out);
-    return t;
 }
 }  // namespace ddt
 
