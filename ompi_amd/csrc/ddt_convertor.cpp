@@ -1684,7 +1684,7 @@ int ddt_tune(const char *key, long value)
     else if (k == "sunroll")
         tuning().sunroll = value >= 16 ? 16 : (value >= 8 ? 8 : 4);
     else if (k == "sseg")
-        tuning().sseg = (value == 128 || value == 32) ? value : 64;
+        tuning().sseg = (value == 128 || value == 64 || value == 32) ? value : 1;
     else if (k == "schunk")
         tuning().schunk = value == 2 ? 2 : 1;
     else if (k == "sorted_commit")

@@ -370,18 +370,18 @@ SortedList *sorted_build(Plan &P, hipStream_t stream)
     const uint64_t min_blocks = knob > 0 ? uint64_t(knob) : (1ull << 20);
     const uint64_t g = X.disp_gcd | (X.len.empty() ? X.ulen : X.len_gcd);
     uint64_t esz = 0, ne = 0;
-    uint64_t segb = (tuning().sseg == 128 || tuning().sseg == 32) ? uint64_t(tuning().sseg) : 64;
+    uint64_t segb = (tuning().sseg == 128 || tuning().sseg == 64 || tuning().sseg == 32) ? uint64_t(tuning().sseg) : 1;
     for (int pass = 0; pass < 2 && !esz; ++pass) {
         for (uint64_t e = 16; e >= 4 && !esz; e /= 2) {
             const uint64_t ch = (128ull << 10) / e;
             // buckets <= the pass-1 LDS tables (MAXNB = 4096 = 2 * CH / SEG at 64-byte segments)
-            if (g % e == 0 && X.total / e <= ch * std::min<uint64_t>(4096, 2 * ch / (segb / e))) {
+            if (g % e == 0 && X.total / e <= ch * std::min<uint64_t>(4096, 2 * ch / ((segb == 1 ? 64 : segb) / e))) {
                 esz = e;
                 ne = X.total / e;
             }
         }
         if (!esz)
-            segb = 64;   // too many elements for the longer segments: the 64-byte form
+            segb = segb == 1 ? 1 : 64;   // too many elements for the longer segments: the 64-byte form
     }
     if (!esz || nblk < min_blocks || X.total > 32 * nblk || !D.disp32) {
         P.sorted_state = -1;

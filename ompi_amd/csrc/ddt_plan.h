@@ -43,7 +43,8 @@ struct Tuning {
     long hd_grid_pack = 0;   // the same cap for a pack writing pinned host memory
     long sunroll = 16;    // address-ordered engine: pack 1 elements per thread in flight (4, 8, 16)
     long s2unroll = 8;    // the same for its unpack pass 2' 
-    long sseg = 64;       // address-ordered engine: U segment bytes (32, 64 or 128), read at plan build
+    long sseg = 1;        // address-ordered engine: U run padding, read at plan build: 1 = none (runs end
+                          // to end, pass-1 chunks in XCD slabs; r5) or whole 32/64/128-byte segments
     long schunk = 1;      // address-ordered engine: 2 = half-size chunks, two pass-1 workgroups per
                           // CU (read at plan build)
     int sorted_commit = 1;   // build the address-ordered tables at commit / bridge import (1) or

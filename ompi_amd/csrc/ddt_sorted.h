@@ -18,6 +18,7 @@ struct SortedList {
     uint32_t cdiv = 1;       // 2: half-size chunks, two pass-1 workgroups per CU
     uint32_t seg = 0;        // elements per segment of U
     uint32_t segb = 64;      // segment bytes: 64 or 128
+    bool unpadded = false;   // runs packed end to end in U (segb = the lanes per run only)
     uint32_t nc = 0, nb = 0; // chunks, buckets
     uint64_t slots = 0;      // U slots, runs padded to whole segments
     uint64_t dev_bytes = 0;  // device bytes held (tables + U)

@@ -16,8 +16,10 @@
 //            lds[upos[s]] = U[s];  packed[k*RG + t] = lds[t]
 //   unpack is the same two passes reversed.
 //
-// U is bucket-major, each (chunk, bucket) run padded to a 64-byte segment so every U
-// store is a whole segment.  CH = RG = 128 KiB / element size, so the LDS image of a
+// U is bucket-major, the (chunk, bucket) runs end to end (round 5; they were padded to whole
+// 64-byte segments before: 43 % of U was padding at cfg4).  Neighbouring chunks' runs share
+// segments, so pass 1 deals its chunks to the XCDs in contiguous slabs and both halves of a
+// shared segment meet in one L2.  CH = RG = 128 KiB / element size, so the LDS image of a
 // chunk or a bucket is 128 KiB (gfx950: 160 KiB per CU).  The plan (A, SL, run tables,
 // upos) is built once on the device from the list's displacements: a bitmap of the
 // touched elements gives each element its address rank by popcount, and a repeated element
@@ -50,11 +52,11 @@ template <> struct Elem<16> { using T = u32x4; };
 constexpr int PT = 1024;               // threads per pass workgroup (16 wave64)
 constexpr int BT = 256;                // threads per build workgroup
 constexpr uint32_t LDS_BYTES = 128u << 10;
-// U runs are padded to whole segments of SEGB bytes (a plan's choice, SortedList::segb): 64 B
-// (round 1; 32 B segments: less padding, but cfg4 1461 -> 1512 us) or 128 B (round 2: half the
-// memory requests of the scattered run writes and reads, more padding; ddt_tune("sseg")).
-// 32 B is kept for half chunks (round 4): their runs are half as long, so 32-byte segments
-// pad them as little as 64-byte segments pad full-chunk runs.
+// SEGB bytes of a run move per lane group (SEG lanes, SortedList::segb).  U runs are unpadded
+// by default (ddt_tune("sseg") 1, round 5: cfg4 1399 -> 1362 us per step) or padded to whole
+// SEGB segments (sseg 32 / 64 / 128): 64 B (round 1; 32 B: less padding, but cfg4 1461 -> 1512
+// us) or 128 B (round 2: half the memory requests of the scattered run writes and reads, more
+// padding).
 constexpr uint32_t SEG_DEFAULT = 64;
 constexpr uint16_t PAD = 0xFFFF;       // upos of a padding slot
 
@@ -67,6 +69,19 @@ constexpr uint32_t POL_USER_NTL = 8;   // pack 1: user-side loads non-temporal
 // of pass 1 / 1' (the address-ordered gather or scatter), or its run phase (emit or load runs)
 constexpr uint32_t POL_SKIP_USER = 16;
 constexpr uint32_t POL_SKIP_RUNS = 32;
+// set by run() for a plan built with sseg = 1 (the default): U runs end to end, no padding slots
+constexpr uint32_t POL_UNPADDED = 64;
+// pass 1 / 1': chunks dealt to the XCDs in contiguous slabs (workgroups are dealt round-robin
+// over the 8 XCDs), so the runs of neighbouring chunks -- adjacent in U -- are written into one L2
+constexpr uint32_t POL_XCD_SLAB = 128;
+
+__device__ __forceinline__ uint32_t chunk_of(uint32_t b, uint32_t n, uint32_t pol)
+{
+    if (!(pol & POL_XCD_SLAB))
+        return b;
+    const uint32_t x = b & 7u, i = b >> 3, per = n >> 3, rem = n & 7u;
+    return x * per + (x < rem ? x : rem) + i;   // a bijection on [0, n)
+}
 
 template <typename T> __device__ __forceinline__ T ldp(const T *p, bool nt)
 {
@@ -256,7 +271,7 @@ __device__ __forceinline__ void stage_tables(const uint16_t *__restrict__ off16,
 // pack pass 1, second phase: the chunk image's runs out to U, bucket by bucket
 template <int E, int SEGB, int NT>
 __device__ __forceinline__ void emit_runs(const typename Elem<E>::T *lds, const uint16_t *toff, const uint32_t *tub,
-                                          uint8_t *__restrict__ U, uint32_t nb, bool nts)
+                                          uint8_t *__restrict__ U, uint32_t nb, bool nts, bool unpadded)
 {
     using T = typename Elem<E>::T;
     constexpr uint32_t SEG = SEGB / E;
@@ -264,7 +279,7 @@ __device__ __forceinline__ void emit_runs(const typename Elem<E>::T *lds, const 
     const uint32_t sub = threadIdx.x / SEG, lane = threadIdx.x % SEG;
     for (uint32_t k = sub; k < nb; k += NT / SEG) {
         const uint32_t o = toff[k], cn = toff[k + 1] - o;
-        const uint32_t b = tub[k], pn = (cn + SEG - 1) / SEG * SEG;
+        const uint32_t b = tub[k], pn = unpadded ? cn : (cn + SEG - 1) / SEG * SEG;
         for (uint32_t q = lane; q < pn; q += SEG)
             stp(&dst[b + q], lds[o + q], nts);   // padding slots carry a neighbour's bytes: whole segments
     }
@@ -287,7 +302,7 @@ __global__ __launch_bounds__(PT / CDIV) void k_pack1(const uint8_t *__restrict__
     __shared__ T lds[CH + SEG];
     __shared__ uint16_t toff[MAXNB / CDIV + 1];
     __shared__ uint32_t tub[MAXNB / CDIV];
-    const uint32_t c = blockIdx.x, j0 = c * CH;
+    const uint32_t c = chunk_of(blockIdx.x, gridDim.x, pol), j0 = c * CH;
     const uint32_t m = min(CH, n - j0);
     stage_tables<NT>(off16, ub, c, nb, m, toff, tub);
     const T *src = reinterpret_cast<const T *>(user);
@@ -311,7 +326,7 @@ __global__ __launch_bounds__(PT / CDIV) void k_pack1(const uint8_t *__restrict__
                 lds[s[q]] = v[q];
     }
     __syncthreads();
-    emit_runs<E, SEGB, NT>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, nts);
+    emit_runs<E, SEGB, NT>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, nts, pol & POL_UNPADDED);
 }
 
 // pack pass 2: the bucket's runs scatter into LDS by destination, then stream out
@@ -456,7 +471,7 @@ __global__ __launch_bounds__(PT / CDIV) void k_unpack1(uint8_t *__restrict__ use
     __shared__ T lds[CH];
     __shared__ uint16_t toff[MAXNB / CDIV + 1];
     __shared__ uint32_t tub[MAXNB / CDIV];
-    const uint32_t c = blockIdx.x, j0 = c * CH;
+    const uint32_t c = chunk_of(blockIdx.x, gridDim.x, pol), j0 = c * CH;
     const uint32_t m = min(CH, n - j0);
     stage_tables<NT>(off16, ub, c, nb, m, toff, tub);
     __syncthreads();
@@ -552,11 +567,12 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
     n = n_;
     esz = esz_;
     segb = (segb_ == 128 || segb_ == 32) ? segb_ : SEG_DEFAULT;
+    unpadded = segb_ == 1;
     rg = LDS_BYTES / esz;
     nb = (n + rg - 1) / rg;
     cdiv = (cdiv_ == 2 && nb <= MAXNB / 2) ? 2 : 1;   // half chunks: the tables must fit half the LDS
     ch = rg / cdiv;
-    seg = segb / esz;
+    seg = unpadded ? 1 : segb / esz;
     nc = (n + ch - 1) / ch;
     uint32_t shift = 0;
     while ((1u << shift) < esz)
@@ -675,6 +691,8 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol
     const dim3 gc(nc), gb(nb), blk(PT), blk1(PT / cdiv);
     const AddrList al{A, A16, Abase};
     uint8_t *u8 = static_cast<uint8_t *>(U);
+    if (unpadded)   // r5 A/B (profiles/r5_ab_cfg4_unpadded.jsonl): the slabs pay only without padding
+        pol |= POL_UNPADDED | POL_XCD_SLAB;
 #define DDT_SORTED_PASS1(E, SB, K, CD)                                                                          \
     if (dir == 0)                                                                                               \
         hipLaunchKernelGGL((k_pack1<E, SB, K, CD>), gc, blk1, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol); \

@@ -1,8 +1,9 @@
 """CPU replay of the address-ordered index-list engine (ompi_amd/csrc/ddt_sorted.hip).
 
 The device builds its tables with atomics; this replays the same table definitions and
-the two passes of pack and unpack with numpy index arithmetic, including the padded
-64-byte segments that read a neighbouring run's LDS bytes, and checks that every packed
+the two passes of pack and unpack with numpy index arithmetic, with the runs end to end in U
+(the default since round 5) and padded to 64-byte segments that read a neighbouring run's LDS
+bytes, and checks that every packed
 element equals the direct gather user[disp[i]] (type-map order) and that unpack restores
 exactly the touched elements.  It pins the layout math the kernels share, not the kernels.
 """
@@ -91,11 +92,12 @@ def unpack(packed, user, T, n, ch, seg):
         user[T["A"][j0:j0 + m]] = lds[T["SL"][j0:j0 + m]]
 
 
+@pytest.mark.parametrize("padded", [False, True])
 @pytest.mark.parametrize("esz,n,density", [(4, 3 * 512 + 77, 4), (8, 2000, 1), (16, 513, 64), (4, 5, 3)])
-def test_sorted_engine_replay(esz, n, density):
+def test_sorted_engine_replay(esz, n, density, padded):
     # the device uses CH = 128 KiB / esz; a smaller CH keeps many chunks/buckets here
     ch = {4: 512, 8: 256, 16: 128}[esz]
-    seg = 64 // esz
+    seg = 64 // esz if padded else 1
     rng = np.random.default_rng(esz * 7 + n)
     a = rng.permutation(density * n)[:n].astype(np.int64)
     user = rng.integers(1, 2 ** 31, density * n + 1).astype(np.int64)
@@ -120,3 +122,20 @@ def test_sorted_engine_size_limits():
         assert nmax / runs >= seg / 2
     # BASELINE config 4 (64 Mi floats) qualifies: 16 elements (one segment) per run
     assert (64 << 20) <= 2 * (32 << 10) ** 2 // 16
+
+
+def chunk_of(b, n):
+    """ddt_sorted.hip chunk_of with POL_XCD_SLAB: workgroup b (dealt to XCD b % 8) -> chunk."""
+    x, i, per, rem = b & 7, b >> 3, n >> 3, n & 7
+    return x * per + min(x, rem) + i
+
+
+@pytest.mark.parametrize("n", list(range(1, 70)) + [2047, 2048, 2049, 4096 + 5])
+def test_xcd_slab_chunk_map_is_a_bijection(n):
+    """Every chunk is moved exactly once, and the chunks of one XCD (b % 8 equal) form one
+    contiguous slab in workgroup order."""
+    cs = [chunk_of(b, n) for b in range(n)]
+    assert sorted(cs) == list(range(n))
+    for x in range(8):
+        mine = [chunk_of(b, n) for b in range(x, n, 8)]
+        assert mine == list(range(mine[0], mine[0] + len(mine))) if mine else True

@@ -940,7 +940,37 @@ def test_sorted_list_engine_half_chunks(device, sorted_from, esz, count, density
         assert st["sorted"] == 1 and st["chunks"] == (n + ch // 2 - 1) // (ch // 2), st
     finally:
         L.ddt_tune(b"schunk", 1)
-        L.ddt_tune(b"sseg", 64)
+        L.ddt_tune(b"sseg", 1)
+
+
+@pytest.mark.parametrize("spol", [0, 128])
+@pytest.mark.parametrize("schunk", [1, 2])
+@pytest.mark.parametrize("esz,count,density", [(4, 1, 4), (8, 2, 5), (16, 1, 4), (4, 1, 64)])
+def test_sorted_list_engine_unpadded(device, sorted_from, esz, count, density, schunk, spol):
+    """U runs end to end (ddt_tune sseg 1): runs of neighbouring chunks share U segments, so
+    two workgroups write parts of one segment; bit-exact both ways, full and half chunks, chunks
+    dealt round-robin or in XCD slabs (spol 128)."""
+    import ompi_amd
+    L = ompi_amd.lib()
+    sorted_from(1)
+    L.ddt_tune(b"schunk", schunk)
+    L.ddt_tune(b"sseg", 1)
+    L.ddt_tune(b"spol", spol)
+    try:
+        rng = np.random.default_rng(esz * 7000 + count * 10 + density)
+        ch = (128 << 10) // esz
+        n = 3 * ch + 1237
+        unit = {4: ("basic", 15), 8: ("basic", 16), 16: ("basic", 16)}[esz]
+        per = esz // (8 if esz == 16 else esz)
+        disps = (rng.permutation(density * n)[:n] * per).astype(np.int64)
+        b = R.Built(("indexed_block", per, disps.tolist(), unit))
+        _roundtrip(b, count, device, 13 + esz)
+        st = b.engine().engine_info()
+        assert st["sorted"] == 1, st
+    finally:
+        L.ddt_tune(b"schunk", 1)
+        L.ddt_tune(b"sseg", 1)
+        L.ddt_tune(b"spol", 0)
 
 
 @pytest.mark.parametrize("name", ["contig16", "adv_mixed_promote", "one_contig_instance"])
