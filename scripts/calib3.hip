@@ -41,27 +41,34 @@ __global__ __launch_bounds__(256) void flush(const u32x4 *__restrict__ p, size_t
         sink[threadIdx.x] = acc;
 }
 
-// x element t: row r = t % (N*N), face s = (t / (N*N)) % 2, field f = t / (2*N*N)
+// x element t: row r = t % (N*N), face s = (t / (N*N)) % 2, field f = t / (2*N*N); PAIR: the two
+// faces' elements of one row adjacent (s = t % 2), so a row's two lines are touched together
+template <bool PAIR = false>
 __device__ __forceinline__ size_t xoff(size_t t)
 {
+    if (PAIR) {
+        const size_t s = t & 1, r = (t >> 1) % (N * N), f = t / (2 * N * N);
+        return f * FIELD + r * ROW + s * (ROW - E);
+    }
     const size_t r = t % (N * N), s = (t / (N * N)) & 1, f = t / (2 * N * N);
     return f * FIELD + r * ROW + s * (ROW - E);
 }
 
+template <bool PAIR = false>
 __global__ __launch_bounds__(256) void xgather(const uint8_t *__restrict__ u, uint64_t *__restrict__ p)
 {
     const size_t t = size_t(blockIdx.x) * 256 + threadIdx.x;
     if (t < NX)
-        __builtin_nontemporal_store(*reinterpret_cast<const uint64_t *>(u + xoff(t)), p + t);
+        __builtin_nontemporal_store(*reinterpret_cast<const uint64_t *>(u + xoff<PAIR>(t)), p + t);
 }
 
-template <bool NTS>
+template <bool NTS, bool PAIR = false>
 __global__ __launch_bounds__(256) void xscatter(uint8_t *__restrict__ u, const uint64_t *__restrict__ p)
 {
     const size_t t = size_t(blockIdx.x) * 256 + threadIdx.x;
     if (t >= NX)
         return;
-    uint64_t *q = reinterpret_cast<uint64_t *>(u + xoff(t));
+    uint64_t *q = reinterpret_cast<uint64_t *>(u + xoff<PAIR>(t));
     const uint64_t v = __builtin_nontemporal_load(p + t);
     if (NTS)
         __builtin_nontemporal_store(v, q);
@@ -117,8 +124,9 @@ int main(int argc, char **argv)
     hipEvent_t ev[8];
     for (auto &e : ev)
         CHK(hipEventCreate(&e));
-    // op codes: 0 x gather, 1 x scatter nt, 2 x scatter plain, 3 yz pack, 4 yz unpack
-    const char *oname[5] = {"xg", "xs_nt", "xs_plain", "yzp", "yzu"};
+    // op codes: 0 x gather, 1 x scatter nt, 2 x scatter plain, 3 yz pack, 4 yz unpack; 5-7 the
+    // x kernels with a row's two face elements adjacent
+    const char *oname[8] = {"xg", "xs_nt", "xs_plain", "yzp", "yzu", "xg_pair", "xs_nt_pair", "xs_plain_pair"};
     struct Seq { const char *name; int n; int op[4]; };
     const Seq seqs[] = {
         {"x_alone_nt", 2, {0, 1}},
@@ -129,6 +137,9 @@ int main(int argc, char **argv)
         {"x_pack_last_nt", 4, {3, 0, 4, 1}},  // x last in both passes
         {"x_inner_plain", 4, {3, 0, 2, 4}},
         {"x_first_plain", 4, {0, 3, 2, 4}},
+        {"x_alone_nt_pair", 2, {5, 6}},
+        {"x_alone_plain_pair", 2, {5, 7}},
+        {"x_first_nt_pair", 4, {5, 3, 6, 4}},
     };
     for (const Seq &s : seqs) {
         float acc[4] = {0, 0, 0, 0}, tot = 0;
@@ -137,10 +148,13 @@ int main(int argc, char **argv)
             CHK(hipEventRecord(ev[0], nullptr));
             for (int i = 0; i < s.n; ++i) {
                 switch (s.op[i]) {
-                case 0: hipLaunchKernelGGL(xgather, gx, b, 0, nullptr, u, px); break;
+                case 0: hipLaunchKernelGGL(xgather<false>, gx, b, 0, nullptr, u, px); break;
                 case 1: hipLaunchKernelGGL(xscatter<true>, gx, b, 0, nullptr, u, px); break;
                 case 2: hipLaunchKernelGGL(xscatter<false>, gx, b, 0, nullptr, u, px); break;
                 case 3: hipLaunchKernelGGL(yz<0>, gyz, b, 0, nullptr, u, pyz); break;
+                case 5: hipLaunchKernelGGL(xgather<true>, gx, b, 0, nullptr, u, px); break;
+                case 6: hipLaunchKernelGGL((xscatter<true, true>), gx, b, 0, nullptr, u, px); break;
+                case 7: hipLaunchKernelGGL((xscatter<false, true>), gx, b, 0, nullptr, u, px); break;
                 default: hipLaunchKernelGGL(yz<1>, gyz, b, 0, nullptr, u, pyz); break;
                 }
                 CHK(hipEventRecord(ev[i + 1], nullptr));
