@@ -333,6 +333,13 @@ int ddt_type_cache_info(const ddt_datatype_t *type, int64_t *out4);
  * bytes, blocks kept for graphs, blocks in use]. */
 int ddt_trim(void);
 int ddt_pool_info(int64_t *out6);
+/* Argument-free launches: a descriptor set launched twice in a row on the same buffers is
+ * bound to one of 8 launch records per direction in device memory, and its later launches on
+ * those buffers take no kernel arguments (HIP writes device-resident kernel arguments across
+ * PCIe: ~2.9 us of host time per launch with arguments, 0.7 us without).  ddt_slot_info: out4 =
+ * [pack slots bound, unpack slots bound (current device), binds so far, argument-free launches
+ * so far].  ddt_tune("slots", 0) turns them off. */
+int ddt_slot_info(int64_t *out4);
 /* ---- introspection for the CPU test-suite (no data movement; never used by pack/unpack) ----
  * ddt_type_plan_leaves: serialises the plan's leaf streams as int64 records
  *   [kind, blen, src_off, dst_off, ndim, list_leaf_index, (cnt, sstr, dstr) x ndim] and returns

@@ -130,6 +130,10 @@ void recycle(Plan &P, Retired &r)   // P.mu held
     for (hipEvent_t e : S.late)
         (void) hipEventDestroy(e);
     S.late.clear();
+    if (S.slot >= 0) {   // every launch of the set has passed: its record is free
+        slot_release(S.slot_dev, S.slot >> 8, S.slot & 15, S.slot_gen, nullptr);
+        S.slot = -1;
+    }
     if (S.d_items) {
         P.spare.push_back({S.d_items, S.items.size() * sizeof(Item)});
         S.d_items = nullptr;
@@ -341,6 +345,8 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         assign_tasks(S->items, same_layout ? 0 : dir);
         stream_policy(S->items);
         S->ntasks = total_tasks(S->items);
+        for (const Item &it : S->items)
+            S->bytes += it.kind == ITEM_FRAG ? it.nbytes : (it.u1 - it.u0) * it.U;
         for (Item &it : S->items)
             it.slab = use_slab(it) ? (tuning().xchunk > 0 ? uint32_t(tuning().xchunk) : SLAB_FULL) : 0;
         S->all_dense = !S->items.empty();
@@ -418,6 +424,8 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     // across PCIe, and a 528-byte block costs 2.6 us of host time per launch against 0.7 us
     // for a pointer (scripts/hostbench.cpp, profiles/r1_hostbench.log).
     Item *d_items = nullptr;
+    int slot_k = -1;
+    uint32_t slot_gen = 0;
     {
         std::lock_guard<std::mutex> g(P.mu);
         if (S->inline_ok && !S->retired && ++S->uses >= 2 && !S->d_items && tuning().ptr) {
@@ -432,11 +440,40 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         }
         d_items = (S->inline_ok && (!tuning().ptr || S->retired)) ? nullptr : S->d_items;
         if (d_items) {
-            if (capturing(stream)) {
+            const bool cap = capturing(stream);
+            if (cap) {
                 // the graph keeps this pointer: never recycle it before the plan goes
                 if (S->retired && !S->pinned)
                     pin_retired(P, S);
                 S->pinned = true;
+            } else if (tuning().slots && grid_cap == 0 && !S->all_dense && !S->has_lists && !S->retired
+                       && S->bytes <= uint64_t(tuning().slot_max_kb) << 10) {
+                // an argument-free launch (ddt_move.hip.h, ddt_move_slot_kernel): a set bound to
+                // a slot for these buffers and this direction; a set launched twice in a row on
+                // the same buffers binds one (its record is in device memory before this launch).
+                // Small launches only: a slot kernel's workgroups first load the record (one more
+                // dependent load than arguments preloaded into registers), which a large launch of
+                // latency-bound gathers pays (the halo's 48 MiB pack 67.6 -> 74.8 us), while the host's
+                // 2.2 us saving only matters where the kernel is as short as a launch
+                const int fam = dir << 8;
+                if (S->slot >= 0 && (S->slot & ~15) == fam && S->slot_ubase == ubase && S->slot_pbase == pbase) {
+                    slot_k = S->slot & 15;
+                    slot_gen = S->slot_gen;
+                } else if (S->slot < 0 && S->last_ubase == ubase && S->last_pbase == pbase) {
+                    const LaunchRec rec{uint64_t(uintptr_t(d_items)), ubase, pbase, uint32_t(S->items.size()),
+                                        S->ntasks};
+                    const int k = slot_bind(P.device, dir, rec, &S->slot_gen);
+                    if (k >= 0) {
+                        S->slot = fam | k;
+                        S->slot_dev = P.device;
+                        S->slot_ubase = ubase;
+                        S->slot_pbase = pbase;
+                        slot_k = k;
+                        slot_gen = S->slot_gen;
+                    }
+                }
+                S->last_ubase = ubase;
+                S->last_pbase = pbase;
             }
             if (std::find(S->streams.begin(), S->streams.end(), stream) == S->streams.end())
                 S->streams.push_back(stream);
@@ -446,6 +483,16 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     }
     if (!d_items && S->has_lists)
         note_stream(P, stream);   // an inline launch of index lists reads the plan's lists
+    if (slot_k >= 0) {
+        hipError_t e = hipSuccess;
+        if (slot_launch(P.device, dir, slot_k, slot_gen, S->ntasks, stream, &e)) {
+            HIPCHK(e);
+            return DDT_SUCCESS;
+        }
+        std::lock_guard<std::mutex> g(P.mu);   // the binding was ended (evicted): launch with arguments
+        if (S->slot == ((dir << 8) | slot_k) && S->slot_gen == slot_gen)
+            S->slot = -1;
+    }
     if (!d_items)
         HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, ubase, pbase, stream, grid_cap,
                                   S->all_dense));
@@ -1634,13 +1681,30 @@ int ddt_selftest(void)
     return 0;
 }
 
-int ddt_trim(void) { return pool_trim(); }
+int ddt_trim(void)
+{
+    slot_trim();   // every launch-slot binding ends (its set launches with arguments until it binds again)
+    return pool_trim();
+}
 
 int ddt_pool_info(int64_t *out6)
 {
     if (!out6)
         return DDT_ERR_BAD_PARAM;
     pool_stats(out6);
+    return DDT_SUCCESS;
+}
+
+int ddt_slot_info(int64_t *out4)
+{
+    if (!out4)
+        return DDT_ERR_BAD_PARAM;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void) hipGetLastError();
+        dev = -1;
+    }
+    slot_stats(dev, out4);
     return DDT_SUCCESS;
 }
 
@@ -1657,6 +1721,10 @@ int ddt_tune(const char *key, long value)
         tuning().interleave = value;
     else if (k == "uinterleave")
         tuning().uinterleave = value < 0 ? -1 : value;
+    else if (k == "slots")
+        tuning().slots = value ? 1 : 0;
+    else if (k == "slot_max_kb")
+        tuning().slot_max_kb = value < 0 ? 0 : value;
     else if (k == "policy")
         tuning().policy = int(value);
     else if (k == "ptr")

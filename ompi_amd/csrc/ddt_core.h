@@ -120,6 +120,7 @@ struct ItemSet {
     std::vector<Item> items;
     Item *d_items = nullptr;
     uint32_t ntasks = 0;
+    uint64_t bytes = 0;           // packed bytes the launch moves
     bool has_lists = false;
     bool all_dense = false;       // every item line-dense: the dense kernel runs the launch
     bool inline_ok = false;       // <= INLINE_ITEMS: launched from the kernarg segment
@@ -135,6 +136,14 @@ struct ItemSet {
     bool retired = false;
     std::vector<hipEvent_t> late;
     ItemBlock blk{};
+    // argument-free launches (run_windows): the slot this set is bound to (-1 none) and on which
+    // buffers; the bases of the previous launch by pointer (a set binds when two launches in a
+    // row use the same ones)
+    int slot = -1;                // (dir << 8) | k
+    int slot_dev = -1;
+    uint32_t slot_gen = 0;
+    uint64_t slot_ubase = 0, slot_pbase = 0;
+    uint64_t last_ubase = ~0ull, last_pbase = ~0ull;
     ~ItemSet();
 };
 

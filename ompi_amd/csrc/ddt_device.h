@@ -127,6 +127,16 @@ struct ItemArgs {
 };
 constexpr uint32_t ITEM_ARG_DIMS = 4;
 
+// The launch record of an argument-free move launch (ddt_move.hip.h, ddt_move_slot_kernel):
+// NSLOT records per (direction, lists) kernel family per device, bound by the host to hot
+// descriptor sets on fixed buffers (ddt_plan.cpp: slot_bind).
+constexpr uint32_t NSLOT = 8;
+struct LaunchRec {
+    uint64_t items;    // const Item * in device memory
+    uint64_t ubase, pbase;
+    uint32_t nitems, ntasks;
+};
+
 // ---- external32 conversion (ddt_external.cpp, ddt_ext_kernel) ----
 // CONV_LDBL: each 16-byte component x87 80-bit (native) <-> IEEE quad big-endian (external)
 enum ConvKind : uint32_t { CONV_COPY = 0, CONV_SWAP = 1, CONV_LONG = 2, CONV_ULONG = 3, CONV_LDBL = 4 };

@@ -149,6 +149,21 @@ hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, in
                  : launch_move_u0(d_items, nitems, ntasks, g, ubase, pbase, stream);
 }
 
+hipError_t launch_move_slot_p0(uint32_t k, uint32_t ntasks, hipStream_t stream);
+hipError_t launch_move_slot_u0(uint32_t k, uint32_t ntasks, hipStream_t stream);
+hipError_t slot_table_p0(void **addr);
+hipError_t slot_table_u0(void **addr);
+
+hipError_t launch_move_slot(int dir, uint32_t k, uint32_t ntasks, hipStream_t stream)
+{
+    return dir == 0 ? launch_move_slot_p0(k, ntasks, stream) : launch_move_slot_u0(k, ntasks, stream);
+}
+
+hipError_t slot_table(int dir, void **addr)
+{
+    return dir == 0 ? slot_table_p0(addr) : slot_table_u0(addr);
+}
+
 // ---------------------------------------------------------------- external32
 // One thread per basic element of the type signature: locate the element's segment and
 // run (binary searches over tiny tables), then move it between the native packed stream

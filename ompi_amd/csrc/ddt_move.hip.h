@@ -821,6 +821,43 @@ __global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restric
     move_body<DIR, LISTS>(items, nitems, Bases{ubase, pbase}, ntasks);
 }
 
+// Argument-free launches (round 5).  Under HIP's default device-resident kernel arguments ANY
+// launch with arguments costs the host ~2.9 us (the arguments are written across PCIe and read
+// back before the doorbell), one without arguments 0.7 us (scripts/hostcost.cpp,
+// profiles/r5_hostcost.jsonl): for a small message that is most of a call.  A hot descriptor set
+// launched again and again on the same buffers (a persistent halo exchange, a fragment loop on
+// fixed staging slots) is bound to one of NSLOT launch records in device memory, written once;
+// the slot's kernel reads its record and takes no arguments at all -- no gridDim either (that
+// would add hidden arguments): one workgroup per task.  One record table per translation unit
+// (direction, lists); ddt_convertor.cpp binds and releases the slots.
+static __device__ LaunchRec g_launch[NSLOT];
+
+template <int DIR, bool LISTS, uint32_t K>
+__global__ __launch_bounds__(THREADS) void ddt_move_slot_kernel()
+{
+    const LaunchRec &r = g_launch[K];
+    if (blockIdx.x < r.ntasks)
+        move_task<DIR, LISTS>(reinterpret_cast<const Item *>(r.items), r.nitems, Bases{r.ubase, r.pbase},
+                              blockIdx.x);
+}
+
+template <int DIR, bool LISTS>
+static void launch_slot(uint32_t k, uint32_t grid, hipStream_t stream)
+{
+    const dim3 g(grid), b(THREADS);
+    switch (k) {
+    case 0: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 0>), g, b, 0, stream); break;
+    case 1: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 1>), g, b, 0, stream); break;
+    case 2: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 2>), g, b, 0, stream); break;
+    case 3: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 3>), g, b, 0, stream); break;
+    case 4: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 4>), g, b, 0, stream); break;
+    case 5: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 5>), g, b, 0, stream); break;
+    case 6: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 6>), g, b, 0, stream); break;
+    default: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 7>), g, b, 0, stream); break;
+    }
+}
+static_assert(NSLOT == 8, "launch_slot dispatches eight slot kernels");
+
 // Small launches carry their descriptors in the kernel-argument segment: no device
 // buffer, no upload, no cache entry (fragment pipelines, windows, one-off messages).
 template <int DIR, bool LISTS, uint32_t NI>
@@ -916,6 +953,19 @@ static void launch_inline(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, 
         hipLaunchKernelGGL((ddt_move_kernel<DIRV, LISTSV>), dim3(grid), dim3(THREADS), 0, stream,      \
                            d_items, nitems, ubase, pbase, ntasks);                                     \
         return hipGetLastError();                                                                      \
+    }
+
+// The argument-free launchers of the affine kernel families (LISTS = false units only: index-list
+// launches keep their arguments; eight slot kernels per direction are a large part of the code).
+#define DDT_SLOT_INSTANCE(DIRV, TAG)                                                                   \
+    hipError_t launch_move_slot_##TAG(uint32_t k, uint32_t ntasks, hipStream_t stream)                 \
+    {                                                                                                  \
+        launch_slot<DIRV, false>(k, ntasks, stream);                                                   \
+        return hipGetLastError();                                                                      \
+    }                                                                                                  \
+    hipError_t slot_table_##TAG(void **addr)                                                           \
+    {                                                                                                  \
+        return hipGetSymbolAddress(addr, HIP_SYMBOL(g_launch));                                        \
     }
 
 }  // namespace ddt

@@ -5,4 +5,5 @@
 namespace ddt {
 DDT_MOVE_INSTANCE(0, false, p0)
 DDT_DENSE_INSTANCE(0, p0)
+DDT_SLOT_INSTANCE(0, p0)
 }  // namespace ddt

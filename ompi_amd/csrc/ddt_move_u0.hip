@@ -5,4 +5,5 @@
 namespace ddt {
 DDT_MOVE_INSTANCE(1, false, u0)
 DDT_DENSE_INSTANCE(1, u0)
+DDT_SLOT_INSTANCE(1, u0)
 }  // namespace ddt

@@ -9,7 +9,11 @@
 // per block -- the reference issues one cbmemcpy per block instead
 // (opal_datatype_accelerator_copy.h:51-75).
 #include <algorithm>
+#include <array>
+#include <atomic>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <cstring>
 #include <stdexcept>
 
@@ -108,6 +112,10 @@ Plan::~Plan()
         for (hipEvent_t e : S.late)
             (void) hipEventDestroy(e);
         S.late.clear();
+        if (S.slot >= 0) {   // free once every stream that launched the plan's work passes
+            slot_release(S.slot_dev, S.slot >> 8, S.slot & 15, S.slot_gen, &streams);
+            S.slot = -1;
+        }
         if (!S.d_items)
             return;
         if (S.pinned)
@@ -157,6 +165,190 @@ Plan::~Plan()
     graveyard.clear();
     pinned.clear();
     spare.clear();
+}
+
+// ------------------------------------------------------------------ launch slots
+// NSLOT launch records per direction per device (ddt_move.hip.h g_launch, one table per kernel
+// family).  A record is rewritten only when its slot is free AND every launch that read its
+// previous binding has passed: a binding ends by release (its set's memory is recycled, or its
+// plan is destroyed: fences on the plan's streams) or by eviction (idle for kEvictIdle slot
+// launches of the device while another set wants a slot: fences on the streams the binding
+// launched on).  Slot launches are enqueued under the table lock, so an eviction's fences follow
+// every launch of the binding it ends; a set whose binding ended (generation changed) launches
+// with arguments again and may bind anew.
+namespace {
+constexpr uint64_t kEvictIdle = 256;   // ticks: slot launches and bind attempts of the process
+struct SlotEntry {
+    bool used = false;
+    uint32_t gen = 0;                   // bumped when a binding ends
+    uint64_t last = 0;                  // tick of the last launch or bind
+    std::vector<hipStream_t> streams;   // streams the binding launched on
+    std::vector<hipEvent_t> fences;     // the last binding's launches: passed before the next bind
+};
+struct SlotFamily {
+    bool init = false;
+    LaunchRec *rec = nullptr;           // the family's record table on its device
+    SlotEntry e[NSLOT];
+};
+struct Slots {
+    std::mutex mu;
+    std::map<int, std::array<SlotFamily, 2>> dev;   // per device: pack, unpack
+    uint64_t tick = 0;
+    std::atomic<int64_t> binds{0}, launches{0};
+};
+Slots &slots()
+{
+    static Slots *s = new Slots();   // never destroyed: releases may come at exit
+    return *s;
+}
+bool fences_passed(std::vector<hipEvent_t> &f)
+{
+    for (hipEvent_t e : f)
+        if (hipEventQuery(e) != hipSuccess) {
+            (void) hipGetLastError();
+            return false;
+        }
+    for (hipEvent_t e : f)
+        (void) hipEventDestroy(e);
+    f.clear();
+    return true;
+}
+// End entry E's binding behind events on `streams` (false: no fence could be recorded, the slot
+// stays taken for good -- its record may still be read).  Table lock held.
+bool end_binding(SlotEntry &E, const std::vector<hipStream_t> &streams)
+{
+    ++E.gen;
+    std::vector<hipEvent_t> f;
+    for (hipStream_t st : streams) {
+        hipEvent_t e = nullptr;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone
+            || hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess || hipEventRecord(e, st) != hipSuccess) {
+            (void) hipGetLastError();
+            if (e)
+                (void) hipEventDestroy(e);
+            for (hipEvent_t x : f)
+                (void) hipEventDestroy(x);
+            E.streams.clear();
+            return false;
+        }
+        f.push_back(e);
+    }
+    E.used = false;
+    E.streams.clear();
+    E.fences.insert(E.fences.end(), f.begin(), f.end());
+    return true;
+}
+SlotFamily *family(Slots &S, int dev, int dir)   // table lock held
+{
+    SlotFamily &F = S.dev[dev][size_t(dir)];
+    if (!F.init) {
+        void *p = nullptr;
+        if (slot_table(dir, &p) != hipSuccess || !p) {
+            (void) hipGetLastError();
+            return nullptr;
+        }
+        F.rec = static_cast<LaunchRec *>(p);
+        F.init = true;
+    }
+    return &F;
+}
+}  // namespace
+
+int slot_bind(int dev, int dir, const LaunchRec &rec, uint32_t *gen)
+{
+    Slots &S = slots();
+    std::lock_guard<std::mutex> g(S.mu);
+    SlotFamily *F = family(S, dev, dir);
+    if (!F)
+        return -1;
+    ++S.tick;   // bind attempts age the bindings too: a full table of idle sets does not block
+    int victim = -1;
+    for (uint32_t k = 0; k < NSLOT; ++k) {
+        SlotEntry &E = F->e[k];
+        if (E.used) {
+            if (S.tick - E.last >= kEvictIdle && (victim < 0 || E.last < F->e[victim].last))
+                victim = int(k);
+            continue;
+        }
+        if (!fences_passed(E.fences))
+            continue;
+        // on the library-private stream, waited for: the record is in place before any
+        // stream's next launch, and the caller's stream (capturing or not) is not touched
+        if (upload(F->rec + k, &rec, sizeof(rec)) != hipSuccess) {
+            (void) hipGetLastError();
+            return -1;
+        }
+        E.used = true;
+        E.last = ++S.tick;
+        *gen = E.gen;
+        ++S.binds;
+        return int(k);
+    }
+    if (victim >= 0)   // free it for a later bind, once its launches pass
+        (void) end_binding(F->e[victim], F->e[victim].streams);
+    return -1;
+}
+
+bool slot_launch(int dev, int dir, int k, uint32_t gen, uint32_t ntasks, hipStream_t stream, hipError_t *err)
+{
+    Slots &S = slots();
+    std::lock_guard<std::mutex> g(S.mu);
+    SlotFamily *F = family(S, dev, dir);
+    if (!F || k < 0 || k >= int(NSLOT))
+        return false;
+    SlotEntry &E = F->e[k];
+    if (!E.used || E.gen != gen)
+        return false;   // the binding ended
+    if (std::find(E.streams.begin(), E.streams.end(), stream) == E.streams.end())
+        E.streams.push_back(stream);
+    E.last = ++S.tick;
+    *err = launch_move_slot(dir, uint32_t(k), ntasks, stream);
+    ++S.launches;
+    return true;
+}
+
+void slot_release(int dev, int dir, int k, uint32_t gen, const std::vector<hipStream_t> *fence_streams)
+{
+    if (k < 0 || k >= int(NSLOT))
+        return;
+    Slots &S = slots();
+    std::lock_guard<std::mutex> g(S.mu);
+    SlotEntry &E = S.dev[dev][size_t(dir)].e[k];
+    if (!E.used || E.gen != gen)
+        return;   // already ended (evicted)
+    if (fence_streams) {
+        (void) end_binding(E, *fence_streams);
+    } else {      // its launches have all passed
+        ++E.gen;
+        E.used = false;
+        E.streams.clear();
+    }
+}
+
+void slot_trim()
+{
+    Slots &S = slots();
+    std::lock_guard<std::mutex> g(S.mu);
+    for (auto &kv : S.dev)
+        for (SlotFamily &F : kv.second)
+            for (SlotEntry &E : F.e)
+                if (E.used)
+                    (void) end_binding(E, E.streams);
+}
+
+void slot_stats(int dev, int64_t *out4)
+{
+    Slots &S = slots();
+    std::lock_guard<std::mutex> g(S.mu);
+    out4[0] = out4[1] = 0;
+    auto it = S.dev.find(dev);
+    if (it != S.dev.end())
+        for (int dir = 0; dir < 2; ++dir)
+            for (const SlotEntry &E : it->second[size_t(dir)].e)
+                out4[dir] += E.used ? 1 : 0;
+    out4[2] = S.binds.load();
+    out4[3] = S.launches.load();
 }
 
 ItemSet::~ItemSet()

@@ -18,6 +18,8 @@ struct Tuning {
     long task_kb = 0;  // packed KiB per workgroup task: 0 = adaptive
     long interleave = 0;  // >0: interleave items in runs of this many tasks (pack, typed copy)
     long uinterleave = 256;  // the same for an unpack (-1: as `interleave`); see assign_tasks
+    long slots = 1;       // argument-free launches of hot descriptor sets (ddt_move_slot_kernel); 0 off
+    long slot_max_kb = 4096;  // ... for launches of at most this many packed KiB
     int policy = 1;       // task sizing: 0 = v0 (~6 K tasks), 1 = per-leaf passes
     int wt = -1;          // write-through (sc1) stores: -1 auto, 0 off, 1 sparse user side, 2 all
     long sorted = -1;     // address-ordered list engine: -1 auto, 0 off, n > 0 from n blocks up
@@ -92,6 +94,24 @@ bool launch_single_item(const Item &it, int dir, uint64_t ubase, uint64_t pbase,
 hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, int dir, bool lists,
                        uint64_t ubase, uint64_t pbase, hipStream_t stream, uint32_t grid_cap = 0,
                        bool dense = false);
+// The argument-free launch of slot k's record (grid = ntasks) and the device address of a kernel
+// family's record table (current device).
+hipError_t launch_move_slot(int dir, uint32_t k, uint32_t ntasks, hipStream_t stream);
+hipError_t slot_table(int dir, void **addr);
+// Launch slots (ddt_plan.cpp; affine launches only).  slot_bind: a free slot of direction `dir`
+// on device `dev` whose last binding's launches have passed, with `rec` written into it
+// (uploaded and waited for on the private stream) and its generation in *gen, or -1 (then a
+// binding idle for long may have been ended for the next try).  slot_launch: the argument-free
+// launch of slot k if binding `gen` still holds it (false: launch with arguments).
+// slot_release: binding `gen` ends; the slot is free once `fence_streams` (null: none) pass
+// the events recorded now.
+int slot_bind(int dev, int dir, const LaunchRec &rec, uint32_t *gen);
+bool slot_launch(int dev, int dir, int k, uint32_t gen, uint32_t ntasks, hipStream_t stream, hipError_t *err);
+void slot_release(int dev, int dir, int k, uint32_t gen, const std::vector<hipStream_t> *fence_streams);
+// every binding ends behind fences on its streams (ddt_trim)
+void slot_trim();
+// out4 = [pack slots bound on dev, unpack slots bound, binds so far, argument-free launches so far]
+void slot_stats(int dev, int64_t *out4);
 
 // external32 conversion between a native packed stream and its big-endian form.
 // uniform = C in {1,2,4,8,16}: every element is a C-byte word swap (C = 1: a copy) with identical native

@@ -41,6 +41,37 @@ __global__ void empty_kernel_args(const void *p, uint32_t n, uint64_t a, uint64_
         *reinterpret_cast<uint64_t *>(const_cast<void *>(p)) = a + b;
 }
 
+// a 512 KiB copy with its pointers in kernel arguments, and the same with the pointers in a
+// device-global record (no kernel arguments at all: no gridDim / blockDim, which would add
+// hidden arguments): 32 workgroups x 256 threads x 4 x 16 B
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+struct SlotRec { const u32x4v *src; u32x4v *dst; };
+__device__ SlotRec g_slot[4];
+__global__ __launch_bounds__(256) void copy_args(const u32x4v *__restrict__ src, u32x4v *__restrict__ dst)
+{
+    const uint32_t t = blockIdx.x * 1024 + threadIdx.x;
+    u32x4v v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        v[k] = src[t + k * 256];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        dst[t + k * 256] = v[k];
+}
+template <int K>
+__global__ __launch_bounds__(256) void copy_slot()
+{
+    const SlotRec r = g_slot[K];
+    const uint32_t t = blockIdx.x * 1024 + threadIdx.x;
+    u32x4v v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        v[k] = r.src[t + k * 256];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        r.dst[t + k * 256] = v[k];
+}
+
 using clk = std::chrono::steady_clock;
 
 struct Res { double host_us, dev_us; };
@@ -99,6 +130,16 @@ int main(int argc, char **argv)
     std::printf("\"host_us\": %.3f, \"device_us\": %.3f}\n", r.host_us, r.dev_us);
     std::printf("{\"what\": \"empty kernel, 36 B of arguments, 32 x 256 threads\", \"bytes\": 0, ");
     r = run(s, iters, [&] { hipLaunchKernelGGL(empty_kernel_args, dim3(32), dim3(256), 0, s, (const void *) packed, 1u, 2ull, 3ull, 4u); });
+    std::printf("\"host_us\": %.3f, \"device_us\": %.3f}\n", r.host_us, r.dev_us);
+    std::printf("{\"what\": \"512 KiB copy kernel, pointers in arguments\", \"bytes\": %zu, ", face);
+    r = run(s, iters, [&] { hipLaunchKernelGGL(copy_args, dim3(32), dim3(256), 0, s, (const u32x4v *) packed, (u32x4v *) copy); });
+    std::printf("\"host_us\": %.3f, \"device_us\": %.3f}\n", r.host_us, r.dev_us);
+    {
+        SlotRec h{(const u32x4v *) packed, (u32x4v *) copy};
+        CHK(hipMemcpyToSymbol(HIP_SYMBOL(g_slot), &h, sizeof(h)));
+    }
+    std::printf("{\"what\": \"512 KiB copy kernel, pointers in a device record (no arguments)\", \"bytes\": %zu, ", face);
+    r = run(s, iters, [&] { hipLaunchKernelGGL(copy_slot<0>, dim3(32), dim3(256), 0, s); });
     std::printf("\"host_us\": %.3f, \"device_us\": %.3f}\n", r.host_us, r.dev_us);
     std::printf("{\"what\": \"hipMemcpyAsync D2D\", \"bytes\": %zu, ", face);
     r = run(s, iters, [&] { CHK(hipMemcpyAsync(copy, packed, face, hipMemcpyDeviceToDevice, s)); });

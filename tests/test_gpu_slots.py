@@ -1,0 +1,224 @@
+"""Argument-free launches (ddt_move.hip.h ddt_move_slot_kernel, ddt_plan.cpp slot_bind; round 5).
+
+A descriptor set launched twice in a row on the same buffers is bound to a launch record in
+device memory and later launches on those buffers take no kernel arguments.  Every launch must
+still move exactly the oracle's bytes: new contents each call, buffers that change after a bind,
+more hot sets than slots, a second stream, slots released with their type and bound again.
+"""
+from __future__ import annotations
+
+import gc
+
+import numpy as np
+import pytest
+
+from . import recipes as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _slots():
+    import ctypes
+    from ompi_amd._lib import lib
+    out = (ctypes.c_int64 * 4)()
+    assert lib().ddt_slot_info(out) == 0
+    return list(out)
+
+
+@pytest.fixture(autouse=True)
+def _no_bindings():
+    """Every test starts with all slots free: ddt_trim ends the bindings earlier tests left."""
+    import torch
+    from ompi_amd._lib import lib
+    torch.cuda.synchronize()
+    assert lib().ddt_trim() == 0
+    st = _slots()
+    assert st[0] == 0 and st[1] == 0, st
+    yield
+
+
+def _face(n, which):
+    import bench
+    return bench.face_recipes(n=n)[which]
+
+
+class _Msg:
+    """One type on fixed device buffers, packed / unpacked again and again through one
+    asynchronous convertor pair on `stream`."""
+
+    def __init__(self, recipe, count, device, stream, seed):
+        import torch
+        import ompi_amd
+        self.b = R.Built(recipe)
+        self.e = self.b.engine()
+        info = self.b.o.info()
+        self.count = count
+        self.size = info["size"] * count
+        self.span, self.origin = R.layout(info, count)
+        self.device = device
+        self.user = torch.zeros(self.span + 16, dtype=torch.uint8, device=device)
+        self.out = torch.zeros(self.span + 16, dtype=torch.uint8, device=device)
+        self.packed = torch.zeros(self.size, dtype=torch.uint8, device=device)
+        self.stream = stream
+        self.cp, self.cu = ompi_amd.Convertor(), ompi_amd.Convertor()
+        for c in (self.cp, self.cu):
+            c.set_stream(stream, True)
+        self.rng = np.random.default_rng(seed)
+
+    def step(self, packed=None):
+        """New user contents, pack, unpack into a 0xA5-filled buffer; both checked."""
+        import torch
+        packed = self.packed if packed is None else packed
+        host = self.rng.integers(1, 255, self.span, dtype=np.uint8)
+        torch.cuda.synchronize()
+        self.user[:self.span].copy_(torch.from_numpy(host))
+        self.out.fill_(0xA5)
+        torch.cuda.synchronize()
+        uptr = self.user.data_ptr() + self.origin
+        self.cp.prepare_for_send(self.e, self.count, uptr)
+        rc, _, md = self.cp.pack([(packed.data_ptr(), self.size)])
+        assert rc == 1 and md == self.size
+        self.cu.prepare_for_recv(self.e, self.count, self.out.data_ptr() + self.origin)
+        rc, _, md = self.cu.unpack([(packed.data_ptr(), self.size)])
+        assert rc == 1 and md == self.size
+        torch.cuda.synchronize()
+        ref = np.frombuffer(self.b.o.pack(self.count, host, self.origin, 0, self.size, element_granular=False),
+                            dtype=np.uint8)
+        np.testing.assert_array_equal(packed.cpu().numpy(), ref)
+        exp = np.full(self.span, 0xA5, dtype=np.uint8)
+        self.b.o.unpack(self.count, exp, self.origin, 0, ref.tobytes())
+        np.testing.assert_array_equal(self.out[:self.span].cpu().numpy(), exp)
+
+
+def test_hot_faces_bind_slots_and_move_the_oracle_bytes(device):
+    import torch
+    s = torch.cuda.Stream(device)
+    before = _slots()
+    msgs = [_Msg(_face(32, w), 3, device, s, 10 + i) for i, w in enumerate("xyz")]
+    for _ in range(5):
+        for m in msgs:
+            m.step()
+    after = _slots()
+    # three sets per direction bound (pack and unpack sets are distinct: their task orders differ)
+    assert after[0] - before[0] == 3 and after[1] - before[1] == 3, (before, after)
+    # launches 3..5 of each of the 6 sets ran without arguments
+    assert after[3] - before[3] >= 6 * 3, (before, after)
+
+
+def test_changed_buffers_fall_back_and_return(device):
+    import torch
+    s = torch.cuda.Stream(device)
+    m = _Msg(_face(32, "y"), 2, device, s, 21)
+    for _ in range(3):
+        m.step()
+    other = torch.zeros_like(m.packed)
+    n0 = _slots()[3]
+    m.step(packed=other)           # a different packed buffer: launches with arguments
+    assert _slots()[3] == n0
+    m.step()                       # the bound buffers again: argument-free, both directions
+    assert _slots()[3] == n0 + 2
+
+
+def test_more_hot_sets_than_slots(device):
+    """Twelve hot types of one direction: eight bind, the rest keep launching with arguments;
+    all move the right bytes."""
+    import torch
+    s = torch.cuda.Stream(device)
+    msgs = [_Msg(("resized", ("vector", 64, 1 + (i % 3), 8 + i, ("basic", 16)), 0, 8 * (8 + i) * 64), 2,
+                 device, s, 40 + i) for i in range(12)]
+    for _ in range(3):
+        for m in msgs:
+            m.step()
+    st = _slots()
+    assert st[0] <= 8 and st[1] <= 8
+    for m in msgs:
+        m.step()
+
+
+def test_idle_bindings_are_evicted_for_a_new_hot_set(device):
+    """Eight sets bind every pack slot and go idle; a ninth set's bind attempts age them and,
+    after kEvictIdle ticks, end the least recent binding (behind fences): the ninth set binds and
+    launches argument-free; the evicted set falls back to arguments and stays correct."""
+    import torch
+    s = torch.cuda.Stream(device)
+    # one 8-byte element per 64+ bytes: the unit loop (line-dense records take no slots)
+    idle = [_Msg(("resized", ("vector", 16, 1, 8 + i, ("basic", 16)), 0, 8 * (8 + i) * 16), 1, device, s, 70 + i)
+            for i in range(8)]
+    for _ in range(3):
+        for m in idle:
+            m.step()
+    assert _slots()[0] == 8
+    hot = _Msg(("resized", ("vector", 16, 1, 40, ("basic", 16)), 0, 8 * 40 * 16), 1, device, s, 90)
+    n0 = _slots()[3]
+    for _ in range(140):   # 2 calls per step: >= 256 bind attempts in the unpack and pack families
+        hot.step()
+    assert _slots()[3] > n0, _slots()   # the hot set launched from a slot at last
+    for m in idle:
+        m.step()
+
+
+def test_second_stream_uses_a_bound_slot(device):
+    import torch
+    s1, s2 = torch.cuda.Stream(device), torch.cuda.Stream(device)
+    m = _Msg(_face(32, "z"), 2, device, s1, 31)
+    for _ in range(3):
+        m.step()
+    for c in (m.cp, m.cu):
+        c.set_stream(s2, True)
+    n0 = _slots()[3]
+    m.step()                       # the record is in device memory: s2 launches from the slot too
+    assert _slots()[3] == n0 + 2
+
+
+def test_slots_are_released_with_their_type_and_bound_again(device):
+    import torch
+    s = torch.cuda.Stream(device)
+    base = _slots()
+    m = _Msg(_face(32, "x"), 2, device, s, 51)
+    for _ in range(3):
+        m.step()
+    bound = _slots()
+    assert bound[0] == base[0] + 1 and bound[1] == base[1] + 1
+    del m
+    gc.collect()
+    torch.cuda.synchronize()
+    freed = _slots()
+    assert freed[0] == base[0] and freed[1] == base[1], (base, freed)
+    m2 = _Msg(_face(32, "y"), 2, device, s, 52)
+    for _ in range(4):
+        m2.step()
+    assert _slots()[0] == base[0] + 1
+
+
+def test_slots_off(device):
+    import torch
+    import ompi_amd
+    L = ompi_amd.lib()
+    L.ddt_tune(b"slots", 0)
+    try:
+        s = torch.cuda.Stream(device)
+        m = _Msg(_face(32, "y"), 2, device, s, 61)
+        n0 = _slots()[3]
+        for _ in range(4):
+            m.step()
+        assert _slots()[3] == n0
+    finally:
+        L.ddt_tune(b"slots", 1)
+
+
+def test_large_launches_keep_their_arguments(device):
+    """Only launches of at most slot_max_kb packed KiB bind (a slot kernel's extra record load
+    costs a large latency-bound launch more than the host saves)."""
+    import torch
+    import ompi_amd
+    L = ompi_amd.lib()
+    L.ddt_tune(b"slot_max_kb", 16)
+    try:
+        s = torch.cuda.Stream(device)
+        m = _Msg(_face(32, "y"), 3, device, s, 81)   # 24 KiB packed
+        n0 = _slots()
+        for _ in range(4):
+            m.step()
+        assert _slots()[2:] == n0[2:]
+    finally:
+        L.ddt_tune(b"slot_max_kb", 4096)
