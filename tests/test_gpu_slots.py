@@ -222,3 +222,39 @@ def test_large_launches_keep_their_arguments(device):
         assert _slots()[2:] == n0[2:]
     finally:
         L.ddt_tune(b"slot_max_kb", 4096)
+
+
+def test_random_interleaving_of_types_buffers_streams_and_trims(device):
+    """A random schedule over twelve small affine types: each step packs and unpacks one type on
+    one of two buffer sets and one of two streams, now and then destroys a type and builds it
+    again, or trims; every step moves the oracle's bytes (bindings bind, fall back, end and bind
+    again underneath)."""
+    import random
+    import torch
+    from ompi_amd._lib import lib
+    rng = random.Random(1234)
+    streams = [torch.cuda.Stream(device), torch.cuda.Stream(device)]
+
+    def recipe(i):
+        if i % 3 == 0:
+            return _face(16 + 8 * (i % 2), "xyz"[i % 3])
+        return ("resized", ("vector", 24 + i, 1 + i % 2, 6 + i, ("basic", 16 if i % 2 else 6)), 0, 8 * (6 + i) * (24 + i))
+
+    msgs = [_Msg(recipe(i), 1 + i % 3, device, streams[i % 2], 300 + i) for i in range(12)]
+    alt = [torch.zeros_like(m.packed) for m in msgs]
+    for step in range(240):
+        i = rng.randrange(12)
+        m = msgs[i]
+        st = streams[rng.randrange(2)]   # one stream per step: the unpack reads what the pack wrote
+        for c in (m.cp, m.cu):
+            c.set_stream(st, True)
+        m.step(packed=alt[i] if rng.random() < 0.2 else None)
+        r = rng.random()
+        if r < 0.03:
+            msgs[i] = _Msg(recipe(i), 1 + i % 3, device, streams[i % 2], 500 + step)
+            alt[i] = torch.zeros_like(msgs[i].packed)
+        elif r < 0.05:
+            torch.cuda.synchronize()
+            assert lib().ddt_trim() == 0
+    st = _slots()
+    assert st[3] > 0 and st[0] <= 8 and st[1] <= 8, st
