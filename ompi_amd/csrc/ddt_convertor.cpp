@@ -362,6 +362,8 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                 S->blk.items[i] = S->items[i];
         } else if (!S->items.empty()) {
             size_t bytes = S->items.size() * sizeof(Item);
+            RelaxedCapture relaxed;   // reap queries, allocation, upload: leave other threads' captures be
+            PoolNoDeviceSync no_sync;
             {
                 std::lock_guard<std::mutex> g(P.mu);
                 S->d_items = take_items_memory(P, bytes, !capturing(stream));
@@ -430,6 +432,8 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         std::lock_guard<std::mutex> g(P.mu);
         if (S->inline_ok && !S->retired && ++S->uses >= 2 && !S->d_items && tuning().ptr) {
             size_t bytes = S->items.size() * sizeof(Item);
+            RelaxedCapture relaxed;
+            PoolNoDeviceSync no_sync;
             Item *d = take_items_memory(P, bytes, !capturing(stream));
             if (d) {
                 if (upload(d, S->items.data(), bytes) == hipSuccess)

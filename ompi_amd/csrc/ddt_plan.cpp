@@ -257,6 +257,8 @@ SlotFamily *family(Slots &S, int dev, int dir)   // table lock held
 
 int slot_bind(int dev, int dir, const LaunchRec &rec, uint32_t *gen)
 {
+    RelaxedCapture relaxed;   // fence queries and the upload: never another thread's capture's business
+    PoolNoDeviceSync no_sync;
     Slots &S = slots();
     std::lock_guard<std::mutex> g(S.mu);
     SlotFamily *F = family(S, dev, dir);
@@ -696,20 +698,15 @@ int prebuild_device(ddt_datatype *t)
     hipStream_t bs = nullptr;
     if (private_stream(&bs) != hipSuccess)
         return DDT_ERR_HIP;
-    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-    const bool swapped = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
-    (void) hipGetLastError();
-    int rc = DDT_SUCCESS;
+    RelaxedCapture relaxed;
     PoolNoDeviceSync no_sync;   // allocation, upload and stream waits only: no device-wide wait
     try {
         ensure_device_lists(*P);
         (void) sorted_build(*P, bs);
     } catch (const std::exception &) {
-        rc = DDT_ERR_OUT_OF_RESOURCE;
+        return DDT_ERR_OUT_OF_RESOURCE;
     }
-    if (swapped)
-        (void) hipThreadExchangeStreamCaptureMode(&mode);
-    return rc;
+    return DDT_SUCCESS;
 }
 
 // ------------------------------------------------------------------ items for one call

@@ -67,6 +67,22 @@ struct Tuning {
 Tuning &tuning();
 // Synchronous host -> device copy on a library-private stream (capture-safe).
 hipError_t upload(void *dst, const void *src, size_t n);
+// While one lives, this thread's stream-capture mode is relaxed: the event queries, allocations
+// and private-stream waits of descriptor uploads and slot binds are then this thread's own
+// business and leave another thread's global-mode capture intact
+// (profiles/r5_probe_capture.log); device-wide waits stay off (PoolNoDeviceSync).
+struct RelaxedCapture {
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    bool swapped;
+    RelaxedCapture() : swapped(hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess) { (void) hipGetLastError(); }
+    ~RelaxedCapture()
+    {
+        if (swapped)
+            (void) hipThreadExchangeStreamCaptureMode(&mode);
+    }
+    RelaxedCapture(const RelaxedCapture &) = delete;
+    RelaxedCapture &operator=(const RelaxedCapture &) = delete;
+};
 // The library-private non-blocking stream of the current device (uploads, table builds).
 hipError_t private_stream(hipStream_t *out);
 

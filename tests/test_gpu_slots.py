@@ -258,3 +258,66 @@ def test_random_interleaving_of_types_buffers_streams_and_trims(device):
             assert lib().ddt_trim() == 0
     st = _slots()
     assert st[3] > 0 and st[0] <= 8 and st[1] <= 8, st
+
+
+@pytest.mark.parametrize("mode", ["global", "relaxed"])
+def test_binding_during_foreign_capture(device, mode):
+    """A set's descriptor upload and its slot bind (event queries, a private-stream upload and
+    wait) happen while ANOTHER thread captures a graph: they run in relaxed capture mode, so the
+    foreign capture ends intact and replays; the packs are bit-exact."""
+    import threading
+    import torch
+    import ompi_amd
+    x = torch.zeros(1024, device=device)
+    sb, sa = torch.cuda.Stream(device), torch.cuda.Stream(device)
+    g = torch.cuda.CUDAGraph()
+    b = R.Built(_face(32, "y"))
+    e = b.engine()
+    info = b.o.info()
+    count, size = 2, info["size"] * 2
+    span, origin = R.layout(info, count)
+    host = np.random.default_rng(7).integers(1, 255, span, dtype=np.uint8)
+    user = torch.from_numpy(host).to(device)
+    packed = torch.zeros(size, dtype=torch.uint8, device=device)
+    torch.cuda.synchronize()
+    started, done = threading.Event(), threading.Event()
+    errors = []
+    n0 = _slots()
+
+    def capture():
+        try:
+            with torch.cuda.graph(g, stream=sb, capture_error_mode=mode):
+                x.add_(1)
+                started.set()
+                done.wait(120)
+                x.add_(1)
+        except Exception as ex:   # noqa: BLE001 -- reported below
+            errors.append(repr(ex))
+            started.set()
+
+    def packs():
+        try:
+            started.wait(60)
+            c = ompi_amd.Convertor()
+            c.set_stream(sa, True)
+            for _ in range(4):
+                c.prepare_for_send(e, count, user.data_ptr() + origin)
+                rc, _, md = c.pack([(packed.data_ptr(), size)])
+                assert rc == 1 and md == size
+        except Exception as ex:   # noqa: BLE001
+            errors.append(repr(ex))
+        finally:
+            done.set()
+
+    tb, ta = threading.Thread(target=capture), threading.Thread(target=packs)
+    tb.start()
+    ta.start()
+    ta.join(180)
+    tb.join(180)
+    assert not errors, errors
+    g.replay()
+    torch.cuda.synchronize()
+    assert float(x[0].item()) == 2.0
+    ref = np.frombuffer(b.o.pack(count, host, origin, 0, size, element_granular=False), dtype=np.uint8)
+    np.testing.assert_array_equal(packed.cpu().numpy(), ref)
+    assert _slots()[3] > n0[3]   # the fourth pack ran from its slot
