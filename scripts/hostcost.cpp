@@ -182,6 +182,49 @@ int main(int argc, char **argv)
         std::printf("{\"what\": \"engine prepare_for_send %s face\", \"bytes\": 0, \"host_us\": %.3f}\n",
                     names[f], r.host_us);
     }
+    // synchronous calls (MPI_Pack semantics: the data is in place on return): an empty kernel
+    // then a wait, by hipStreamSynchronize, by hipEventSynchronize, by polling hipEventQuery;
+    // then the engine's own synchronous MPI_Pack of the y face
+    {
+        hipEvent_t ev;
+        CHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        auto wall = [&](auto op) {
+            for (int i = 0; i < 20; ++i)
+                op();
+            const auto t0 = clk::now();
+            for (int i = 0; i < iters; ++i)
+                op();
+            return std::chrono::duration<double, std::micro>(clk::now() - t0).count() / iters;
+        };
+        double w = wall([&] {
+            hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s);
+            CHK(hipStreamSynchronize(s));
+        });
+        std::printf("{\"what\": \"empty kernel + hipStreamSynchronize\", \"call_us\": %.3f}\n", w);
+        w = wall([&] {
+            hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s);
+            CHK(hipEventRecord(ev, s));
+            CHK(hipEventSynchronize(ev));
+        });
+        std::printf("{\"what\": \"empty kernel + event record + hipEventSynchronize\", \"call_us\": %.3f}\n", w);
+        w = wall([&] {
+            hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s);
+            CHK(hipEventRecord(ev, s));
+            while (hipEventQuery(ev) == hipErrorNotReady) {
+            }
+        });
+        std::printf("{\"what\": \"empty kernel + event record + hipEventQuery poll\", \"call_us\": %.3f}\n", w);
+        for (int f = 0; f < 3; ++f) {
+            size_t pos = 0;
+            w = wall([&] {
+                pos = 0;
+                DCHK(ddt_pack(user, 1, faces[f], packed, face, &pos));
+            });
+            std::printf("{\"what\": \"engine MPI_Pack (synchronous) %s face\", \"bytes\": %zu, \"call_us\": %.3f}\n",
+                        names[f], face, w);
+        }
+        CHK(hipEventDestroy(ev));
+    }
     // the same with descriptors always in the kernel arguments (ddt_tune "ptr" 0)
     ddt_tune("ptr", 0);
     for (int f = 1; f < 2; ++f) {
