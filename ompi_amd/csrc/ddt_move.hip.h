@@ -830,15 +830,22 @@ __global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restric
 // the slot's kernel reads its record and takes no arguments at all -- no gridDim either (that
 // would add hidden arguments): one workgroup per task.  One record table per translation unit
 // (direction, lists); ddt_convertor.cpp binds and releases the slots.
-static __device__ LaunchRec g_launch[NSLOT];
+// constant address space: the record loads are scalar and uniform (as kernel arguments are);
+// from a __device__ array the compiler kept the fields in vector registers (92 VGPRs against
+// the pointer kernel's 56) and large launches lost occupancy
+static __constant__ LaunchRec g_launch[NSLOT];
 
 template <int DIR, bool LISTS, uint32_t K>
 __global__ __launch_bounds__(THREADS) void ddt_move_slot_kernel()
 {
     const LaunchRec &r = g_launch[K];
+    // the descriptor set is read-only for the kernel's lifetime, as a kernel-argument pointer is:
+    // in the constant address space its uniform loads are scalar (a plain pointer loaded from
+    // memory gives flat vector loads and twice the registers)
+    using CItem = const __attribute__((address_space(4))) Item;
+    const Item *items = (const Item *) (CItem *) r.items;
     if (blockIdx.x < r.ntasks)
-        move_task<DIR, LISTS>(reinterpret_cast<const Item *>(r.items), r.nitems, Bases{r.ubase, r.pbase},
-                              blockIdx.x);
+        move_task<DIR, LISTS>(items, r.nitems, Bases{r.ubase, r.pbase}, blockIdx.x);
 }
 
 template <int DIR, bool LISTS>
