@@ -454,16 +454,21 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                        && S->bytes <= uint64_t(tuning().slot_max_kb) << 10) {
                 // an argument-free launch (ddt_move.hip.h, ddt_move_slot_kernel): a set bound to
                 // a slot for these buffers and this direction; a set launched twice in a row on
-                // the same buffers binds one (its record is in device memory before this launch).
-                // Small launches only: a slot kernel's workgroups first load the record (one more
-                // dependent load than arguments preloaded into registers), which a large launch of
-                // latency-bound gathers pays (the halo's 48 MiB pack 67.6 -> 74.8 us), while the host's
-                // 2.2 us saving only matters where the kernel is as short as a launch
+                // the same buffers binds one (its record is in device memory before this launch),
+                // giving up a binding on other buffers first.  Small launches only: a slot
+                // kernel's workgroups first load the record (one more dependent load than
+                // arguments preloaded into registers), which a large launch of latency-bound
+                // gathers pays (the halo's 48 MiB pack 66.4 -> 68.2 us), while the host's 2.2 us
+                // saving only matters where the kernel is as short as a launch
                 const int fam = dir << 8;
                 if (S->slot >= 0 && (S->slot & ~15) == fam && S->slot_ubase == ubase && S->slot_pbase == pbase) {
                     slot_k = S->slot & 15;
                     slot_gen = S->slot_gen;
-                } else if (S->slot < 0 && S->last_ubase == ubase && S->last_pbase == pbase) {
+                } else if (S->last_ubase == ubase && S->last_pbase == pbase) {
+                    if (S->slot >= 0) {   // bound to other buffers (or direction): free it behind its launches
+                        slot_release(S->slot_dev, S->slot >> 8, S->slot & 15, S->slot_gen, &S->streams);
+                        S->slot = -1;
+                    }
                     const LaunchRec rec{uint64_t(uintptr_t(d_items)), ubase, pbase, uint32_t(S->items.size()),
                                         S->ntasks};
                     const int k = slot_bind(P.device, dir, rec, &S->slot_gen);

@@ -321,3 +321,22 @@ def test_binding_during_foreign_capture(device, mode):
     ref = np.frombuffer(b.o.pack(count, host, origin, 0, size, element_granular=False), dtype=np.uint8)
     np.testing.assert_array_equal(packed.cpu().numpy(), ref)
     assert _slots()[3] > n0[3]   # the fourth pack ran from its slot
+
+
+def test_a_set_that_moves_to_other_buffers_rebinds(device):
+    """Bound on buffers A, then used on buffers B for good: the second call on B gives up the A
+    binding (behind fences) and binds B; one slot per direction stays in use."""
+    import torch
+    s = torch.cuda.Stream(device)
+    m = _Msg(_face(32, "z"), 2, device, s, 91)
+    for _ in range(3):
+        m.step()
+    assert _slots()[0] == 1 and _slots()[1] == 1
+    other = torch.zeros_like(m.packed)
+    n0 = _slots()[3]
+    m.step(packed=other)     # first call on B: with arguments
+    assert _slots()[3] == n0
+    m.step(packed=other)     # second: rebinds to B, argument-free
+    m.step(packed=other)
+    st = _slots()
+    assert st[3] == n0 + 4 and st[0] == 1 and st[1] == 1, st
