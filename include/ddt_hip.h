@@ -333,8 +333,8 @@ int ddt_type_cache_info(const ddt_datatype_t *type, int64_t *out4);
  * bytes, blocks kept for graphs, blocks in use]. */
 int ddt_trim(void);
 int ddt_pool_info(int64_t *out6);
-/* Argument-free launches: a descriptor set launched twice in a row on the same buffers is
- * bound to one of 8 launch records per direction in device memory, and its later launches on
+/* Argument-free launches: a descriptor set launched on the same buffers twice within three calls
+ * (two bindings per set) is bound to one of 8 launch records per direction in device memory, and its later launches on
  * those buffers take no kernel arguments (HIP writes device-resident kernel arguments across
  * PCIe: ~2.9 us of host time per launch with arguments, 0.7 us without).  ddt_slot_info: out4 =
  * [pack slots bound, unpack slots bound (current device), binds so far, argument-free launches

@@ -130,10 +130,11 @@ void recycle(Plan &P, Retired &r)   // P.mu held
     for (hipEvent_t e : S.late)
         (void) hipEventDestroy(e);
     S.late.clear();
-    if (S.slot >= 0) {   // every launch of the set has passed: its record is free
-        slot_release(S.slot_dev, S.slot >> 8, S.slot & 15, S.slot_gen, nullptr);
-        S.slot = -1;
-    }
+    for (ItemSet::Binding &b : S.bind)
+        if (b.slot >= 0) {   // every launch of the set has passed: its record is free
+            slot_release(S.slot_dev, b.slot >> 8, b.slot & 15, b.gen, nullptr);
+            b.slot = -1;
+        }
     if (S.d_items) {
         P.spare.push_back({S.d_items, S.items.size() * sizeof(Item)});
         S.d_items = nullptr;
@@ -426,7 +427,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     // across PCIe, and a 528-byte block costs 2.6 us of host time per launch against 0.7 us
     // for a pointer (scripts/hostbench.cpp, profiles/r1_hostbench.log).
     Item *d_items = nullptr;
-    int slot_k = -1;
+    int slot_k = -1, slot_b = -1;
     uint32_t slot_gen = 0;
     {
         std::lock_guard<std::mutex> g(P.mu);
@@ -453,36 +454,53 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             } else if (tuning().slots && grid_cap == 0 && !S->all_dense && !S->has_lists && !S->retired
                        && S->bytes <= uint64_t(tuning().slot_max_kb) << 10) {
                 // an argument-free launch (ddt_move.hip.h, ddt_move_slot_kernel): a set bound to
-                // a slot for these buffers and this direction; a set launched twice in a row on
-                // the same buffers binds one (its record is in device memory before this launch),
-                // giving up a binding on other buffers first.  Small launches only: a slot
+                // a slot for these buffers and this direction; buffers seen twice in the set's
+                // last three launches bind one (its record is in device memory before this launch;
+                // two bindings per set serve a double-buffered exchange).  Small launches only: a slot
                 // kernel's workgroups first load the record (one more dependent load than
                 // arguments preloaded into registers), which a large launch of latency-bound
                 // gathers pays (the halo's 48 MiB pack 66.4 -> 68.2 us), while the host's 2.2 us
                 // saving only matters where the kernel is as short as a launch
                 const int fam = dir << 8;
-                if (S->slot >= 0 && (S->slot & ~15) == fam && S->slot_ubase == ubase && S->slot_pbase == pbase) {
-                    slot_k = S->slot & 15;
-                    slot_gen = S->slot_gen;
-                } else if (S->last_ubase == ubase && S->last_pbase == pbase) {
-                    if (S->slot >= 0) {   // bound to other buffers (or direction): free it behind its launches
-                        slot_release(S->slot_dev, S->slot >> 8, S->slot & 15, S->slot_gen, &S->streams);
-                        S->slot = -1;
+                ++S->launches;
+                int hit = -1;
+                for (int i = 0; i < 2; ++i)
+                    if (S->bind[i].slot >= 0 && (S->bind[i].slot & ~15) == fam && S->bind[i].ubase == ubase
+                        && S->bind[i].pbase == pbase)
+                        hit = i;
+                const bool seen = (S->hist_u[0] == ubase && S->hist_p[0] == pbase)
+                                  || (S->hist_u[1] == ubase && S->hist_p[1] == pbase);
+                if (hit < 0 && seen) {
+                    // bind these buffers in a free binding, else in place of the less recent one
+                    // (given up behind fences on the set's streams)
+                    hit = S->bind[0].slot < 0 ? 0 : S->bind[1].slot < 0 ? 1 : (S->bind[0].used <= S->bind[1].used ? 0 : 1);
+                    ItemSet::Binding &B = S->bind[hit];
+                    if (B.slot >= 0) {
+                        slot_release(S->slot_dev, B.slot >> 8, B.slot & 15, B.gen, &S->streams);
+                        B.slot = -1;
                     }
                     const LaunchRec rec{uint64_t(uintptr_t(d_items)), ubase, pbase, uint32_t(S->items.size()),
                                         S->ntasks};
-                    const int k = slot_bind(P.device, dir, rec, &S->slot_gen);
+                    const int k = slot_bind(P.device, dir, rec, &B.gen);
                     if (k >= 0) {
-                        S->slot = fam | k;
+                        B.slot = fam | k;
+                        B.ubase = ubase;
+                        B.pbase = pbase;
                         S->slot_dev = P.device;
-                        S->slot_ubase = ubase;
-                        S->slot_pbase = pbase;
-                        slot_k = k;
-                        slot_gen = S->slot_gen;
+                    } else {
+                        hit = -1;
                     }
                 }
-                S->last_ubase = ubase;
-                S->last_pbase = pbase;
+                if (hit >= 0) {
+                    S->bind[hit].used = S->launches;
+                    slot_k = S->bind[hit].slot & 15;
+                    slot_gen = S->bind[hit].gen;
+                    slot_b = hit;
+                }
+                S->hist_u[1] = S->hist_u[0];
+                S->hist_p[1] = S->hist_p[0];
+                S->hist_u[0] = ubase;
+                S->hist_p[0] = pbase;
             }
             if (std::find(S->streams.begin(), S->streams.end(), stream) == S->streams.end())
                 S->streams.push_back(stream);
@@ -499,8 +517,9 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             return DDT_SUCCESS;
         }
         std::lock_guard<std::mutex> g(P.mu);   // the binding was ended (evicted): launch with arguments
-        if (S->slot == ((dir << 8) | slot_k) && S->slot_gen == slot_gen)
-            S->slot = -1;
+        ItemSet::Binding &B = S->bind[slot_b];
+        if (B.slot == ((dir << 8) | slot_k) && B.gen == slot_gen)
+            B.slot = -1;
     }
     if (!d_items)
         HIPCHK(launch_move_inline(S->blk, S->ntasks, dir, S->has_lists, ubase, pbase, stream, grid_cap,

@@ -136,14 +136,20 @@ struct ItemSet {
     bool retired = false;
     std::vector<hipEvent_t> late;
     ItemBlock blk{};
-    // argument-free launches (run_windows): the slot this set is bound to (-1 none) and on which
-    // buffers; the bases of the previous launch by pointer (a set binds when two launches in a
-    // row use the same ones)
-    int slot = -1;                // (dir << 8) | k
+    // argument-free launches (run_windows): up to two launch-slot bindings, each for one
+    // direction and one pair of buffers (a double-buffered exchange alternates two), and the
+    // buffers of the two previous launches by pointer (a set binds buffers seen twice in its last
+    // three launches)
+    struct Binding {
+        int slot = -1;            // (dir << 8) | k, -1 none
+        uint32_t gen = 0;
+        uint64_t ubase = 0, pbase = 0;
+        uint64_t used = 0;        // launches of the set when last used (the older one is given up)
+    };
+    Binding bind[2];
     int slot_dev = -1;
-    uint32_t slot_gen = 0;
-    uint64_t slot_ubase = 0, slot_pbase = 0;
-    uint64_t last_ubase = ~0ull, last_pbase = ~0ull;
+    uint64_t launches = 0;
+    uint64_t hist_u[2] = {~0ull, ~0ull}, hist_p[2] = {~0ull, ~0ull};
     ~ItemSet();
 };
 

@@ -112,10 +112,11 @@ Plan::~Plan()
         for (hipEvent_t e : S.late)
             (void) hipEventDestroy(e);
         S.late.clear();
-        if (S.slot >= 0) {   // free once every stream that launched the plan's work passes
-            slot_release(S.slot_dev, S.slot >> 8, S.slot & 15, S.slot_gen, &streams);
-            S.slot = -1;
-        }
+        for (ItemSet::Binding &b : S.bind)
+            if (b.slot >= 0) {   // free once every stream that launched the plan's work passes
+                slot_release(S.slot_dev, b.slot >> 8, b.slot & 15, b.gen, &streams);
+                b.slot = -1;
+            }
         if (!S.d_items)
             return;
         if (S.pinned)

@@ -324,19 +324,39 @@ def test_binding_during_foreign_capture(device, mode):
 
 
 def test_a_set_that_moves_to_other_buffers_rebinds(device):
-    """Bound on buffers A, then used on buffers B for good: the second call on B gives up the A
-    binding (behind fences) and binds B; one slot per direction stays in use."""
+    """Bound on buffers A, then used on buffers B: the second call on B binds B beside A (two
+    bindings per set, a double-buffered exchange); moving on to C gives up the less recent one
+    (A, behind fences): two slots per direction stay in use, and every call moves the right bytes."""
     import torch
     s = torch.cuda.Stream(device)
     m = _Msg(_face(32, "z"), 2, device, s, 91)
     for _ in range(3):
         m.step()
     assert _slots()[0] == 1 and _slots()[1] == 1
-    other = torch.zeros_like(m.packed)
+    b, c = torch.zeros_like(m.packed), torch.zeros_like(m.packed)
     n0 = _slots()[3]
-    m.step(packed=other)     # first call on B: with arguments
+    m.step(packed=b)     # first call on B: with arguments
     assert _slots()[3] == n0
-    m.step(packed=other)     # second: rebinds to B, argument-free
-    m.step(packed=other)
+    m.step(packed=b)     # second: binds B, argument-free
+    m.step()             # A is still bound
     st = _slots()
-    assert st[3] == n0 + 4 and st[0] == 1 and st[1] == 1, st
+    assert st[3] == n0 + 4 and st[0] == 2 and st[1] == 2, st
+    m.step(packed=c)
+    m.step(packed=c)     # binds C in place of the less recent binding
+    st2 = _slots()
+    assert st2[3] == st[3] + 2 and st2[0] == 2 and st2[1] == 2, st2
+
+
+def test_double_buffered_exchange_alternates_two_bindings(device):
+    """Send buffers alternating A, B, A, B ... (a double-buffered halo): from the third call on
+    every launch is argument-free."""
+    import torch
+    s = torch.cuda.Stream(device)
+    m = _Msg(_face(32, "y"), 2, device, s, 93)
+    b = torch.zeros_like(m.packed)
+    for i in range(4):
+        m.step(packed=b if i % 2 else None)
+    n0 = _slots()[3]
+    for i in range(6):
+        m.step(packed=b if i % 2 else None)
+    assert _slots()[3] == n0 + 12
