@@ -338,7 +338,7 @@ int ddt_pool_info(int64_t *out6);
  * those buffers take no kernel arguments (HIP writes device-resident kernel arguments across
  * PCIe: ~2.9 us of host time per launch with arguments, 0.7 us without).  ddt_slot_info: out4 =
  * [pack slots bound, unpack slots bound (current device), binds so far, argument-free launches
- * so far].  ddt_tune("slots", 0) turns them off. */
+ * so far].  ddt_tune("slots", 0) turns them off; ddt_trim ends every binding. */
 int ddt_slot_info(int64_t *out4);
 /* ---- introspection for the CPU test-suite (no data movement; never used by pack/unpack) ----
  * ddt_type_plan_leaves: serialises the plan's leaf streams as int64 records
