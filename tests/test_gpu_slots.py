@@ -360,3 +360,31 @@ def test_double_buffered_exchange_alternates_two_bindings(device):
     for i in range(6):
         m.step(packed=b if i % 2 else None)
     assert _slots()[3] == n0 + 12
+
+
+def test_threads_bind_launch_and_evict_concurrently(device):
+    """Four threads, each with its own stream and three small types, packing and unpacking at
+    once (ctypes releases the GIL in the calls): bindings, argument-free launches and releases
+    race under the table lock; every step of every thread moves the oracle's bytes."""
+    import threading
+    import torch
+    errors = []
+
+    def worker(t):
+        try:
+            s = torch.cuda.Stream(device)
+            msgs = [_Msg(("resized", ("vector", 20 + 3 * t + i, 1 + i % 2, 7 + t + i, ("basic", 16)), 0,
+                          8 * (7 + t + i) * (20 + 3 * t + i)), 1 + i, device, s, 1000 + 10 * t + i)
+                    for i in range(3)]
+            for k in range(25):
+                msgs[k % 3].step()
+        except Exception as ex:   # noqa: BLE001 -- reported below
+            errors.append(repr(ex))
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in ts:
+        th.start()
+    for th in ts:
+        th.join(300)
+    assert not errors, errors[:3]
+    assert _slots()[3] > 0
