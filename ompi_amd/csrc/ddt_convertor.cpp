@@ -1808,7 +1808,7 @@ int ddt_tune(const char *key, long value)
     else if (k == "opt_preserve")
         tuning().opt_preserve = value ? 1 : 0;
     else if (k == "reset")
-        tuning() = Tuning{};
+        tuning() = tuning_defaults();
     else
         return fail(DDT_ERR_BAD_PARAM, "unknown tuning key " + k);
     return DDT_SUCCESS;

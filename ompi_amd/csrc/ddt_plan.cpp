@@ -26,10 +26,12 @@
 
 namespace ddt {
 
-Tuning &tuning()
+// The defaults with the environment applied (DDT_* and the reference's OMPI_MCA_* forms): the
+// initial values, and what ddt_tune("reset") restores.
+Tuning tuning_defaults()
 {
-    static Tuning t = [] {
-        Tuning v;
+    Tuning v;
+    {
         if (const char *e = std::getenv("DDT_NT"))
             v.nt = e[0] == '1' ? 1 : 0;
         if (const char *e = std::getenv("DDT_TASK_KB"))
@@ -59,8 +61,13 @@ Tuning &tuning()
         v.opt_growth = std::clamp<long>(v.opt_growth, 0, 1024);
         v.opt_unroll_items = std::max<long>(v.opt_unroll_items, 0);
         v.opt_unroll_bytes = std::max<long>(v.opt_unroll_bytes, 0);
-        return v;
-    }();
+    }
+    return v;
+}
+
+Tuning &tuning()
+{
+    static Tuning t = tuning_defaults();
     return t;
 }
 

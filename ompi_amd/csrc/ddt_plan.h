@@ -65,6 +65,7 @@ struct Tuning {
     long consolidate = 250;
 };
 Tuning &tuning();
+Tuning tuning_defaults();   // the defaults with the environment's DDT_* / OMPI_MCA_* values applied
 // Synchronous host -> device copy on a library-private stream (capture-safe).
 hipError_t upload(void *dst, const void *src, size_t n);
 // While one lives, this thread's stream-capture mode is relaxed: the event queries, allocations

@@ -128,3 +128,24 @@ def test_consolidated_send_positions_follow_its_description():
     total = 300 * 20
     for p in sorted(rng.randrange(total) for _ in range(50)):
         assert e.snap_position(p) == o.set_position(1, p, send=True), p
+
+
+def test_reset_restores_the_environment_threshold():
+    """OMPI_MCA_datatype_consolidate_threshold sets the initial threshold; ddt_tune("reset")
+    restores it (not the compiled default)."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from tests import recipes as R\n"
+        "from ompi_amd._lib import lib\n"
+        "b = R.Built(('vector', 16, 1, 3, ('basic', 16)))\n"
+        "assert b.engine().consolidate(999) is None\n"
+        "assert lib().ddt_tune(b'consolidate', 5) == 0 and b.engine().consolidate(999) is not None\n"
+        "assert lib().ddt_tune(b'reset', 0) == 0 and b.engine().consolidate(999) is None\n"
+        "assert b.engine().consolidate(1000) is not None\n"
+        "print('ok')\n" % os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, OMPI_MCA_datatype_consolidate_threshold="1000")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
