@@ -114,6 +114,13 @@ hipError_t upload(void *dst, const void *src, size_t n)
 // or a launching stream is capturing now) is kept for good.
 Plan::~Plan()
 {
+    // events for fences (the pool's and the launch slots') are the plan's device's: a destroy may
+    // run with another device current, and an event of that device recorded on this device's
+    // streams would fail and mark the release unknown
+    int cur = -1;
+    const bool other = device >= 0 && hipGetDevice(&cur) == hipSuccess && cur != device
+                       && hipSetDevice(device) == hipSuccess;
+    (void) hipGetLastError();
     std::vector<void *> blocks;
     auto take_set = [&](ItemSet &S) {
         for (hipEvent_t e : S.late)
@@ -151,13 +158,6 @@ Plan::~Plan()
         sorted->take_blocks(blocks);
     std::vector<hipEvent_t> fences;
     bool unknown = false;
-    // the fences are events of the plan's device (a destroy may run with another device
-    // current: an event of that device recorded on this device's streams would fail and mark the
-    // release unknown)
-    int cur = -1;
-    const bool other = device >= 0 && hipGetDevice(&cur) == hipSuccess && cur != device
-                       && hipSetDevice(device) == hipSuccess;
-    (void) hipGetLastError();
     const bool fenced = !captured && pool_fences(streams, fences, unknown);
     if (other)
         (void) hipSetDevice(cur);
