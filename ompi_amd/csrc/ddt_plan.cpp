@@ -340,11 +340,22 @@ void slot_trim()
 {
     Slots &S = slots();
     std::lock_guard<std::mutex> g(S.mu);
-    for (auto &kv : S.dev)
+    int cur = -1;
+    const bool known = hipGetDevice(&cur) == hipSuccess;
+    for (auto &kv : S.dev) {
+        // the fences are events of the binding's device (another device's would fail to record
+        // and keep the slot taken for good)
+        if (known && kv.first != cur && hipSetDevice(kv.first) != hipSuccess) {
+            (void) hipGetLastError();
+            continue;
+        }
         for (SlotFamily &F : kv.second)
             for (SlotEntry &E : F.e)
                 if (E.used)
                     (void) end_binding(E, E.streams);
+    }
+    if (known)
+        (void) hipSetDevice(cur);
 }
 
 void slot_stats(int dev, int64_t *out4)
