@@ -18,7 +18,8 @@ pytestmark = pytest.mark.gpu
 
 def _dev(arr, device):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(arr)).to(device)
+    # writable and C-contiguous (a read-only fixture view would make torch warn)
+    return torch.from_numpy(np.require(arr, requirements=["C", "W"])).to(device)
 
 
 def _host(t):
