@@ -1195,14 +1195,21 @@ void assign_tasks(std::vector<Item> &items, int dir)
                 continue;
             }
             uint64_t cap = tb;
+            bool sparse = false;
             if (it.kind == ITEM_AFFINE) {
                 const uint64_t pass = uint64_t(THREADS) * unroll_of(it.U) * it.U;
-                const bool sparse = it.upb * it.U <= 64;
+                sparse = it.upb * it.U <= 64;
                 cap = pass * uint64_t(sparse ? 1 : std::max<long>(1, tuning().spass));
                 if (!sparse && tuning().stask > 0)
                     cap = uint64_t(tuning().stask);
             }
-            const uint64_t b = tb < cap ? tb : cap;
+            uint64_t b = tb < cap ? tb : cap;
+            // sparse gathers (one element per line) take at least four units per lane even in a
+            // small launch: four independent line loads in flight per lane instead of two (a
+            // single-field x face, 512 KiB: pack 3.15 -> 2.94 us, alternating pack/unpack 3.8 ->
+            // 3.2 us per operation; 16 KiB tasks 3.96; profiles/r5_b2b_x_tasks.jsonl)
+            if (sparse)
+                b = std::min(cap, std::max(b, uint64_t(THREADS) * 4 * it.U));
             uint64_t u = b / it.U;
             it.units_per_task = u < THREADS ? THREADS : u;
         }
