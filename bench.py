@@ -350,12 +350,14 @@ def back_to_back(dev, fields, K=200, faces=("x", "y", "z"), with_copy=True):
         tiny.add_(1)
     out["empty_kernel_us"] = {m: round(timed(empty, m), 3) for m in ("eager", "host", "graph")}
     for k in faces:
-        ft = ER.build_committed(recs[k])
+        # "h": the whole 6-face halo type (the bench's workload) at this field count, engine only
+        ft = ER.build_committed(halo_recipe()[0] if k == "h" else recs[k])
         S = ft.info()["size"] * fields
         pk = torch.empty(S, dtype=torch.uint8, device=dev)
         cv = ompi_amd.Convertor()
-        kind, es, ls, ss, base, lw = face_floor_part(k, fields)
-        part = Part(kind, es, ls[0], ls[1], ls[2], lw, ss[0], ss[1], ss[2], base, 0)
+        if k != "h":
+            kind, es, ls, ss, base, lw = face_floor_part(k, fields)
+            part = Part(kind, es, ls[0], ls[1], ls[2], lw, ss[0], ss[1], ss[2], base, 0)
 
         def engine(d):
             def f(i, s=None):
@@ -382,7 +384,8 @@ def back_to_back(dev, fields, K=200, faces=("x", "y", "z"), with_copy=True):
                 dd = d if d < 2 else i & 1
                 (pk.copy_(src) if dd == 0 else src.copy_(pk))
             return f
-        paths = [("engine", engine), ("bare", bare)] + ([("copy", copy)] if with_copy and k != "x" else [])
+        paths = [("engine", engine)] + ([("bare", bare)] if k != "h" else []) \
+            + ([("copy", copy)] if with_copy and k not in ("x", "h") else [])
         res = {"bytes": S, "hbm_us": round(2 * S / HBM_MEASURED * 1e6, 3)}
         res["model_us"] = [round(res["hbm_us"] + x, 3) for x in BOUNDARY_US]
         for name, mk in paths:

@@ -1751,6 +1751,8 @@ int ddt_tune(const char *key, long value)
         tuning().uinterleave = value < 0 ? -1 : value;
     else if (k == "slots")
         tuning().slots = value ? 1 : 0;
+    else if (k == "sfloor")
+        tuning().sfloor = value;
     else if (k == "slot_max_kb")
         tuning().slot_max_kb = value < 0 ? 0 : value;
     else if (k == "policy")

@@ -1187,6 +1187,10 @@ void assign_tasks(std::vector<Item> &items, int dir)
         uint64_t tb = 4096;
         while (tb < (64u << 10) && tb * 1024 < total)
             tb *= 2;
+        bool all_sparse = true;
+        for (const Item &it : items)
+            if (!(it.kind == ITEM_AFFINE && !it.nbytes && it.upb * it.U <= 64))
+                all_sparse = false;
         for (Item &it : items) {
             if (it.kind != ITEM_AFFINE && it.kind != ITEM_LIST_UNI)
                 continue;
@@ -1204,11 +1208,15 @@ void assign_tasks(std::vector<Item> &items, int dir)
                     cap = uint64_t(tuning().stask);
             }
             uint64_t b = tb < cap ? tb : cap;
-            // sparse gathers (one element per line) take at least four units per lane even in a
-            // small launch: four independent line loads in flight per lane instead of two (a
-            // single-field x face, 512 KiB: pack 3.15 -> 2.94 us, alternating pack/unpack 3.8 ->
-            // 3.2 us per operation; 16 KiB tasks 3.96; profiles/r5_b2b_x_tasks.jsonl)
-            if (sparse)
+            // a launch of sparse gathers only (one element per line) takes at least four units
+            // per lane even when small: four independent line loads in flight per lane instead
+            // of two (a single-field x face, 512 KiB: pack 3.15 -> 2.94 us, alternating
+            // pack/unpack 3.75 -> 3.18 us per operation; 16 KiB tasks 3.96).  Not beside streams:
+            // the single-field halo's alternating pair goes 5.67 -> 6.39 us with it.  Pack and
+            // unpack must agree (with the floor on one side only the x face's pair takes 4.2-4.5
+            // us: a task's lines are in its XCD's L2 for the other direction's same task);
+            // profiles/r5_b2b_x_tasks.jsonl
+            if (sparse && all_sparse && (tuning().sfloor == 2 || tuning().sfloor == dir))
                 b = std::min(cap, std::max(b, uint64_t(THREADS) * 4 * it.U));
             uint64_t u = b / it.U;
             it.units_per_task = u < THREADS ? THREADS : u;

@@ -20,6 +20,7 @@ struct Tuning {
     long uinterleave = 256;  // the same for an unpack (-1: as `interleave`); see assign_tasks
     long slots = 1;       // argument-free launches of hot descriptor sets (ddt_move_slot_kernel); 0 off
     long slot_max_kb = 4096;  // ... for launches of at most this many packed KiB
+    long sfloor = 2;      // sparse-gather task floor (4 units per lane): 0 pack, 1 unpack, 2 both, -1 off
     int policy = 1;       // task sizing: 0 = v0 (~6 K tasks), 1 = per-leaf passes
     int wt = -1;          // write-through (sc1) stores: -1 auto, 0 off, 1 sparse user side, 2 all
     long sorted = -1;     // address-ordered list engine: -1 auto, 0 off, n > 0 from n blocks up
