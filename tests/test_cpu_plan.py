@@ -295,3 +295,28 @@ def test_opal_bigcount_large_contiguous():
         assert t.size == n and i["ub"] - i["lb"] == n and (i["true_lb"], i["true_ub"]) == (0, n)
         assert t.get_elements(n) == n
     assert t.plan_info()["leaves"] == 1
+
+
+def test_sparse_only_launch_task_floor():
+    """ddt_plan.cpp:assign_tasks: a small launch of sparse gathers alone (a single-field x face,
+    one 8-B element per line) takes four units per lane per task (1024 units); beside streams
+    (the single-field halo) its x leaves keep two (512); ddt_tune("sfloor", -1) switches it off
+    (profiles/r5_b2b_x_tasks.jsonl)."""
+    import bench
+    from ompi_amd import lib
+    from ompi_amd import recipe as ER
+    L = lib()
+    x = ER.build_committed(bench.face_recipes()["x"])
+    halo = ER.build_committed(bench.halo_recipe()[0])
+
+    def upt(t, count):
+        its = E.items(t, count, 0, 0, 0, t.info()["size"] * count)
+        return {int(it.units_per_task) for it in its if it.kind == E.ITEM_AFFINE and it.U == 8}
+
+    try:
+        assert upt(x, 1) == {1024}
+        assert upt(halo, 1) == {512}
+        L.ddt_tune(b"sfloor", -1)
+        assert upt(x, 1) == {512}
+    finally:
+        L.ddt_tune(b"reset", 0)
