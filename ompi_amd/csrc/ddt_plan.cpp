@@ -1155,6 +1155,9 @@ void stream_policy(std::vector<Item> &items)
                 it.nt = 2;
 }
 
+// the chip's CUs: a sparse-only launch with fewer tasks than this takes the task floor below
+constexpr uint64_t kFloorTasks = 256;
+
 void assign_tasks(std::vector<Item> &items, int dir)
 {
     uint64_t total = 0;
@@ -1187,10 +1190,6 @@ void assign_tasks(std::vector<Item> &items, int dir)
         uint64_t tb = 4096;
         while (tb < (64u << 10) && tb * 1024 < total)
             tb *= 2;
-        bool all_sparse = true;
-        for (const Item &it : items)
-            if (!(it.kind == ITEM_AFFINE && !it.nbytes && it.upb * it.U <= 64))
-                all_sparse = false;
         for (Item &it : items) {
             if (it.kind != ITEM_AFFINE && it.kind != ITEM_LIST_UNI)
                 continue;
@@ -1199,27 +1198,40 @@ void assign_tasks(std::vector<Item> &items, int dir)
                 continue;
             }
             uint64_t cap = tb;
-            bool sparse = false;
             if (it.kind == ITEM_AFFINE) {
                 const uint64_t pass = uint64_t(THREADS) * unroll_of(it.U) * it.U;
-                sparse = it.upb * it.U <= 64;
+                const bool sparse = it.upb * it.U <= 64;
                 cap = pass * uint64_t(sparse ? 1 : std::max<long>(1, tuning().spass));
                 if (!sparse && tuning().stask > 0)
                     cap = uint64_t(tuning().stask);
             }
-            uint64_t b = tb < cap ? tb : cap;
-            // a launch of sparse gathers only (one element per line) takes at least four units
-            // per lane even when small: four independent line loads in flight per lane instead
-            // of two (a single-field x face, 512 KiB: pack 3.15 -> 2.94 us, alternating
-            // pack/unpack 3.75 -> 3.18 us per operation; 16 KiB tasks 3.96).  Not beside streams:
-            // the single-field halo's alternating pair goes 5.67 -> 6.39 us with it.  Pack and
-            // unpack must agree (with the floor on one side only the x face's pair takes 4.2-4.5
-            // us: a task's lines are in its XCD's L2 for the other direction's same task);
-            // profiles/r5_b2b_x_tasks.jsonl
-            if (sparse && all_sparse && (tuning().sfloor == 2 || tuning().sfloor == dir))
-                b = std::min(cap, std::max(b, uint64_t(THREADS) * 4 * it.U));
+            const uint64_t b = tb < cap ? tb : cap;
             uint64_t u = b / it.U;
             it.units_per_task = u < THREADS ? THREADS : u;
+        }
+        // A launch of sparse gathers alone (one element per line) too small to give every CU a
+        // task takes four units per lane: four independent line loads in flight per lane instead
+        // of two or one (a single-field x face, 512 KiB, 128 -> 64 tasks: pack 3.15 -> 2.94 us,
+        // alternating pack/unpack 3.75 -> 3.18 us per operation).  Launches that fill the CUs keep
+        // their tasks (x face at 2 / 4 fields: 4.1 / 5.7 us against 4.6 / 5.9 with the floor; at 8
+        // fields the floor would win 0.5 us), and so do sparse leaves beside streams (the single-
+        // field halo's pair 5.67 -> 6.39 us with it).  Pack and unpack must agree: with the floor
+        // on one side only the x face's pair takes 4.2-4.5 us (a task's lines sit in its XCD's L2
+        // for the other direction's same task).  profiles/r5_b2b_x_tasks.jsonl
+        if (tuning().sfloor == 2 || tuning().sfloor == dir) {
+            bool all_sparse = !items.empty();
+            uint64_t ntasks = 0;
+            for (const Item &it : items) {
+                if (!(it.kind == ITEM_AFFINE && !it.nbytes && it.upb * it.U <= 64))
+                    all_sparse = false;
+                else
+                    ntasks += (it.u1 - it.u0 + it.units_per_task - 1) / it.units_per_task;
+            }
+            if (all_sparse && ntasks < kFloorTasks)
+                for (Item &it : items) {
+                    const uint64_t cap = uint64_t(THREADS) * unroll_of(it.U);   // one pass, in units
+                    it.units_per_task = std::min(cap, std::max<uint64_t>(it.units_per_task, uint64_t(THREADS) * 4));
+                }
         }
     }
     // Split items into runs of `chunk` tasks and order the runs by their fractional position

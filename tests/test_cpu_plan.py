@@ -298,7 +298,7 @@ def test_opal_bigcount_large_contiguous():
 
 
 def test_sparse_only_launch_task_floor():
-    """ddt_plan.cpp:assign_tasks: a small launch of sparse gathers alone (a single-field x face,
+    """ddt_plan.cpp:assign_tasks: a launch of sparse gathers alone with fewer tasks than CUs (a single-field x face,
     one 8-B element per line) takes four units per lane per task (1024 units); beside streams
     (the single-field halo) its x leaves keep two (512); ddt_tune("sfloor", -1) switches it off
     (profiles/r5_b2b_x_tasks.jsonl)."""
