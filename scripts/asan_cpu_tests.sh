@@ -21,5 +21,6 @@ wait
   -o build_asan/libddt_hip_asan.so build_asan/*.o
 cd ../..
 ASAN_RT=$(/opt/rocm/bin/hipcc -print-file-name=libclang_rt.asan-x86_64.so)
-DDT_LIB_PATH=$PWD/ompi_amd/csrc/build_asan/libddt_hip_asan.so LD_PRELOAD=$ASAN_RT \
+# the ASan runtime goes first; whatever the environment already preloads stays in the list
+DDT_LIB_PATH=$PWD/ompi_amd/csrc/build_asan/libddt_hip_asan.so LD_PRELOAD=$ASAN_RT${LD_PRELOAD:+:$LD_PRELOAD} \
   ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 python -m pytest tests -q -x -m "not gpu" -p no:cacheprovider "$@"
