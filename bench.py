@@ -60,6 +60,20 @@ def face_recipes(n=256, esize=8, tid=16):
     }
 
 
+def cfg3_face_recipes(n=512):
+    """BASELINE config 3's three faces of the 512^3 float grid (C order, start 511), each alone
+    and resized to the field (ompi_datatype_create_subarray.c:32-112): dim0 = the last plane
+    (1 MiB contiguous), dim1 = 512 rows of 2 KiB at a plane stride, dim2 = 4-byte elements at a
+    2 KiB row stride."""
+    field = n * n * n * 4
+    f4 = ("basic", 15)
+    return {
+        "dim0": ("resized", ("subarray", [n] * 3, [1, n, n], [n - 1, 0, 0], 0, f4), 0, field),
+        "dim1": ("resized", ("subarray", [n] * 3, [n, 1, n], [0, n - 1, 0], 0, f4), 0, field),
+        "dim2": ("resized", ("subarray", [n] * 3, [n, n, 1], [0, 0, n - 1], 0, f4), 0, field),
+    }
+
+
 def lcg_disps(n):
     """cfg4 displacements: x_{i+1} = (1664525 x_i + 1013904223) mod 2^28, x_0 = 0x5EED."""
     out = np.empty(n, dtype=np.int64)
@@ -356,7 +370,7 @@ def back_to_back(dev, fields, K=200, faces=("x", "y", "z"), with_copy=True):
         pk = torch.empty(S, dtype=torch.uint8, device=dev)
         cv = ompi_amd.Convertor()
         if k != "h":
-            kind, es, ls, ss, base, lw = face_floor_part(k, fields)
+            kind, es, ls, ss, base, lw = face_floor_part(k, fields, grid=grid)
             part = Part(kind, es, ls[0], ls[1], ls[2], lw, ss[0], ss[1], ss[2], base, 0)
 
         def engine(d):
@@ -409,7 +423,7 @@ def back_to_back(dev, fields, K=200, faces=("x", "y", "z"), with_copy=True):
 
 
 # ------------------------------------------------------------------ per-face throughput
-def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z"), flush="read"):
+def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z"), flush="read", grid="cfg2"):
     """The north star's per-face figure: ONE face type of the 256^3
     double grid over `fields` fields in one launch (count = fields), pack then unpack, each
     timed with HIP events (median over `steps`).  With 512 fields a face's working set
@@ -424,12 +438,17 @@ def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z"), flush="
                (during the flush, outside the events);
       "write": a fill writes it, so each operation starts cold but with up to 256 MiB of dirty
                scribble lines whose write-back it pays inside its own events;
-      None:    no flush (the face's own 512 MiB working set, partly cache-resident)."""
+      None:    no flush (the face's own 512 MiB working set, partly cache-resident).
+
+    grid "cfg3": config 3's faces of the 512^3 float grid instead (faces dim0 / dim1 / dim2).
+    Faces of single elements (x, dim2) also report the rate in 128-byte lines: each element is
+    one whole-line request (profiles/r5_counter_calibration.json)."""
     import torch
     import ompi_amd
     from ompi_amd import recipe as ER
-    recs = face_recipes()
-    field = 256 ** 3 * 8
+    recs = face_recipes() if grid == "cfg2" else cfg3_face_recipes()
+    field = 256 ** 3 * 8 if grid == "cfg2" else 512 ** 3 * 4
+    elem = 8 if grid == "cfg2" else 4
     user = torch.empty(fields * field, dtype=torch.uint8, device=dev)
     user.fill_(0x5A)
     scribble = torch.full((1 << 27,), 3, dtype=torch.int64, device=dev) if flush else None
@@ -486,12 +505,20 @@ def face_throughput(dev, fields, steps, warmup=2, faces=("x", "y", "z"), flush="
         out[k] = {"packed_bytes": fS, "pack_us": round(tp * 1e6, 2), "unpack_us": round(tu * 1e6, 2),
                   "GiBs": round(2 * fS / (tp + tu) / GiB, 1), "frac": round(4 * fS / (tp + tu) / HBM_PEAK, 4),
                   "pack_frac": round(2 * fS / tp / HBM_PEAK, 4), "unpack_frac": round(2 * fS / tu / HBM_PEAK, 4)}
+        if k in ("x", "dim2"):
+            # one element per 128-byte line: the memory moves whole lines (the pack reads them,
+            # the unpack's partial writes complete as whole lines below the L2)
+            lines = fS // elem
+            out[k]["line_bytes"] = lines * 128
+            out[k]["pack_line_GBs"] = round(lines * 128 / tp / 1e9, 1)
+            out[k]["pack_line_frac"] = round(lines * 128 / tp / HBM_PEAK, 4)
+            out[k]["unpack_line_GBs"] = round((lines * 128 + fS) / tu / 1e9, 1)
         # the same protocol around the face's bare kernel (ompi_amd/csrc/ddt_floor.hip): same
         # buffers, events, flushes; frac_of_floor = floor / engine (1.0 = the engine at the floor)
         try:
             import ctypes
             L, Part = floor_lib()
-            kind, es, ls, ss, base, lw = face_floor_part(k, fields)
+            kind, es, ls, ss, base, lw = face_floor_part(k, fields, grid=grid)
             part = Part(kind, es, ls[0], ls[1], ls[2], lw, ss[0], ss[1], ss[2], base, 0)
             fev = []
             for i in range(warmup + steps):
@@ -586,11 +613,19 @@ def floor_lib():
     return _FLOOR
 
 
-def face_floor_part(face, fields, n=256, e=8):
-    """One face type of the 256^3 double grid over `fields` fields (a power of two) as a floor
-    part: x = element gather/scatter, y = 2 KiB rows, z = 512 KiB planes."""
+def face_floor_part(face, fields, n=256, e=8, grid="cfg2"):
+    """One face type over `fields` fields (a power of two) as a floor part.  cfg2 (256^3
+    double): x = element gather/scatter, y = 2 KiB rows, z = 512 KiB planes; cfg3 (512^3 float,
+    start 511): dim0 = the 1 MiB last plane, dim1 = 2 KiB rows at a plane stride, dim2 = 4-byte
+    elements at a 2 KiB row stride (floor_parts("cfg3") per face)."""
     lf = fields.bit_length() - 1
     assert 1 << lf == fields
+    if grid == "cfg3":
+        n, e = 512, 4
+        field, row, plane = n * n * n * e, n * e, n * n * e
+        return {"dim0": (1, 0, (lf, 0, 0), (field, 0, 0), (n - 1) * plane, 16),
+                "dim1": (1, 0, (9, lf, 0), (plane, field, 0), (n - 1) * row, 7),
+                "dim2": (0, 4, (18, lf, 0), (row, field, 0), (n - 1) * e, 0)}[face]
     field, row, plane = n * n * n * e, n * e, n * n * e
     return {"x": (0, 8, (16, lf, 0), (row, field, 0), 0, 0),
             "y": (1, 0, (8, lf, 0), (plane, field, 0), 0, 7),
@@ -918,6 +953,23 @@ def gather_check(packed, S, world, rank, dev, backend):
             "seconds": round(g_s, 4)}
 
 
+def per_rank_times(tp, tu, world, dev, backend):
+    """All ranks' pack / unpack event times (seconds in, ms out), all-gathered after the timed
+    region: min / max over ranks and the per-rank list in rank order."""
+    import torch
+    import torch.distributed as dist
+    mine = torch.tensor([tp * 1e3, tu * 1e3], dtype=torch.float64,
+                        device=dev if backend == "nccl" else "cpu")
+    allk = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allk, mine)
+    rk = [[round(float(x[0]), 4), round(float(x[1]), 4)] for x in allk]
+    return {"pack": {"min": min(r[0] for r in rk), "max": max(r[0] for r in rk)},
+            "unpack": {"min": min(r[1] for r in rk), "max": max(r[1] for r in rk)},
+            "ranks": rk,
+            "source": "each rank's HIP events on every Nth timed step, all-gathered after the timed "
+                      "region; [pack_ms, unpack_ms] per rank in rank order"}
+
+
 # ------------------------------------------------------------------ main
 def main():
     ap = argparse.ArgumentParser()
@@ -1082,6 +1134,10 @@ def main():
     tp = float(np.mean([a.elapsed_time(b) for a, b, _ in ev])) / 1e3
     tu = float(np.mean([b.elapsed_time(c) for _, b, c in ev])) / 1e3
 
+    # Every rank's own pack / unpack event times, gathered outside the timed region, so an N > 1
+    # line shows the imbalance or a slow rank behind the max-over-ranks wall time
+    per_rank = per_rank_times(tp, tu, world, dev, backend) if world > 1 else None
+
     # The same K steps captured once into a HIP graph and replayed: the launch-bound
     # regime a persistent halo exchange runs in (reported beside the eager value).
     graph_step = None
@@ -1205,6 +1261,7 @@ def main():
             "per_gpu_GiBs_from_events": round(2.0 * S / (tp + tu) / GiB, 3),
             "all_gather_check": rccl,
             "kernel_ms": {"pack": round(tp * 1e3, 4), "unpack": round(tu * 1e3, 4)},
+            "per_rank_kernel_ms": per_rank,
             "graph_replay_GiBs_per_gpu": (round(2.0 * S / graph_step / GiB, 3) if graph_step else None),
             # achieved/frac: the step's pack + unpack launches together (traffic is per step too);
             # dominant_kernel: the longer of the two alone, 2S over its own event time
@@ -1283,10 +1340,20 @@ def main():
                 result[key][k]["back_to_back_us"] = bb[k]["back_to_back_us"]
                 result[key][k]["graph_us"] = bb[k]["graph_us"]
 
+    if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_faces and not split:
+        # config 3's faces alone: dim0 / dim1 / dim2 of the 512^3 float grid,
+        # cold and clean over --face-fields fields (default 64 here: 32 GiB of fields), with
+        # each face's bare kernel under the same protocol
+        user = packed = None
+        torch.cuda.empty_cache()
+        ff = min(args.face_fields, 64)
+        result["faces"] = face_throughput(dev, ff, max(5, min(args.steps, 20)),
+                                          faces=("dim0", "dim1", "dim2"), grid="cfg3")
+
     if rank == 0 and world == 1 and args.e2e:
         # the path starts and ends in host memory (north star): the copies to and from the GPU
         # included, for the small, the default and the largest config, pinned and pageable
-        del user, packed
+        user = packed = None
         torch.cuda.empty_cache()
         result["e2e"] = [end_to_end(dev, c, pageable=pg, reps=5)
                          for c in ("cfg1", "cfg2", "cfg5") for pg in (False, True)]

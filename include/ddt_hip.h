@@ -333,13 +333,25 @@ int ddt_type_cache_info(const ddt_datatype_t *type, int64_t *out4);
  * bytes, blocks kept for graphs, blocks in use]. */
 int ddt_trim(void);
 int ddt_pool_info(int64_t *out6);
-/* Argument-free launches: a descriptor set launched on the same buffers twice within three calls
- * (two bindings per set) is bound to one of 8 launch records per direction in device memory, and its later launches on
+/* Argument-free launches: a descriptor set launched on the same buffers again within its last 8 launches
+ * (up to 8 bindings per set) is bound to one of 32 launch records per direction in device memory, and its later launches on
  * those buffers take no kernel arguments (HIP writes device-resident kernel arguments across
  * PCIe: ~2.9 us of host time per launch with arguments, 0.7 us without).  ddt_slot_info: out4 =
  * [pack slots bound, unpack slots bound (current device), binds so far, argument-free launches
  * so far].  ddt_tune("slots", 0) turns them off; ddt_trim ends every binding. */
 int ddt_slot_info(int64_t *out4);
+/* Diagnostic: the state of launch slot k of direction dir (0 pack, 1 unpack) on the current
+ * device: bit 0 bound, bit 1 ending (its binding ended but the fences on its streams could not be
+ * recorded yet, e.g. one is capturing: never rebound before they are), bits 8.. the number of
+ * streams its binding launched on; -1 when no slot of that direction exists yet. */
+int ddt_slot_state(int dir, int k);
+/* Synchronous completion (round 6): a synchronous pack / unpack (MPI_Pack, MPI_Unpack, a
+ * convertor without the async flag) returns once a signal kernel enqueued behind its work has
+ * written a pinned host word, instead of HIP's ~9.5 us completion round trip; it falls back to
+ * hipStreamSynchronize when the stream captures, all 16 signal slots are taken, a window is in
+ * host memory, or the word is not seen within 20 ms.  ddt_tune("sigsync", 0) turns it off.
+ * out3 = [calls completed by the signal, signal fallbacks (timeout), plain stream syncs]. */
+int ddt_sync_info(int64_t *out3);
 /* ---- introspection for the CPU test-suite (no data movement; never used by pack/unpack) ----
  * ddt_type_plan_leaves: serialises the plan's leaf streams as int64 records
  *   [kind, blen, src_off, dst_off, ndim, list_leaf_index, (cnt, sstr, dstr) x ndim] and returns

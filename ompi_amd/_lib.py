@@ -100,6 +100,8 @@ SIGNATURES = {
     "ddt_trim": (c_int, []),
     "ddt_pool_info": (c_int, [P(c_int64)]),
     "ddt_slot_info": (c_int, [P(c_int64)]),
+    "ddt_slot_state": (c_int, [c_int, c_int]),
+    "ddt_sync_info": (c_int, [P(c_int64)]),
     "ddt_type_plan_leaves": (c_int64, [c_void_p, P(c_int64), c_size_t]),
     "ddt_debug_items": (c_int, [c_void_p, c_size_t, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                 ctypes.c_uint64, c_int, c_void_p, c_size_t, P(c_size_t), P(c_size_t)]),

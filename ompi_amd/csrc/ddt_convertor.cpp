@@ -10,8 +10,10 @@
 // it in opal_convertor_generic_simple_position, opal_datatype_position.c:167-367).
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 
@@ -107,6 +109,106 @@ bool capturing(hipStream_t s)
     return cs != hipStreamCaptureStatusNone;
 }
 
+// ---------------------------------------------------------------- synchronous completion
+// A synchronous call returns once the device says its work is done.  HIP's own answer
+// (hipStreamSynchronize) is a ~9.5 us round trip whatever the kernel; the engine instead enqueues
+// a signal kernel (ddt_kernels.hip) behind the call's work and spins on the pinned host word it
+// writes, falling back to hipStreamSynchronize when no signal slot is free, the stream captures,
+// the setup failed, or the word does not arrive within kSigSpin (the work is long, or faulted:
+// hipStreamSynchronize then reports the error).
+struct SigDev {
+    std::mutex mu;
+    bool tried = false, ok = false;
+    uint32_t *page = nullptr;                 // kSigSlots lines of a pinned host page
+    std::atomic<uint32_t> busy{0};            // one bit per slot owned by a call
+    uint32_t expect[kSigSlots] = {};          // the slot owner's count of its signals
+};
+std::atomic<int64_t> g_sig_fast{0}, g_sig_fallback{0}, g_sig_plain{0};
+
+SigDev *sig_device()
+{
+    static SigDev devs[64];
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) {
+        (void) hipGetLastError();
+        return nullptr;
+    }
+    SigDev &D = devs[d];
+    std::lock_guard<std::mutex> g(D.mu);
+    if (!D.tried) {
+        D.tried = true;
+        void *p = nullptr;
+        hipStream_t ps = nullptr;
+        if (hipHostMalloc(&p, 4096, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+            std::memset(p, 0, 4096);
+            void *dp = nullptr;
+            if (hipHostGetDevicePointer(&dp, p, 0) == hipSuccess && private_stream(&ps) == hipSuccess
+                && signal_setup(static_cast<uint32_t *>(dp), ps) == hipSuccess) {
+                D.page = static_cast<uint32_t *>(p);
+                D.ok = true;
+            }
+        }
+        (void) hipGetLastError();
+    }
+    return D.ok ? &D : nullptr;
+}
+
+hipError_t complete_sync(hipStream_t s, bool signal_ok)
+{
+    SigDev *D = (signal_ok && tuning().sigsync && !capturing(s)) ? sig_device() : nullptr;
+    int k = -1;
+    if (D) {
+        uint32_t b = D->busy.load(std::memory_order_relaxed);
+        while (k < 0 && b != (1u << kSigSlots) - 1u) {
+            const int f = __builtin_ctz(~b);
+            if (D->busy.compare_exchange_weak(b, b | (1u << f), std::memory_order_acquire))
+                k = f;
+        }
+    }
+    if (k < 0) {
+        ++g_sig_plain;
+        return hipStreamSynchronize(s);
+    }
+    const uint32_t want = ++D->expect[k];
+    hipError_t e = launch_signal(k, s);
+    if (e != hipSuccess) {
+        --D->expect[k];   // the kernel did not run: the device count did not move
+        D->busy.fetch_and(~(1u << k), std::memory_order_release);
+        ++g_sig_plain;
+        (void) hipGetLastError();
+        return hipStreamSynchronize(s);
+    }
+    const volatile uint32_t *w = D->page + k * kSigStride;
+    bool seen = false;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1;; ++i) {
+        if (int32_t(__atomic_load_n(const_cast<const uint32_t *>(w), __ATOMIC_ACQUIRE) - want) >= 0) {
+            seen = true;
+            break;
+        }
+        if ((i & 1023u) == 0
+            && std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count()
+                   > double(tuning().sigspin_us))
+            break;
+        __builtin_ia32_pause();
+    }
+    D->busy.fetch_and(~(1u << k), std::memory_order_release);
+    if (seen) {
+        ++g_sig_fast;
+        return hipSuccess;
+    }
+    ++g_sig_fallback;
+    return hipStreamSynchronize(s);
+}
+
+// A capture this call can see: on its stream, or one that makes the legacy stream unusable
+// (another thread's global-mode capture).  Only then do its allocations skip the device-wide
+// settle of fenceless releases (PoolNoDeviceSync).
+bool capture_seen(hipStream_t s)
+{
+    return capturing(s) || (s != nullptr && capturing(nullptr));
+}
+
 bool events_passed(const std::vector<hipEvent_t> &evs)
 {
     for (hipEvent_t e : evs) {
@@ -132,7 +234,7 @@ void recycle(Plan &P, Retired &r)   // P.mu held
     S.late.clear();
     for (ItemSet::Binding &b : S.bind)
         if (b.slot >= 0) {   // every launch of the set has passed: its record is free
-            slot_release(S.slot_dev, b.slot >> 8, b.slot & 15, b.gen, nullptr);
+            slot_release(S.slot_dev, b.slot >> 8, b.slot & 255, b.gen, nullptr);
             b.slot = -1;
         }
     if (S.d_items) {
@@ -315,7 +417,10 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                 uint8_t *u = reinterpret_cast<uint8_t *>(user + uint64_t(L.list_shift) + uint64_t(P.dev[0].disp_base)
                                                          + i * uint64_t(t->extent()));
                 uint8_t *pk = reinterpret_cast<uint8_t *>(wins[0].ptr + i * uint64_t(t->size));
-                HIPCHK(SL->run(u, pk, dir, uint32_t(tuning().spol), stream, uint32_t(tuning().sunroll),
+                // spol bits, plus the pass-2 quads (256) and the pass-1 stagger (bits 16..23)
+                const uint32_t pol = uint32_t(tuning().spol) | (tuning().s2vec ? 256u : 0u)
+                                     | (uint32_t(std::min<long>(tuning().sstagger, 255)) << 16);
+                HIPCHK(SL->run(u, pk, dir, pol, stream, uint32_t(tuning().sunroll),
                                uint32_t(tuning().s2unroll)));
             }
             return DDT_SUCCESS;
@@ -364,7 +469,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         } else if (!S->items.empty()) {
             size_t bytes = S->items.size() * sizeof(Item);
             RelaxedCapture relaxed;   // reap queries, allocation, upload: leave other threads' captures be
-            PoolNoDeviceSync no_sync;
+            PoolNoDeviceSync no_sync(capture_seen(stream));
             {
                 std::lock_guard<std::mutex> g(P.mu);
                 S->d_items = take_items_memory(P, bytes, !capturing(stream));
@@ -434,7 +539,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         if (S->inline_ok && !S->retired && ++S->uses >= 2 && !S->d_items && tuning().ptr) {
             size_t bytes = S->items.size() * sizeof(Item);
             RelaxedCapture relaxed;
-            PoolNoDeviceSync no_sync;
+            PoolNoDeviceSync no_sync(capture_seen(stream));
             Item *d = take_items_memory(P, bytes, !capturing(stream));
             if (d) {
                 if (upload(d, S->items.data(), bytes) == hipSuccess)
@@ -454,9 +559,9 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             } else if (tuning().slots && grid_cap == 0 && !S->all_dense && !S->has_lists && !S->retired
                        && S->bytes <= uint64_t(tuning().slot_max_kb) << 10) {
                 // an argument-free launch (ddt_move.hip.h, ddt_move_slot_kernel): a set bound to
-                // a slot for these buffers and this direction; buffers seen twice in the set's
-                // last three launches bind one (its record is in device memory before this launch;
-                // two bindings per set serve a double-buffered exchange).  Small launches only: a slot
+                // a slot for these buffers and this direction; buffers seen again within the set's
+                // last kHist launches bind one (its record is in device memory before this launch;
+                // two bindings serve a double-buffered exchange).  Small launches only: a slot
                 // kernel's workgroups first load the record (one more dependent load than
                 // arguments preloaded into registers), which a large launch of latency-bound
                 // gathers pays (the halo's 48 MiB pack 66.4 -> 68.2 us), while the host's 2.2 us
@@ -464,43 +569,61 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                 const int fam = dir << 8;
                 ++S->launches;
                 int hit = -1;
-                for (int i = 0; i < 2; ++i)
-                    if (S->bind[i].slot >= 0 && (S->bind[i].slot & ~15) == fam && S->bind[i].ubase == ubase
+                for (int i = 0; i < ItemSet::kSetBind; ++i)
+                    if (S->bind[i].slot >= 0 && (S->bind[i].slot & ~255) == fam && S->bind[i].ubase == ubase
                         && S->bind[i].pbase == pbase)
                         hit = i;
-                const bool seen = (S->hist_u[0] == ubase && S->hist_p[0] == pbase)
-                                  || (S->hist_u[1] == ubase && S->hist_p[1] == pbase);
-                if (hit < 0 && seen) {
-                    // bind these buffers in a free binding, else in place of the less recent one
-                    // (given up behind fences on the set's streams)
-                    hit = S->bind[0].slot < 0 ? 0 : S->bind[1].slot < 0 ? 1 : (S->bind[0].used <= S->bind[1].used ? 0 : 1);
-                    ItemSet::Binding &B = S->bind[hit];
-                    if (B.slot >= 0) {
-                        slot_release(S->slot_dev, B.slot >> 8, B.slot & 15, B.gen, &S->streams);
-                        B.slot = -1;
+                bool seen = false;
+                for (int i = 0; i < ItemSet::kHist; ++i)
+                    seen = seen || (S->hist_u[i] == ubase && S->hist_p[i] == pbase);
+                if (hit < 0 && seen && S->launches >= S->bind_backoff) {
+                    // bind these buffers in a free binding, else in place of the least recently
+                    // used one if it sat idle for kSetIdle launches of the set (given up behind
+                    // fences on the set's streams).  A binding in use is never taken: threads
+                    // sharing the set on more buffer pairs than it holds bindings keep theirs,
+                    // the rest launch with arguments (round 6: taking turns rebound on every
+                    // call, a synchronous record upload each, bridgethreads shared 4 threads
+                    // 16.8 us per call)
+                    constexpr uint64_t kSetIdle = 32, kBindBackoff = 32;
+                    int pick = -1, lru = 0;
+                    for (int i = 0; i < ItemSet::kSetBind && pick < 0; ++i)
+                        if (S->bind[i].slot < 0)
+                            pick = i;
+                        else if (S->bind[i].used < S->bind[lru].used)
+                            lru = i;
+                    if (pick < 0 && S->launches - S->bind[lru].used >= kSetIdle)
+                        pick = lru;
+                    if (pick >= 0) {
+                        ItemSet::Binding &B = S->bind[pick];
+                        if (B.slot >= 0) {
+                            slot_release(S->slot_dev, B.slot >> 8, B.slot & 255, B.gen, &S->streams);
+                            B.slot = -1;
+                        }
+                        const LaunchRec rec{uint64_t(uintptr_t(d_items)), ubase, pbase, uint32_t(S->items.size()),
+                                            S->ntasks};
+                        const int k = slot_bind(P.device, dir, rec, &B.gen);
+                        if (k >= 0) {
+                            B.slot = fam | k;
+                            B.ubase = ubase;
+                            B.pbase = pbase;
+                            S->slot_dev = P.device;
+                            hit = pick;
+                        }
                     }
-                    const LaunchRec rec{uint64_t(uintptr_t(d_items)), ubase, pbase, uint32_t(S->items.size()),
-                                        S->ntasks};
-                    const int k = slot_bind(P.device, dir, rec, &B.gen);
-                    if (k >= 0) {
-                        B.slot = fam | k;
-                        B.ubase = ubase;
-                        B.pbase = pbase;
-                        S->slot_dev = P.device;
-                    } else {
-                        hit = -1;
-                    }
+                    // every binding of the set in use: do not rescan on every call (a full slot
+                    // table is retried at once: each attempt ages the table's idle bindings)
+                    if (pick < 0)
+                        S->bind_backoff = S->launches + kBindBackoff;
                 }
                 if (hit >= 0) {
                     S->bind[hit].used = S->launches;
-                    slot_k = S->bind[hit].slot & 15;
+                    slot_k = S->bind[hit].slot & 255;
                     slot_gen = S->bind[hit].gen;
                     slot_b = hit;
                 }
-                S->hist_u[1] = S->hist_u[0];
-                S->hist_p[1] = S->hist_p[0];
-                S->hist_u[0] = ubase;
-                S->hist_p[0] = pbase;
+                S->hist_u[S->hist_at] = ubase;
+                S->hist_p[S->hist_at] = pbase;
+                S->hist_at = (S->hist_at + 1) % ItemSet::kHist;
             }
             if (std::find(S->streams.begin(), S->streams.end(), stream) == S->streams.end())
                 S->streams.push_back(stream);
@@ -726,8 +849,10 @@ int execute(ddt_convertor *c, const std::vector<Window> &dev_wins,
         if (dir == 0)
             HIPCHK(hipStreamWaitEvent(c->stream, c->ev_free, 0));
     }
+    // data in place on return: the signal kernel when every window is device memory (the
+    // staged and PCIe paths end in host memory written by copies or over the link)
     if (!c->async)
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(complete_sync(c->stream, host_wins.empty() && !pcie));
     return DDT_SUCCESS;
 }
 
@@ -1522,7 +1647,7 @@ int ddt_copy_content_same_ddt(const ddt_datatype_t *t, size_t count, void *dst, 
     int rc = run_windows(dt, *P, count, uint64_t(uintptr_t(src)), w, true, 0, s);
     if (rc != DDT_SUCCESS)
         return rc;
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(complete_sync(s, true));   // both sides in HBM: the signal kernel's word
     return DDT_SUCCESS;
 }
 
@@ -1736,6 +1861,26 @@ int ddt_slot_info(int64_t *out4)
     return DDT_SUCCESS;
 }
 
+int ddt_sync_info(int64_t *out3)
+{
+    if (!out3)
+        return DDT_ERR_BAD_PARAM;
+    out3[0] = g_sig_fast.load();
+    out3[1] = g_sig_fallback.load();
+    out3[2] = g_sig_plain.load();
+    return DDT_SUCCESS;
+}
+
+int ddt_slot_state(int dir, int k)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void) hipGetLastError();
+        return -1;
+    }
+    return (dir == 0 || dir == 1) ? slot_debug_state(dev, dir, k) : -1;
+}
+
 int ddt_tune(const char *key, long value)
 {
     if (!key)
@@ -1779,6 +1924,14 @@ int ddt_tune(const char *key, long value)
         tuning().s2unroll = value >= 16 ? 16 : (value >= 8 ? 8 : 4);
     else if (k == "dsplit")
         tuning().dsplit = value ? 1 : 0;
+    else if (k == "sigsync")
+        tuning().sigsync = value ? 1 : 0;
+    else if (k == "sigspin_us")
+        tuning().sigspin_us = value < 0 ? 0 : value;
+    else if (k == "s2vec")
+        tuning().s2vec = value ? 1 : 0;
+    else if (k == "sstagger")
+        tuning().sstagger = value < 0 ? 0 : (value > 255 ? 255 : value);
     else if (k == "sunroll")
         tuning().sunroll = value >= 16 ? 16 : (value >= 8 ? 8 : 4);
     else if (k == "sseg")

@@ -136,20 +136,28 @@ struct ItemSet {
     bool retired = false;
     std::vector<hipEvent_t> late;
     ItemBlock blk{};
-    // argument-free launches (run_windows): up to two launch-slot bindings, each for one
-    // direction and one pair of buffers (a double-buffered exchange alternates two), and the
-    // buffers of the two previous launches by pointer (a set binds buffers seen twice in its last
-    // three launches)
+    // argument-free launches (run_windows): up to kSetBind launch-slot bindings, each for one
+    // direction and one pair of buffers (a double-buffered exchange alternates two; threads
+    // sharing a type each bring theirs, r6), and the buffers of the kHist previous launches by
+    // pointer (a set binds buffers seen again within them)
+    static constexpr int kSetBind = 8, kHist = 8;
     struct Binding {
         int slot = -1;            // (dir << 8) | k, -1 none
         uint32_t gen = 0;
         uint64_t ubase = 0, pbase = 0;
-        uint64_t used = 0;        // launches of the set when last used (the older one is given up)
+        uint64_t used = 0;        // launches of the set when last used
     };
-    Binding bind[2];
+    Binding bind[kSetBind];
     int slot_dev = -1;
     uint64_t launches = 0;
-    uint64_t hist_u[2] = {~0ull, ~0ull}, hist_p[2] = {~0ull, ~0ull};
+    uint64_t bind_backoff = 0;    // no bind attempt before `launches` reaches this
+    uint64_t hist_u[kHist], hist_p[kHist];
+    uint32_t hist_at = 0;
+    ItemSet()
+    {
+        for (int i = 0; i < kHist; ++i)
+            hist_u[i] = hist_p[i] = ~0ull;
+    }
     ~ItemSet();
 };
 

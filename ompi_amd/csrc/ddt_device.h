@@ -129,8 +129,12 @@ constexpr uint32_t ITEM_ARG_DIMS = 4;
 
 // The launch record of an argument-free move launch (ddt_move.hip.h, ddt_move_slot_kernel):
 // NSLOT records per (direction, lists) kernel family per device, bound by the host to hot
-// descriptor sets on fixed buffers (ddt_plan.cpp: slot_bind).
-constexpr uint32_t NSLOT = 8;
+// descriptor sets on fixed buffers (ddt_plan.cpp: slot_bind).  A launch of record k asks for
+// (k + 1) x SLOT_LDS_UNIT bytes of dynamic LDS, which the kernel (static LDS 0) reads back from
+// its dispatch packet (round 6: one kernel per direction for any number of records; round 5 had
+// one inlined kernel per record, 8 per direction).
+constexpr uint32_t NSLOT = 32;
+constexpr uint32_t SLOT_LDS_UNIT = 256;
 struct LaunchRec {
     uint64_t items;    // const Item * in device memory
     uint64_t ubase, pbase;

@@ -153,6 +153,8 @@ hipError_t launch_move_slot_p0(uint32_t k, uint32_t ntasks, hipStream_t stream);
 hipError_t launch_move_slot_u0(uint32_t k, uint32_t ntasks, hipStream_t stream);
 hipError_t slot_table_p0(void **addr);
 hipError_t slot_table_u0(void **addr);
+hipError_t slot_probe_p0(uint32_t *d_out, hipStream_t stream);
+hipError_t slot_probe_u0(uint32_t *d_out, hipStream_t stream);
 
 hipError_t launch_move_slot(int dir, uint32_t k, uint32_t ntasks, hipStream_t stream)
 {
@@ -162,6 +164,65 @@ hipError_t launch_move_slot(int dir, uint32_t k, uint32_t ntasks, hipStream_t st
 hipError_t slot_table(int dir, void **addr)
 {
     return dir == 0 ? slot_table_p0(addr) : slot_table_u0(addr);
+}
+
+hipError_t slot_probe(int dir, uint32_t *d_out, hipStream_t stream)
+{
+    return dir == 0 ? slot_probe_p0(d_out, stream) : slot_probe_u0(d_out, stream);
+}
+
+// ---------------------------------------------------------------- completion signal
+// A synchronous call (MPI_Pack / MPI_Unpack, a convertor without ACCELERATOR_ASYNC) must return
+// with the data in place (pack.c.in:129-150).  HIP's completion round trip costs ~9.5 us for a
+// kernel of any size (profiles/r5_hostcost_sync.jsonl); instead, the call enqueues behind its move
+// kernels the argument-free kernel of a signal slot S, which bumps S's device counter and stores
+// the new value to S's word of a pinned, host-coherent page with a system-scope release, and the
+// host spins on that word (ddt_convertor.cpp: complete_sync).  The kernel starts only after the
+// stream's previous work completed, and so after that work's end-of-kernel release.
+constexpr int NSIG_KERNEL = 16;   // = kSigSlots (ddt_plan.h)
+constexpr int SIG_STRIDE = 16;    // words between slots: one 64-byte line each
+static __device__ uint32_t *g_sig_host;
+static __device__ uint32_t g_sig_count[NSIG_KERNEL];
+
+template <int S>
+__global__ __launch_bounds__(64) void ddt_signal_kernel()
+{
+    if (threadIdx.x == 0) {
+        const uint32_t v = __hip_atomic_fetch_add(&g_sig_count[S], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        __hip_atomic_store(g_sig_host + S * SIG_STRIDE, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+hipError_t signal_setup(uint32_t *host_page, hipStream_t s)
+{
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sig_host), &host_page, sizeof(host_page), 0,
+                                          hipMemcpyHostToDevice, s);
+    return e != hipSuccess ? e : hipStreamSynchronize(s);
+}
+
+hipError_t launch_signal(int k, hipStream_t stream)
+{
+    const dim3 g(1), b(64);
+    switch (k) {
+    case 0: hipLaunchKernelGGL(ddt_signal_kernel<0>, g, b, 0, stream); break;
+    case 1: hipLaunchKernelGGL(ddt_signal_kernel<1>, g, b, 0, stream); break;
+    case 2: hipLaunchKernelGGL(ddt_signal_kernel<2>, g, b, 0, stream); break;
+    case 3: hipLaunchKernelGGL(ddt_signal_kernel<3>, g, b, 0, stream); break;
+    case 4: hipLaunchKernelGGL(ddt_signal_kernel<4>, g, b, 0, stream); break;
+    case 5: hipLaunchKernelGGL(ddt_signal_kernel<5>, g, b, 0, stream); break;
+    case 6: hipLaunchKernelGGL(ddt_signal_kernel<6>, g, b, 0, stream); break;
+    case 7: hipLaunchKernelGGL(ddt_signal_kernel<7>, g, b, 0, stream); break;
+    case 8: hipLaunchKernelGGL(ddt_signal_kernel<8>, g, b, 0, stream); break;
+    case 9: hipLaunchKernelGGL(ddt_signal_kernel<9>, g, b, 0, stream); break;
+    case 10: hipLaunchKernelGGL(ddt_signal_kernel<10>, g, b, 0, stream); break;
+    case 11: hipLaunchKernelGGL(ddt_signal_kernel<11>, g, b, 0, stream); break;
+    case 12: hipLaunchKernelGGL(ddt_signal_kernel<12>, g, b, 0, stream); break;
+    case 13: hipLaunchKernelGGL(ddt_signal_kernel<13>, g, b, 0, stream); break;
+    case 14: hipLaunchKernelGGL(ddt_signal_kernel<14>, g, b, 0, stream); break;
+    case 15: hipLaunchKernelGGL(ddt_signal_kernel<15>, g, b, 0, stream); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- external32

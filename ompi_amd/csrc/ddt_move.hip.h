@@ -7,6 +7,7 @@
 #include <cstdlib>
 
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
 
 #include "ddt_device.h"
 #include "ddt_plan.h"
@@ -833,12 +834,27 @@ __global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restric
 // constant address space: the record loads are scalar and uniform (as kernel arguments are);
 // from a __device__ array the compiler kept the fields in vector registers (92 VGPRs against
 // the pointer kernel's 56) and large launches lost occupancy
-static __constant__ LaunchRec g_launch[NSLOT];
+static __constant__ LaunchRec g_launch[NSLOT + 1];   // [NSLOT]: never bound, ntasks 0
 
-template <int DIR, bool LISTS, uint32_t K>
+// The record index of an argument-free launch: its dispatch packet's group_segment_size (the
+// kernel's static LDS, 0, plus the launch's dynamic LDS of (k + 1) x SLOT_LDS_UNIT), read through
+// the dispatch pointer -- an SGPR input of the wave, not a kernel argument.  Out of range (a
+// launch that did not ask for slot LDS): NSLOT, and the kernel does nothing.  slot_probe checks
+// the decoding on each device before any record is bound.
+__device__ __forceinline__ uint32_t slot_index()
+{
+    using CPacket = const __attribute__((address_space(4))) hsa_kernel_dispatch_packet_t;
+    CPacket *pk = (CPacket *) __builtin_amdgcn_dispatch_ptr();
+    const uint32_t k = pk->group_segment_size / SLOT_LDS_UNIT - 1u;
+    return k < NSLOT ? k : NSLOT;
+}
+
+template <int DIR, bool LISTS>
 __global__ __launch_bounds__(THREADS) void ddt_move_slot_kernel()
 {
-    const LaunchRec &r = g_launch[K];
+    // no branch on k: the record table's address load issues beside the packet load, and an
+    // out-of-range launch reads the never-bound record [NSLOT] (no tasks)
+    const LaunchRec &r = g_launch[slot_index()];
     // the descriptor set is read-only for the kernel's lifetime, as a kernel-argument pointer is:
     // in the constant address space its uniform loads are scalar (a plain pointer loaded from
     // memory gives flat vector loads and twice the registers)
@@ -848,22 +864,20 @@ __global__ __launch_bounds__(THREADS) void ddt_move_slot_kernel()
         move_task<DIR, LISTS>(items, r.nitems, Bases{r.ubase, r.pbase}, blockIdx.x);
 }
 
+// slot_probe: the index every launch of k reads back (out[k]), and out[NSLOT] for a launch
+// without slot LDS (must be NSLOT: no record)
+static __global__ __attribute__((unused)) __launch_bounds__(64) void ddt_slot_probe_kernel(uint32_t *out)
+{
+    if (threadIdx.x == 0)
+        out[0] = slot_index();
+}
+
 template <int DIR, bool LISTS>
 static void launch_slot(uint32_t k, uint32_t grid, hipStream_t stream)
 {
-    const dim3 g(grid), b(THREADS);
-    switch (k) {
-    case 0: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 0>), g, b, 0, stream); break;
-    case 1: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 1>), g, b, 0, stream); break;
-    case 2: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 2>), g, b, 0, stream); break;
-    case 3: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 3>), g, b, 0, stream); break;
-    case 4: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 4>), g, b, 0, stream); break;
-    case 5: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 5>), g, b, 0, stream); break;
-    case 6: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 6>), g, b, 0, stream); break;
-    default: hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 7>), g, b, 0, stream); break;
-    }
+    hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS>), dim3(grid), dim3(THREADS), (k + 1) * SLOT_LDS_UNIT,
+                       stream);
 }
-static_assert(NSLOT == 8, "launch_slot dispatches eight slot kernels");
 
 // Small launches carry their descriptors in the kernel-argument segment: no device
 // buffer, no upload, no cache entry (fragment pipelines, windows, one-off messages).
@@ -973,6 +987,13 @@ static void launch_inline(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, 
     hipError_t slot_table_##TAG(void **addr)                                                           \
     {                                                                                                  \
         return hipGetSymbolAddress(addr, HIP_SYMBOL(g_launch));                                        \
+    }                                                                                                  \
+    hipError_t slot_probe_##TAG(uint32_t *d_out, hipStream_t stream)                                   \
+    {                                                                                                  \
+        for (uint32_t k = 0; k <= NSLOT; ++k)                                                          \
+            hipLaunchKernelGGL(ddt_slot_probe_kernel, dim3(1), dim3(64),                               \
+                               k < NSLOT ? (k + 1) * SLOT_LDS_UNIT : 0u, stream, d_out + k);           \
+        return hipGetLastError();                                                                      \
     }
 
 }  // namespace ddt

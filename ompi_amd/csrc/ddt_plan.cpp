@@ -51,9 +51,20 @@ Tuning tuning_defaults()
         mca("loop_unroll_max_items", v.opt_unroll_items);
         mca("loop_unroll_max_data_bytes", v.opt_unroll_bytes);
         if (const char *e = std::getenv("OMPI_MCA_opal_datatype_optimize_preserve_type")) {
-            // an MCA bool: 0/1, true/false, yes/no
-            const std::string b(e);
-            preserve = (b == "0" || b == "false" || b == "no" || b == "f" || b == "n") ? 0 : 1;
+            // an MCA bool as mca_base_var parses one (mca_base_var_enum_bool_vfs,
+            // mca_base_var_enum.c:77-104): leading whitespace skipped, an integer (0 false, else
+            // true), or exactly true/t/enabled/yes/y, false/f/disabled/no/n; anything else is
+            // refused (OPAL_ERR_VALUE_OUT_OF_BOUNDS) and the default kept
+            const char *p = e + std::strspn(e, " \t\n\v\f\r");
+            char *end = nullptr;
+            const long iv = std::strtol(p, &end, 10);
+            const std::string b(p);
+            if (*end == '\0')
+                preserve = iv != 0;
+            else if (b == "true" || b == "t" || b == "enabled" || b == "yes" || b == "y")
+                preserve = 1;
+            else if (b == "false" || b == "f" || b == "disabled" || b == "no" || b == "n")
+                preserve = 0;
         }
         v.opt_preserve = int(preserve);
         if (const char *e = std::getenv("OMPI_MCA_datatype_consolidate_threshold"))
@@ -128,7 +139,7 @@ Plan::~Plan()
         S.late.clear();
         for (ItemSet::Binding &b : S.bind)
             if (b.slot >= 0) {   // free once every stream that launched the plan's work passes
-                slot_release(S.slot_dev, b.slot >> 8, b.slot & 15, b.gen, &streams);
+                slot_release(S.slot_dev, b.slot >> 8, b.slot & 255, b.gen, &streams);
                 b.slot = -1;
             }
         if (!S.d_items)
@@ -181,33 +192,63 @@ Plan::~Plan()
 // previous binding has passed: a binding ends by release (its set's memory is recycled, or its
 // plan is destroyed: fences on the plan's streams) or by eviction (idle for kEvictIdle slot
 // launches of the device while another set wants a slot: fences on the streams the binding
-// launched on).  Slot launches are enqueued under the table lock, so an eviction's fences follow
-// every launch of the binding it ends; a set whose binding ended (generation changed) launches
-// with arguments again and may bind anew.
+// launched on).  A set whose binding ended (generation changed) launches with arguments again and
+// may bind anew.
+//
+// Locking (round 6, for MPI_THREAD_MULTIPLE callers: the reference's convertor path takes no lock,
+// SURVEY §8b): each slot entry has its own mutex, held across its argument-free launch and taken
+// to end its binding, so an ending's fences follow every launch of the binding; each family
+// (device, direction) has a mutex for binds, evictions and releases, taken before an entry's.
+// Threads launching different slots never wait on each other, and a bind's synchronous record
+// upload blocks only other binds of its family.
+//
+// An ending whose fences cannot be recorded (a stream of the binding is capturing now, or an
+// event cannot be created) leaves the entry taken and "ending" with its streams kept: no launch
+// of the binding follows (its generation moved), and later binds and ddt_trim retry the fences
+// (the entry is never picked as an eviction victim or freed without them).
 namespace {
 constexpr uint64_t kEvictIdle = 256;   // ticks: slot launches and bind attempts of the process
+constexpr int kMaxDev = 64;
 struct SlotEntry {
+    std::mutex mu;                      // launches of this record; changes of its binding
     bool used = false;
+    bool ending = false;                // binding ended, fences not recorded yet: retry
     uint32_t gen = 0;                   // bumped when a binding ends
-    uint64_t last = 0;                  // tick of the last launch or bind
+    std::atomic<uint64_t> last{0};      // tick of the last launch or bind
     std::vector<hipStream_t> streams;   // streams the binding launched on
     std::vector<hipEvent_t> fences;     // the last binding's launches: passed before the next bind
 };
 struct SlotFamily {
+    std::mutex mu;                      // binds, evictions, releases, trims (before any entry's)
     bool init = false;
     LaunchRec *rec = nullptr;           // the family's record table on its device
     SlotEntry e[NSLOT];
 };
 struct Slots {
-    std::mutex mu;
-    std::map<int, std::array<SlotFamily, 2>> dev;   // per device: pack, unpack
-    uint64_t tick = 0;
+    std::mutex mu;                                   // creation of a device's families
+    std::atomic<std::array<SlotFamily, 2> *> dev[kMaxDev] = {};   // per device: pack, unpack
+    std::atomic<uint64_t> tick{0};
     std::atomic<int64_t> binds{0}, launches{0};
 };
 Slots &slots()
 {
     static Slots *s = new Slots();   // never destroyed: releases may come at exit
     return *s;
+}
+std::array<SlotFamily, 2> *families(Slots &S, int dev, bool create)
+{
+    if (dev < 0 || dev >= kMaxDev)
+        return nullptr;
+    std::array<SlotFamily, 2> *f = S.dev[dev].load(std::memory_order_acquire);
+    if (f || !create)
+        return f;
+    std::lock_guard<std::mutex> g(S.mu);
+    f = S.dev[dev].load(std::memory_order_acquire);
+    if (!f) {
+        f = new std::array<SlotFamily, 2>();   // never destroyed, like the table
+        S.dev[dev].store(f, std::memory_order_release);
+    }
+    return f;
 }
 bool fences_passed(std::vector<hipEvent_t> &f)
 {
@@ -221,13 +262,23 @@ bool fences_passed(std::vector<hipEvent_t> &f)
     f.clear();
     return true;
 }
-// End entry E's binding behind events on `streams` (false: no fence could be recorded, the slot
-// stays taken for good -- its record may still be read).  Table lock held.
-bool end_binding(SlotEntry &E, const std::vector<hipStream_t> &streams)
+// End entry E's binding behind events on its streams plus `extra` (false: no fence could be
+// recorded now; the entry stays taken and ending, for a later retry).  Family lock held.
+bool end_binding(SlotEntry &E, const std::vector<hipStream_t> *extra = nullptr)
 {
-    ++E.gen;
+    std::lock_guard<std::mutex> g(E.mu);   // after any launch of the binding in progress
+    if (!E.used)
+        return true;
+    if (!E.ending) {
+        ++E.gen;   // no launch of this binding from now on
+        E.ending = true;
+    }
+    if (extra)
+        for (hipStream_t st : *extra)
+            if (std::find(E.streams.begin(), E.streams.end(), st) == E.streams.end())
+                E.streams.push_back(st);
     std::vector<hipEvent_t> f;
-    for (hipStream_t st : streams) {
+    for (hipStream_t st : E.streams) {
         hipEvent_t e = nullptr;
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone
@@ -237,27 +288,54 @@ bool end_binding(SlotEntry &E, const std::vector<hipStream_t> &streams)
                 (void) hipEventDestroy(e);
             for (hipEvent_t x : f)
                 (void) hipEventDestroy(x);
-            E.streams.clear();
-            return false;
+            return false;   // streams kept: the retry fences all of them
         }
         f.push_back(e);
     }
     E.used = false;
+    E.ending = false;
     E.streams.clear();
     E.fences.insert(E.fences.end(), f.begin(), f.end());
     return true;
 }
-SlotFamily *family(Slots &S, int dev, int dir)   // table lock held
+// The slot kernels find their record index in their dispatch packet (ddt_move.hip.h slot_index):
+// checked once per family and device before the first bind, on the private stream.
+bool probe_ok(int dir)
 {
-    SlotFamily &F = S.dev[dev][size_t(dir)];
-    if (!F.init) {
-        void *p = nullptr;
-        if (slot_table(dir, &p) != hipSuccess || !p) {
-            (void) hipGetLastError();
-            return nullptr;
+    hipStream_t s = nullptr;
+    if (private_stream(&s) != hipSuccess)
+        return false;
+    uint32_t *d = static_cast<uint32_t *>(pool_alloc((NSLOT + 1) * sizeof(uint32_t)));
+    if (!d)
+        return false;
+    uint32_t h[NSLOT + 1] = {};
+    bool ok = hipMemsetAsync(d, 0xFF, (NSLOT + 1) * sizeof(uint32_t), s) == hipSuccess
+              && slot_probe(dir, d, s) == hipSuccess
+              && hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s) == hipSuccess
+              && hipStreamSynchronize(s) == hipSuccess;
+    for (uint32_t k = 0; ok && k <= NSLOT; ++k)
+        ok = h[k] == k;
+    (void) hipStreamSynchronize(s);
+    pool_free(d);
+    return ok;
+}
+SlotFamily *family(Slots &S, int dev, int dir, bool create)   // family lock NOT held
+{
+    std::array<SlotFamily, 2> *fs = families(S, dev, create);
+    if (!fs)
+        return nullptr;
+    SlotFamily &F = (*fs)[size_t(dir)];
+    if (create) {
+        std::lock_guard<std::mutex> g(F.mu);
+        if (!F.init) {
+            void *p = nullptr;
+            if (slot_table(dir, &p) != hipSuccess || !p || !probe_ok(dir)) {
+                (void) hipGetLastError();
+                return nullptr;   // no argument-free launches on this device: launches keep arguments
+            }
+            F.rec = static_cast<LaunchRec *>(p);
+            F.init = true;
         }
-        F.rec = static_cast<LaunchRec *>(p);
-        F.init = true;
     }
     return &F;
 }
@@ -268,51 +346,63 @@ int slot_bind(int dev, int dir, const LaunchRec &rec, uint32_t *gen)
     RelaxedCapture relaxed;   // fence queries and the upload: never another thread's capture's business
     PoolNoDeviceSync no_sync;
     Slots &S = slots();
-    std::lock_guard<std::mutex> g(S.mu);
-    SlotFamily *F = family(S, dev, dir);
+    SlotFamily *F = family(S, dev, dir, true);
     if (!F)
         return -1;
-    ++S.tick;   // bind attempts age the bindings too: a full table of idle sets does not block
+    std::lock_guard<std::mutex> g(F->mu);
+    const uint64_t now = ++S.tick;   // bind attempts age the bindings too: a full table of idle sets does not block
     int victim = -1;
+    uint64_t vlast = 0;
     for (uint32_t k = 0; k < NSLOT; ++k) {
         SlotEntry &E = F->e[k];
         if (E.used) {
-            if (S.tick - E.last >= kEvictIdle && (victim < 0 || E.last < F->e[victim].last))
+            if (E.ending) {   // an ending whose fences could not be recorded: retry them
+                (void) end_binding(E);
+                continue;
+            }
+            const uint64_t l = E.last.load(std::memory_order_relaxed);
+            if (now - l >= kEvictIdle && (victim < 0 || l < vlast)) {
                 victim = int(k);
+                vlast = l;
+            }
             continue;
         }
         if (!fences_passed(E.fences))
             continue;
         // on the library-private stream, waited for: the record is in place before any
-        // stream's next launch, and the caller's stream (capturing or not) is not touched
+        // stream's next launch, and the caller's stream (capturing or not) is not touched.
+        // No launch reads this free record, so its entry lock is not needed for the upload.
         if (upload(F->rec + k, &rec, sizeof(rec)) != hipSuccess) {
             (void) hipGetLastError();
             return -1;
         }
+        std::lock_guard<std::mutex> ge(E.mu);
         E.used = true;
-        E.last = ++S.tick;
+        E.last.store(++S.tick, std::memory_order_relaxed);
         *gen = E.gen;
         ++S.binds;
         return int(k);
     }
     if (victim >= 0)   // free it for a later bind, once its launches pass
-        (void) end_binding(F->e[victim], F->e[victim].streams);
+        (void) end_binding(F->e[victim]);
     return -1;
 }
 
 bool slot_launch(int dev, int dir, int k, uint32_t gen, uint32_t ntasks, hipStream_t stream, hipError_t *err)
 {
     Slots &S = slots();
-    std::lock_guard<std::mutex> g(S.mu);
-    SlotFamily *F = family(S, dev, dir);
-    if (!F || k < 0 || k >= int(NSLOT))
+    if (k < 0 || k >= int(NSLOT))
+        return false;
+    SlotFamily *F = family(S, dev, dir, false);
+    if (!F)
         return false;
     SlotEntry &E = F->e[k];
-    if (!E.used || E.gen != gen)
+    std::lock_guard<std::mutex> g(E.mu);   // this entry only: other slots launch concurrently
+    if (!E.used || E.ending || E.gen != gen)
         return false;   // the binding ended
     if (std::find(E.streams.begin(), E.streams.end(), stream) == E.streams.end())
         E.streams.push_back(stream);
-    E.last = ++S.tick;
+    E.last.store(++S.tick, std::memory_order_relaxed);
     *err = launch_move_slot(dir, uint32_t(k), ntasks, stream);
     ++S.launches;
     return true;
@@ -323,36 +413,46 @@ void slot_release(int dev, int dir, int k, uint32_t gen, const std::vector<hipSt
     if (k < 0 || k >= int(NSLOT))
         return;
     Slots &S = slots();
-    std::lock_guard<std::mutex> g(S.mu);
-    SlotEntry &E = S.dev[dev][size_t(dir)].e[k];
-    if (!E.used || E.gen != gen)
-        return;   // already ended (evicted)
-    if (fence_streams) {
-        (void) end_binding(E, *fence_streams);
-    } else {      // its launches have all passed
-        ++E.gen;
-        E.used = false;
-        E.streams.clear();
+    SlotFamily *F = family(S, dev, dir, false);
+    if (!F)
+        return;
+    std::lock_guard<std::mutex> g(F->mu);
+    SlotEntry &E = F->e[k];
+    {
+        std::lock_guard<std::mutex> ge(E.mu);
+        if (!E.used || E.ending || E.gen != gen)
+            return;   // already ended (evicted)
+        if (!fence_streams) {   // its launches have all passed
+            ++E.gen;
+            E.used = false;
+            E.streams.clear();
+            return;
+        }
     }
+    (void) end_binding(E, fence_streams);
 }
 
 void slot_trim()
 {
     Slots &S = slots();
-    std::lock_guard<std::mutex> g(S.mu);
     int cur = -1;
     const bool known = hipGetDevice(&cur) == hipSuccess;
-    for (auto &kv : S.dev) {
+    for (int d = 0; d < kMaxDev; ++d) {
+        std::array<SlotFamily, 2> *fs = families(S, d, false);
+        if (!fs)
+            continue;
         // the fences are events of the binding's device (another device's would fail to record
-        // and keep the slot taken for good)
-        if (known && kv.first != cur && hipSetDevice(kv.first) != hipSuccess) {
+        // and leave the slot ending until a later retry)
+        if (known && d != cur && hipSetDevice(d) != hipSuccess) {
             (void) hipGetLastError();
             continue;
         }
-        for (SlotFamily &F : kv.second)
+        for (SlotFamily &F : *fs) {
+            std::lock_guard<std::mutex> g(F.mu);
             for (SlotEntry &E : F.e)
                 if (E.used)
-                    (void) end_binding(E, E.streams);
+                    (void) end_binding(E);
+        }
     }
     if (known)
         (void) hipSetDevice(cur);
@@ -361,15 +461,30 @@ void slot_trim()
 void slot_stats(int dev, int64_t *out4)
 {
     Slots &S = slots();
-    std::lock_guard<std::mutex> g(S.mu);
     out4[0] = out4[1] = 0;
-    auto it = S.dev.find(dev);
-    if (it != S.dev.end())
-        for (int dir = 0; dir < 2; ++dir)
-            for (const SlotEntry &E : it->second[size_t(dir)].e)
+    if (std::array<SlotFamily, 2> *fs = families(S, dev, false))
+        for (int dir = 0; dir < 2; ++dir) {
+            SlotFamily &F = (*fs)[size_t(dir)];
+            std::lock_guard<std::mutex> g(F.mu);
+            for (const SlotEntry &E : F.e)
                 out4[dir] += E.used ? 1 : 0;
+        }
     out4[2] = S.binds.load();
     out4[3] = S.launches.load();
+}
+
+// Test hook (ddt_slot_debug): the state of slot k of (dev, dir): bit 0 used, bit 1 ending,
+// bits 8.. the number of streams its binding launched on; -1 when the family does not exist.
+int slot_debug_state(int dev, int dir, int k)
+{
+    Slots &S = slots();
+    SlotFamily *F = (k >= 0 && k < int(NSLOT)) ? family(S, dev, dir, false) : nullptr;
+    if (!F)
+        return -1;
+    std::lock_guard<std::mutex> g(F->mu);
+    SlotEntry &E = F->e[k];
+    std::lock_guard<std::mutex> ge(E.mu);
+    return (E.used ? 1 : 0) | (E.ending ? 2 : 0) | int(E.streams.size() << 8);
 }
 
 ItemSet::~ItemSet()

@@ -46,6 +46,10 @@ struct Tuning {
     long hd_grid_pack = 0;   // the same cap for a pack writing pinned host memory
     long sunroll = 16;    // address-ordered engine: pack 1 elements per thread in flight (4, 8, 16)
     long s2unroll = 8;    // the same for its unpack pass 2' 
+    long sigsync = 1;     // synchronous calls complete on the signal kernel's host word (r6); 0: hipStreamSynchronize
+    long sigspin_us = 20000;  // ... spinning at most this long before blocking in hipStreamSynchronize
+    long s2vec = 0;       // address-ordered engine, 4-byte elements: pass 2 / 2' four slots per lane (r6)
+    long sstagger = 0;    // address-ordered engine: pass 1 / 1' first-wave stagger, s_sleep(127) units (r6 A/B)
     long sseg = 1;        // address-ordered engine: U run padding, read at plan build: 1 = none (runs end
                           // to end, pass-1 chunks in XCD slabs; r5) or whole 32/64/128-byte segments
     long schunk = 1;      // address-ordered engine: 2 = half-size chunks, two pass-1 workgroups per
@@ -116,6 +120,16 @@ hipError_t launch_move(const Item *d_items, uint32_t nitems, uint32_t ntasks, in
 // family's record table (current device).
 hipError_t launch_move_slot(int dir, uint32_t k, uint32_t ntasks, hipStream_t stream);
 hipError_t slot_table(int dir, void **addr);
+// Launches the slot-index probe of direction dir on `stream`: d_out[k] = the index a slot launch
+// of record k decodes (k < NSLOT), d_out[NSLOT] = what a launch without slot LDS decodes (NSLOT).
+hipError_t slot_probe(int dir, uint32_t *d_out, hipStream_t stream);
+// Completion signal of synchronous calls (ddt_kernels.hip): kSigSlots argument-free signal
+// kernels; signal_setup points the current device's kernels at a pinned host page (one 64-byte
+// line per slot), launch_signal enqueues slot k's kernel.
+constexpr int kSigSlots = 16;
+constexpr int kSigStride = 16;   // uint32 words between slots
+hipError_t signal_setup(uint32_t *host_page, hipStream_t s);
+hipError_t launch_signal(int k, hipStream_t stream);
 // Launch slots (ddt_plan.cpp; affine launches only).  slot_bind: a free slot of direction `dir`
 // on device `dev` whose last binding's launches have passed, with `rec` written into it
 // (uploaded and waited for on the private stream) and its generation in *gen, or -1 (then a
@@ -130,6 +144,8 @@ void slot_release(int dev, int dir, int k, uint32_t gen, const std::vector<hipSt
 void slot_trim();
 // out4 = [pack slots bound on dev, unpack slots bound, binds so far, argument-free launches so far]
 void slot_stats(int dev, int64_t *out4);
+// bit 0 bound, bit 1 ending, bits 8.. streams of the binding; -1: no such family (ddt_slot_state)
+int slot_debug_state(int dev, int dir, int k);
 
 // external32 conversion between a native packed stream and its big-endian form.
 // uniform = C in {1,2,4,8,16}: every element is a C-byte word swap (C = 1: a copy) with identical native

@@ -144,8 +144,16 @@ void *take_free(Pool &P, int dev, size_t bytes)   // P.mu held
 
 }  // namespace
 
-PoolNoDeviceSync::PoolNoDeviceSync() { ++t_no_device_sync; }
-PoolNoDeviceSync::~PoolNoDeviceSync() { --t_no_device_sync; }
+PoolNoDeviceSync::PoolNoDeviceSync(bool on_) : on(on_)
+{
+    if (on)
+        ++t_no_device_sync;
+}
+PoolNoDeviceSync::~PoolNoDeviceSync()
+{
+    if (on)
+        --t_no_device_sync;
+}
 
 void *pool_alloc(size_t bytes)
 {

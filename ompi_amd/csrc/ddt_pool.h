@@ -48,9 +48,12 @@ int pool_trim();
 // While one lives on a thread, that thread's allocations never settle unknown releases by a
 // device synchronisation (the one call a relaxed-mode thread still may not make during another
 // thread's capture, profiles/r5_probe_capture.log): table builds at commit / import run under it.
+// `on` false: no effect (the hot path enables it only while a capture is seen, ADVICE r5, so its
+// allocations still settle such releases otherwise).
 struct PoolNoDeviceSync {
-    PoolNoDeviceSync();
+    explicit PoolNoDeviceSync(bool on = true);
     ~PoolNoDeviceSync();
+    bool on;
     PoolNoDeviceSync(const PoolNoDeviceSync &) = delete;
     PoolNoDeviceSync &operator=(const PoolNoDeviceSync &) = delete;
 };

@@ -74,6 +74,26 @@ constexpr uint32_t POL_UNPADDED = 64;
 // pass 1 / 1': chunks dealt to the XCDs in contiguous slabs (workgroups are dealt round-robin
 // over the 8 XCDs), so the runs of neighbouring chunks -- adjacent in U -- are written into one L2
 constexpr uint32_t POL_XCD_SLAB = 128;
+// pass 2 / 2' of 4-byte elements move four U slots per lane (one 16-byte U load or store, one
+// 8-byte upos load; round 6) and the packed side as 16-byte words when it is 16-byte aligned
+constexpr uint32_t POL_VEC2 = 256;
+// timing only (wrong results): LDS writes of the permutations go to conflict-free addresses
+// (pass 1: the element's own index, pass 2: its U slot), to price the bank conflicts
+constexpr uint32_t POL_NOCONF = 512;
+// bits 16..23: pass 1 / 1' start stagger (round 6 A/B): the first wave of workgroups (one per CU)
+// sleeps ((blockIdx / 8) % 4) x this many s_sleep(127) periods, so the CUs' gather and emission
+// phases do not run in lockstep
+constexpr uint32_t POL_STAGGER_SHIFT = 16;
+
+__device__ __forceinline__ void stagger(uint32_t pol)
+{
+    const uint32_t units = (pol >> POL_STAGGER_SHIFT) & 0xFFu;
+    if (!units || blockIdx.x >= 256u)
+        return;
+    const uint32_t n = ((blockIdx.x >> 3) & 3u) * units;
+    for (uint32_t i = 0; i < n; ++i)
+        __builtin_amdgcn_s_sleep(127);
+}
 
 __device__ __forceinline__ uint32_t chunk_of(uint32_t b, uint32_t n, uint32_t pol)
 {
@@ -302,10 +322,12 @@ __global__ __launch_bounds__(PT / CDIV) void k_pack1(const uint8_t *__restrict__
     __shared__ T lds[CH + SEG];
     __shared__ uint16_t toff[MAXNB / CDIV + 1];
     __shared__ uint32_t tub[MAXNB / CDIV];
+    stagger(pol);
     const uint32_t c = chunk_of(blockIdx.x, gridDim.x, pol), j0 = c * CH;
     const uint32_t m = min(CH, n - j0);
     stage_tables<NT>(off16, ub, c, nb, m, toff, tub);
     const T *src = reinterpret_cast<const T *>(user);
+    const bool noconf = pol & POL_NOCONF;
     // K elements per thread in flight: each is a dependent pair (offset, then the user
     // element), so K sets how many of the chunk's CH / PT per thread share one latency
     const uint32_t mg = (pol & POL_SKIP_USER) ? 0u : m;
@@ -323,7 +345,7 @@ __global__ __launch_bounds__(PT / CDIV) void k_pack1(const uint8_t *__restrict__
 #pragma unroll
         for (int q = 0; q < K; ++q)
             if (t0 + q * NT < m)
-                lds[s[q]] = v[q];
+                lds[noconf ? t0 + q * NT : s[q]] = v[q];
     }
     __syncthreads();
     emit_runs<E, SEGB, NT>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, nts, pol & POL_UNPADDED);
@@ -412,6 +434,133 @@ __global__ __launch_bounds__(PT) void k_unpack2(const uint8_t *__restrict__ pack
     }
 }
 
+
+// pass 2 / 2' of 4-byte elements, four U slots per lane (POL_VEC2, round 6).  U and upos are
+// read (or U written) as aligned quads of slots covering the bucket's [s0, s1); a quad shared
+// with a neighbouring bucket is read whole and used in part, and written element by element.
+// Allocation slack (dalloc: +16 bytes) covers the last quad's overrun.
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+
+template <int K>
+__global__ __launch_bounds__(PT) void k_pack2v(const uint8_t *__restrict__ U, const uint16_t *__restrict__ upos,
+                                               const uint32_t *__restrict__ bstart, uint8_t *__restrict__ packed,
+                                               uint32_t n, uint32_t pol)
+{
+    constexpr uint32_t RG = LDS_BYTES / 4;
+    const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS, noconf = pol & POL_NOCONF;
+    __shared__ uint32_t lds[RG];
+    const uint32_t k = blockIdx.x;
+    const uint32_t s0 = bstart[k], s1 = bstart[k + 1];
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(U);
+    const u16x4 *up = reinterpret_cast<const u16x4 *>(upos);
+    const uint32_t q0 = s0 >> 2, q1 = (s1 + 3) >> 2;
+    for (uint32_t x0 = q0 + threadIdx.x; x0 < q1; x0 += PT * K) {
+        u32x4 v[K];
+        u16x4 p[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const uint32_t x = x0 + q * PT;
+            if (x < q1) {
+                p[q] = ldp(&up[x], ntl);
+                v[q] = ldp(&src[x], ntl);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const uint32_t x = x0 + q * PT;
+            if (x >= q1)
+                continue;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t slot = 4 * x + e;
+                if (slot >= s0 && slot < s1 && p[q][e] != PAD)
+                    lds[noconf ? (slot - s0) & (RG - 1) : p[q][e]] = v[q][e];
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t m = min(RG, n - k * RG);
+    uint8_t *dst8 = packed + size_t(k) * RG * 4;
+    if ((reinterpret_cast<uintptr_t>(dst8) & 15) == 0) {
+        u32x4 *dst = reinterpret_cast<u32x4 *>(dst8);
+        const u32x4 *l4 = reinterpret_cast<const u32x4 *>(lds);
+        for (uint32_t t = threadIdx.x; t < m / 4; t += PT)
+            stp(&dst[t], l4[t], nts);
+        for (uint32_t t = (m & ~3u) + threadIdx.x; t < m; t += PT)
+            reinterpret_cast<uint32_t *>(dst8)[t] = lds[t];
+    } else {
+        uint32_t *dst = reinterpret_cast<uint32_t *>(dst8);
+        for (uint32_t t = threadIdx.x; t < m; t += PT)
+            stp(&dst[t], lds[t], nts);
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(PT) void k_unpack2v(const uint8_t *__restrict__ packed, const uint16_t *__restrict__ upos,
+                                                 const uint32_t *__restrict__ bstart, uint8_t *__restrict__ U,
+                                                 uint32_t n, uint32_t pol)
+{
+    constexpr uint32_t RG = LDS_BYTES / 4;
+    const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS;
+    __shared__ uint32_t lds[RG];
+    const uint32_t k = blockIdx.x;
+    const uint32_t m = min(RG, n - k * RG);
+    const uint8_t *src8 = packed + size_t(k) * RG * 4;
+    if ((reinterpret_cast<uintptr_t>(src8) & 15) == 0) {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(src8);
+        u32x4 *l4 = reinterpret_cast<u32x4 *>(lds);
+        const uint32_t m4 = m / 4;
+        for (uint32_t t0 = threadIdx.x; t0 < m4; t0 += PT * K) {
+            u32x4 v[K];
+#pragma unroll
+            for (int q = 0; q < K; ++q)
+                if (t0 + q * PT < m4)
+                    v[q] = ldp(&src[t0 + q * PT], ntl);
+#pragma unroll
+            for (int q = 0; q < K; ++q)
+                if (t0 + q * PT < m4)
+                    l4[t0 + q * PT] = v[q];
+        }
+        for (uint32_t t = (m & ~3u) + threadIdx.x; t < m; t += PT)
+            lds[t] = reinterpret_cast<const uint32_t *>(src8)[t];
+    } else {
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(src8);
+        for (uint32_t t = threadIdx.x; t < m; t += PT)
+            lds[t] = ldp(&src[t], ntl);
+    }
+    __syncthreads();
+    const uint32_t s0 = bstart[k], s1 = bstart[k + 1];
+    const uint32_t q0 = s0 >> 2, q1 = (s1 + 3) >> 2;
+    const u16x4 *up = reinterpret_cast<const u16x4 *>(upos);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(U);
+    for (uint32_t x0 = q0 + threadIdx.x; x0 < q1; x0 += PT * K) {
+        u16x4 p[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            if (x0 + q * PT < q1)
+                p[q] = ldp(&up[x0 + q * PT], ntl);
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const uint32_t x = x0 + q * PT;
+            if (x >= q1)
+                continue;
+            u32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                v[e] = p[q][e] != PAD ? lds[p[q][e]] : 0u;   // padding slots written too: whole segments
+            if (4 * x >= s0 && 4 * x + 4 <= s1) {
+                stp(&dst[x], v, nts);
+            } else {   // a quad shared with a neighbouring bucket: this bucket's slots only
+                uint32_t *d1 = reinterpret_cast<uint32_t *>(U);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (4 * x + e >= s0 && 4 * x + e < s1)
+                        d1[4 * x + e] = v[e];
+            }
+        }
+    }
+}
+
 // unpack pass 1', first phase: the chunk's runs from U into the LDS chunk image
 template <int E, int SEGB, int NT>
 __device__ __forceinline__ void load_runs(typename Elem<E>::T *lds, const uint16_t *toff, const uint32_t *tub,
@@ -471,6 +620,7 @@ __global__ __launch_bounds__(PT / CDIV) void k_unpack1(uint8_t *__restrict__ use
     __shared__ T lds[CH];
     __shared__ uint16_t toff[MAXNB / CDIV + 1];
     __shared__ uint32_t tub[MAXNB / CDIV];
+    stagger(pol);
     const uint32_t c = chunk_of(blockIdx.x, gridDim.x, pol), j0 = c * CH;
     const uint32_t m = min(CH, n - j0);
     stage_tables<NT>(off16, ub, c, nb, m, toff, tub);
@@ -509,6 +659,15 @@ void launch_pass2(dim3 gb, dim3 blk, hipStream_t stream, const uint8_t *src, con
                   const uint32_t *bstart, uint8_t *dst, uint32_t n, uint32_t pol, uint32_t k2)
 {
     constexpr int K16 = E == 4 ? 16 : 4, K8 = E <= 8 ? 8 : 4;
+    if (E == 4 && (pol & POL_VEC2)) {   // K quads (4 K slots) per lane in flight
+        if (DIR == 0)
+            hipLaunchKernelGGL((k_pack2v<2>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
+        else if (k2 >= 8)
+            hipLaunchKernelGGL((k_unpack2v<2>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
+        else
+            hipLaunchKernelGGL((k_unpack2v<1>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
+        return;
+    }
     if (DIR == 0) {
         hipLaunchKernelGGL((k_pack2<E, 4>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
     } else {

@@ -634,6 +634,10 @@ int commit(ddt_datatype *t)
                 t->opt = std::move(nodes);
                 t->opt_flags = flags;
                 optimized = true;
+                // the committed opt_desc itself, as the reference keeps it: the
+                // export and MPI_Pack's consolidation read THIS description, not one rebuilt
+                // later under tuning values that may have changed since the commit
+                t->opt_form = std::make_shared<const DescForm>(std::move(out));
             }
         }
     }
@@ -733,7 +737,8 @@ ddt_datatype *consolidate(const ddt_datatype *old, uint64_t count, int64_t thres
         return nullptr;   // already contiguous across counts / nothing to move
     if ((old->flags & F_CONTIGUOUS) && old->size == old->extent())
         return nullptr;
-    // the old type's committed opt_desc (its desc when imported: that already is one)
+    // the old type's committed opt_desc (cached at its commit; its desc when imported: that
+    // already is one)
     DescForm body;
     if (old->opt_form)
         body = *old->opt_form;

@@ -39,34 +39,42 @@ def _worker(rank, world, port, q):
             return float(t.item())
 
         wall = bench.timed_region(step, 5, world, lambda: None, reduce_max, dist.barrier)
-        # shards of different sizes and contents, like a count split 7 over 2 ranks
+        # shards of different sizes and contents, like a count split over the ranks
         S = 4000 if rank == 0 else 3000
         packed = torch.arange(S, dtype=torch.int64).to(torch.uint8) + rank
         chk = bench.gather_check(packed, S, world, rank, torch.device("cpu"), "gloo")
-        q.put((rank, calls, wall, chk))
+        pr = bench.per_rank_times(0.001 * (rank + 1), 0.002 * (rank + 1), world, torch.device("cpu"), "gloo")
+        q.put((rank, calls, wall, (chk, pr)))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as ex:  # surface failures to the parent
         q.put((rank, repr(ex), None, None))
 
 
-def test_timed_region_and_gather_check_world2_gloo():
+@pytest.mark.parametrize("world", [2, 4])
+def test_timed_region_and_gather_check_gloo(world):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = bench.free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    for rank, calls, wall, chk in res:
+    total = 4000 + 3000 * (world - 1)
+    for rank, calls, wall, extra in res:
         assert calls == list(range(5)), calls
-        # both ranks report the slow rank's time (max over ranks), >= 5 x 20 ms
+        chk, pr = extra
+        # every rank reports the slow rank's time (max over ranks), >= 5 x 20 ms
         assert wall >= 0.1
-        assert chk["ok"] and chk["gathered_bytes"] == 7000 and chk["backend"] == "gloo"
-    assert res[0][2] == res[1][2]
+        assert chk["ok"] and chk["gathered_bytes"] == total and chk["backend"] == "gloo"
+        # per-rank event times in rank order, min / max over ranks
+        assert pr["ranks"] == [[round(1.0 * (r + 1), 4), round(2.0 * (r + 1), 4)] for r in range(world)]
+        assert pr["pack"] == {"min": 1.0, "max": 1.0 * world}
+        assert pr["unpack"] == {"min": 2.0, "max": 2.0 * world}
+    assert len({r[2] for r in res}) == 1
 
 
 @pytest.mark.parametrize("cfg", ["cfg1", "cfg2", "cfg3"])

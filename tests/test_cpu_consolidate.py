@@ -149,3 +149,27 @@ def test_reset_restores_the_environment_threshold():
     env = dict(os.environ, OMPI_MCA_datatype_consolidate_threshold="1000")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+def test_committed_description_is_kept_across_tuning_changes():
+    """the committed opt_desc is the one exported and consolidated later, whatever the
+    optimizer parameters are by then (the reference keeps oldType->opt_desc; its MCA parameters
+    are read at commit, opal_datatype_optimize.c:1739-1782).  struct{double,int[3]} committed
+    with preserve_type on is UINT4 x 5; after preserve_type is turned off its export and its
+    MPI_Pack consolidation still carry UINT4, while a type committed now carries UINT1."""
+    from ompi_amd._lib import lib
+    UINT1, UINT4 = 9, 11
+    st = ("struct", [1, 3], [0, 8], [("basic", FLOAT8), ("basic", INT4)])
+    b = R.Built(st)
+    before = S.unpack_entries(b.engine().to_opal_opt_desc()[0])
+    assert before[0][1] == UINT4
+    assert lib().ddt_tune(b"opt_preserve", 0) == 0
+    try:
+        after = S.unpack_entries(b.engine().to_opal_opt_desc()[0])
+        assert after == before
+        cons = S.unpack_entries(b.engine().consolidate(300).to_opal_opt_desc()[0])
+        assert [x[1] for x in cons if x[0] & 0x100] == [UINT4]
+        fresh = S.unpack_entries(R.Built(st).engine().to_opal_opt_desc()[0])
+        assert fresh[0][1] == UINT1
+    finally:
+        lib().ddt_tune(b"opt_preserve", 1)

@@ -377,3 +377,35 @@ def test_sealed_list_in_a_loop_boundary_fusion():
     o = b.o.opt_desc()
     assert eng == o
     assert any(e[1] == 0 and e[3] == 2 for e in o)   # the reference did fuse: a loop of 2
+
+
+# OMPI_MCA_opal_datatype_optimize_preserve_type values and what mca_base_var_enum_bool_vfs
+# (mca_base_var_enum.c:77-104) makes of them: None = refused, the default (true) kept
+_MCA_BOOLS = [("0", False), ("1", True), ("2", True), (" 0", False), ("false", False), ("f", False),
+              ("no", False), ("n", False), ("disabled", False), ("true", True), ("yes", True),
+              ("enabled", True), ("t", True), ("y", True), ("off", None), ("FALSE", None), ("", False),
+              ("bogus", None)]
+
+
+def test_preserve_type_environment_is_parsed_as_an_mca_bool():
+    """the environment form of preserve_type follows mca_base_var's bool rules, so
+    'off' or 'FALSE' (refused by Open MPI) keep the default instead of turning preservation on
+    or off; the effect is read off the committed carrier of struct{double,int[3]} (UINT4 x 5
+    preserved, UINT1 x 20 not)."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from tests import recipes as R\n"
+        "from tests import opal_shapes as S\n"
+        "b = R.Built(('struct', [1, 3], [0, 8], [('basic', 16), ('basic', 6)]))\n"
+        "raw, fl = b.engine().to_opal_opt_desc()\n"
+        "print(S.unpack_entries(raw)[0][1])\n" % os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    for val, expect in _MCA_BOOLS:
+        env = dict(os.environ, OMPI_MCA_opal_datatype_optimize_preserve_type=val)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        carrier = int(r.stdout.split()[-1])
+        preserved = carrier == UINT4
+        assert preserved == (True if expect is None else expect), (val, carrier)

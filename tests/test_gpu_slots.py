@@ -37,6 +37,9 @@ def _no_bindings():
     yield
 
 
+NSLOT = 32   # launch records per direction (ddt_device.h)
+
+
 def _face(n, which):
     import bench
     return bench.face_recipes(n=n)[which]
@@ -120,35 +123,38 @@ def test_changed_buffers_fall_back_and_return(device):
 
 
 def test_more_hot_sets_than_slots(device):
-    """Twelve hot types of one direction: eight bind, the rest keep launching with arguments;
-    all move the right bytes."""
+    """More hot types of one direction than slots: NSLOT bind, the rest keep launching with
+    arguments; all move the right bytes."""
     import torch
+    from ompi_amd._lib import lib
     s = torch.cuda.Stream(device)
     msgs = [_Msg(("resized", ("vector", 64, 1 + (i % 3), 8 + i, ("basic", 16)), 0, 8 * (8 + i) * 64), 2,
-                 device, s, 40 + i) for i in range(12)]
+                 device, s, 40 + i) for i in range(NSLOT + 6)]
     for _ in range(3):
         for m in msgs:
             m.step()
     st = _slots()
-    assert st[0] <= 8 and st[1] <= 8
+    assert st[0] == NSLOT and st[1] == NSLOT, st
+    assert lib().ddt_slot_state(0, NSLOT) == -1 and lib().ddt_slot_state(0, NSLOT - 1) & 1
     for m in msgs:
         m.step()
 
 
 def test_idle_bindings_are_evicted_for_a_new_hot_set(device):
-    """Eight sets bind every pack slot and go idle; a ninth set's bind attempts age them and,
-    after kEvictIdle ticks, end the least recent binding (behind fences): the ninth set binds and
+    """NSLOT sets bind every pack slot and go idle; a further set's bind attempts age them and,
+    after kEvictIdle ticks, end the least recent binding (behind fences): the new set binds and
     launches argument-free; the evicted set falls back to arguments and stays correct."""
     import torch
     s = torch.cuda.Stream(device)
     # one 8-byte element per 64+ bytes: the unit loop (line-dense records take no slots)
     idle = [_Msg(("resized", ("vector", 16, 1, 8 + i, ("basic", 16)), 0, 8 * (8 + i) * 16), 1, device, s, 70 + i)
-            for i in range(8)]
+            for i in range(NSLOT)]
     for _ in range(3):
         for m in idle:
             m.step()
-    assert _slots()[0] == 8
-    hot = _Msg(("resized", ("vector", 16, 1, 40, ("basic", 16)), 0, 8 * 40 * 16), 1, device, s, 90)
+    assert _slots()[0] == NSLOT
+    hot = _Msg(("resized", ("vector", 16, 1, 8 + NSLOT + 3, ("basic", 16)), 0, 8 * (8 + NSLOT + 3) * 16), 1,
+               device, s, 90)
     n0 = _slots()[3]
     for _ in range(140):   # 2 calls per step: >= 256 bind attempts in the unpack and pack families
         hot.step()
@@ -388,3 +394,40 @@ def test_threads_bind_launch_and_evict_concurrently(device):
         th.join(300)
     assert not errors, errors[:3]
     assert _slots()[3] > 0
+
+
+def test_ending_binding_waits_for_a_capturing_stream(device):
+    """a binding whose end cannot record its fences (its stream is capturing) stays
+    taken and "ending" -- never rebound, never freed without fences -- and a later bind attempt
+    (after the capture) records them and frees the slot."""
+    import torch
+    from ompi_amd._lib import lib
+    s = torch.cuda.Stream(device)
+    m = _Msg(_face(32, "y"), 2, device, s, 81)
+    for _ in range(3):
+        m.step()
+    ks = [k for k in range(NSLOT) if lib().ddt_slot_state(0, k) & 1]
+    assert len(ks) == 1, [lib().ddt_slot_state(0, k) for k in range(NSLOT)]
+    k = ks[0]
+    keep = (m.user, m.out, m.packed)   # the buffers outlive the capture (torch's allocator)
+    x = torch.zeros(16, device=device)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s, capture_error_mode="relaxed"):
+        x.add_(1)
+        del m   # type, plan and convertors go while their stream captures: no fence can be recorded
+        gc.collect()
+        during = lib().ddt_slot_state(0, k)
+    assert during & 3 == 3, during          # still taken, ending: no bind may reuse it
+    assert during >> 8 >= 1                 # its streams kept for the retry
+    g.replay()
+    torch.cuda.synchronize()
+    assert lib().ddt_slot_state(0, k) & 3 == 3
+    # a new hot set's bind attempts retry the fences (the stream no longer captures)
+    m2 = _Msg(_face(32, "z"), 2, device, s, 82)
+    for _ in range(3):
+        m2.step()
+    torch.cuda.synchronize()
+    assert lib().ddt_slot_state(0, k) & 2 == 0, lib().ddt_slot_state(0, k)
+    assert float(x[0]) == 1.0
+    del keep
