@@ -285,13 +285,20 @@ def single_face_latency(dev, stream, user, origin, reps=200):
             b.record(stream)
         torch.cuda.synchronize()
         d_us = float(np.median([a.elapsed_time(b) for a, b in held])) * 1e3
-        walls = []
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            ompi_amd.pack(user.data_ptr() + origin, 1, ft, buf, fs, 0)   # synchronous MPI_Pack
-            walls.append(time.perf_counter() - t0)
-        out[name] = {"bytes": fs, "call_to_done_us": round(k_us, 2), "device_us": round(d_us, 2),
-                     "mpi_pack_call_us": round(float(np.median(walls)) * 1e6, 2)}
+        L = ompi_amd.lib()
+        mpi = {}
+        # synchronous MPI_Pack (data in place on return, pack.c.in:129-150): completed on the
+        # signal kernel's pinned host word (default, r6), and on hipStreamSynchronize beside it
+        for key, sig in (("mpi_pack_call_us", 1), ("mpi_pack_call_us_stream_sync", 0)):
+            L.ddt_tune(b"sigsync", sig)
+            walls = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                ompi_amd.pack(user.data_ptr() + origin, 1, ft, buf, fs, 0)
+                walls.append(time.perf_counter() - t0)
+            mpi[key] = round(float(np.median(walls)) * 1e6, 2)
+        L.ddt_tune(b"sigsync", 1)
+        out[name] = dict({"bytes": fs, "call_to_done_us": round(k_us, 2), "device_us": round(d_us, 2)}, **mpi)
     return out
 
 
@@ -1275,6 +1282,18 @@ def main():
             "floor_us": floor,
             "cold_step": cold,
         }
+        # build provenance: the loaded library's baked-in source identity against the tree this
+        # run is in (scripts/srcsha.py)
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "scripts"))
+            import srcsha
+            lib_id = ompi_amd.lib().ddt_build_id().decode()
+            tree_id = srcsha.source_sha(ROOT)
+            result["build"] = {"library_source_sha256": lib_id, "tree_source_sha256": tree_id,
+                               "library_built_from_this_tree": lib_id == tree_id,
+                               "library": os.path.relpath(ompi_amd.LIB_PATH, ROOT)}
+        except Exception as ex:   # reported, never fatal
+            result["build"] = {"error": f"{type(ex).__name__}: {ex}"[:200]}
         if copy and "GB_per_s" in copy:
             copy["engine_frac_of_copy"] = round(achieved / 1e9 / copy["GB_per_s"], 4)
         result["copy_ceiling"] = copy

@@ -402,6 +402,8 @@ int ddt_tune(const char *key, long value);
 /* Library self-check of host-side index arithmetic (fast division); returns 0 on success. */
 int ddt_selftest(void);
 const char *ddt_version(void);
+/* sha256 of the sources the library was linked from (scripts/srcsha.py; build provenance). */
+const char *ddt_build_id(void);
 /* Message of the last failing call on this thread (empty if none). */
 const char *ddt_last_error(void);
 

@@ -110,6 +110,7 @@ SIGNATURES = {
     "ddt_tune": (c_int, [ctypes.c_char_p, ctypes.c_long]),
     "ddt_selftest": (c_int, []),
     "ddt_version": (ctypes.c_char_p, []),
+    "ddt_build_id": (ctypes.c_char_p, []),
     "ddt_last_error": (ctypes.c_char_p, []),
 }
 

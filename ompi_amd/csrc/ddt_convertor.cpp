@@ -340,11 +340,11 @@ void retire(Plan &P, const std::shared_ptr<ItemSet> &S)   // P.mu held
 // Every stream that launched work reading a plan's device memory: the plan's destruction
 // fences its memory behind them (~Plan, ddt_pool.h).  A launch inside a capture marks the
 // plan: a graph may read its memory after the datatype is gone.
-void note_stream_locked(Plan &P, hipStream_t stream)   // P.mu held
+void note_stream_locked(Plan &P, hipStream_t stream, int cap = -1)   // P.mu held; cap: known capture state
 {
     if (std::find(P.streams.begin(), P.streams.end(), stream) == P.streams.end())
         P.streams.push_back(stream);
-    if (capturing(stream))
+    if (cap < 0 ? capturing(stream) : cap != 0)
         P.captured = true;
 }
 
@@ -534,6 +534,9 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     Item *d_items = nullptr;
     int slot_k = -1, slot_b = -1;
     uint32_t slot_gen = 0;
+    // the stream's capture state, queried before the plan lock: HIP answers under a global lock
+    // of its own, and threads sharing this plan must not queue behind it (r6 thread scaling)
+    const bool cap = capturing(stream);
     {
         std::lock_guard<std::mutex> g(P.mu);
         if (S->inline_ok && !S->retired && ++S->uses >= 2 && !S->d_items && tuning().ptr) {
@@ -550,7 +553,6 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         }
         d_items = (S->inline_ok && (!tuning().ptr || S->retired)) ? nullptr : S->d_items;
         if (d_items) {
-            const bool cap = capturing(stream);
             if (cap) {
                 // the graph keeps this pointer: never recycle it before the plan goes
                 if (S->retired && !S->pinned)
@@ -627,7 +629,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             }
             if (std::find(S->streams.begin(), S->streams.end(), stream) == S->streams.end())
                 S->streams.push_back(stream);
-            note_stream_locked(P, stream);
+            note_stream_locked(P, stream, cap ? 1 : 0);   // one capture query per call (HIP takes a global lock)
             hold.by_pointer = true;
         }
     }
@@ -1930,6 +1932,8 @@ int ddt_tune(const char *key, long value)
         tuning().sigspin_us = value < 0 ? 0 : value;
     else if (k == "s2vec")
         tuning().s2vec = value ? 1 : 0;
+    else if (k == "sskew")
+        tuning().sskew = value < 0 ? 0 : (value > (1 << 20) ? (1 << 20) : value);
     else if (k == "sstagger")
         tuning().sstagger = value < 0 ? 0 : (value > 255 ? 255 : value);
     else if (k == "sunroll")

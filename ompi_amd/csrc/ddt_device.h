@@ -129,12 +129,17 @@ constexpr uint32_t ITEM_ARG_DIMS = 4;
 
 // The launch record of an argument-free move launch (ddt_move.hip.h, ddt_move_slot_kernel):
 // NSLOT records per (direction, lists) kernel family per device, bound by the host to hot
-// descriptor sets on fixed buffers (ddt_plan.cpp: slot_bind).  A launch of record k asks for
-// (k + 1) x SLOT_LDS_UNIT bytes of dynamic LDS, which the kernel (static LDS 0) reads back from
-// its dispatch packet (round 6: one kernel per direction for any number of records; round 5 had
-// one inlined kernel per record, 8 per direction).
+// descriptor sets on fixed buffers (ddt_plan.cpp: slot_bind).  Record k is served by slot
+// kernel k / SLOT_PER_KERNEL, launched with ((k % SLOT_PER_KERNEL) + 1) x SLOT_LDS_UNIT bytes of
+// dynamic LDS, which the kernel (static LDS 0) reads back from the hardware register
+// HW_REG_LDS_ALLOC -- no memory access (r6: two kernels per direction serve 32 records; r5 had one
+// inlined kernel per record, 8 per direction; reading the dispatch packet instead costs 14 us
+// per launch, profiles/r6_ldsprobe.log).  SLOT_LDS_UNIT is gfx950's LDS allocation granule
+// (1280 bytes: LDS_SIZE counts 256-byte units in steps of 5); at most 16 x 1280 = 20 KiB, so
+// eight 256-thread workgroups still fit a CU's 160 KiB.
 constexpr uint32_t NSLOT = 32;
-constexpr uint32_t SLOT_LDS_UNIT = 256;
+constexpr uint32_t SLOT_PER_KERNEL = 16;
+constexpr uint32_t SLOT_LDS_UNIT = 1280;
 struct LaunchRec {
     uint64_t items;    // const Item * in device memory
     uint64_t ubase, pbase;

@@ -7,7 +7,6 @@
 #include <cstdlib>
 
 #include <hip/hip_runtime.h>
-#include <hsa/hsa.h>
 
 #include "ddt_device.h"
 #include "ddt_plan.h"
@@ -836,25 +835,27 @@ __global__ __launch_bounds__(THREADS) void ddt_move_kernel(const Item *__restric
 // the pointer kernel's 56) and large launches lost occupancy
 static __constant__ LaunchRec g_launch[NSLOT + 1];   // [NSLOT]: never bound, ntasks 0
 
-// The record index of an argument-free launch: its dispatch packet's group_segment_size (the
-// kernel's static LDS, 0, plus the launch's dynamic LDS of (k + 1) x SLOT_LDS_UNIT), read through
-// the dispatch pointer -- an SGPR input of the wave, not a kernel argument.  Out of range (a
-// launch that did not ask for slot LDS): NSLOT, and the kernel does nothing.  slot_probe checks
+// The record index of an argument-free launch of slot kernel HI: the LDS size of the wave's
+// workgroup from HW_REG_LDS_ALLOC (bits 12..20, 256-byte units; a scalar register read, no
+// memory), which the launch set to (k % SLOT_PER_KERNEL + 1) x SLOT_LDS_UNIT.  Out of range (a
+// launch that asked for no slot LDS, or more): NSLOT, the never-bound record.  slot_probe checks
 // the decoding on each device before any record is bound.
+constexpr int kHwRegLdsSize = ((9 - 1) << 11) | (12 << 6) | 6;   // HW_REG_LDS_ALLOC[20:12]
+
+template <uint32_t HI>
 __device__ __forceinline__ uint32_t slot_index()
 {
-    using CPacket = const __attribute__((address_space(4))) hsa_kernel_dispatch_packet_t;
-    CPacket *pk = (CPacket *) __builtin_amdgcn_dispatch_ptr();
-    const uint32_t k = pk->group_segment_size / SLOT_LDS_UNIT - 1u;
-    return k < NSLOT ? k : NSLOT;
+    const uint32_t units = uint32_t(__builtin_amdgcn_s_getreg(kHwRegLdsSize));   // 256-byte units
+    const uint32_t lo = units * 256u / SLOT_LDS_UNIT - 1u;
+    return lo < SLOT_PER_KERNEL ? HI * SLOT_PER_KERNEL + lo : NSLOT;
 }
 
-template <int DIR, bool LISTS>
+template <int DIR, bool LISTS, uint32_t HI>
 __global__ __launch_bounds__(THREADS) void ddt_move_slot_kernel()
 {
-    // no branch on k: the record table's address load issues beside the packet load, and an
-    // out-of-range launch reads the never-bound record [NSLOT] (no tasks)
-    const LaunchRec &r = g_launch[slot_index()];
+    // no branch on the index: the record table's address load issues beside the register read,
+    // and an out-of-range launch reads the never-bound record [NSLOT] (no tasks)
+    const LaunchRec &r = g_launch[slot_index<HI>()];
     // the descriptor set is read-only for the kernel's lifetime, as a kernel-argument pointer is:
     // in the constant address space its uniform loads are scalar (a plain pointer loaded from
     // memory gives flat vector loads and twice the registers)
@@ -864,20 +865,25 @@ __global__ __launch_bounds__(THREADS) void ddt_move_slot_kernel()
         move_task<DIR, LISTS>(items, r.nitems, Bases{r.ubase, r.pbase}, blockIdx.x);
 }
 
-// slot_probe: the index every launch of k reads back (out[k]), and out[NSLOT] for a launch
-// without slot LDS (must be NSLOT: no record)
+// slot_probe: the index launch k of slot kernel k / SLOT_PER_KERNEL reads back (out[k]), and
+// out[NSLOT] for a launch without slot LDS (must be NSLOT: no record)
+template <uint32_t HI>
 static __global__ __attribute__((unused)) __launch_bounds__(64) void ddt_slot_probe_kernel(uint32_t *out)
 {
     if (threadIdx.x == 0)
-        out[0] = slot_index();
+        out[0] = slot_index<HI>();
 }
 
 template <int DIR, bool LISTS>
 static void launch_slot(uint32_t k, uint32_t grid, hipStream_t stream)
 {
-    hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS>), dim3(grid), dim3(THREADS), (k + 1) * SLOT_LDS_UNIT,
-                       stream);
+    const uint32_t lds = (k % SLOT_PER_KERNEL + 1) * SLOT_LDS_UNIT;
+    if (k < SLOT_PER_KERNEL)
+        hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 0>), dim3(grid), dim3(THREADS), lds, stream);
+    else
+        hipLaunchKernelGGL((ddt_move_slot_kernel<DIR, LISTS, 1>), dim3(grid), dim3(THREADS), lds, stream);
 }
+static_assert(NSLOT == 2 * SLOT_PER_KERNEL, "launch_slot dispatches two slot kernels");
 
 // Small launches carry their descriptors in the kernel-argument segment: no device
 // buffer, no upload, no cache entry (fragment pipelines, windows, one-off messages).
@@ -990,9 +996,14 @@ static void launch_inline(const ItemBlock &blk, uint32_t ntasks, uint32_t grid, 
     }                                                                                                  \
     hipError_t slot_probe_##TAG(uint32_t *d_out, hipStream_t stream)                                   \
     {                                                                                                  \
-        for (uint32_t k = 0; k <= NSLOT; ++k)                                                          \
-            hipLaunchKernelGGL(ddt_slot_probe_kernel, dim3(1), dim3(64),                               \
-                               k < NSLOT ? (k + 1) * SLOT_LDS_UNIT : 0u, stream, d_out + k);           \
+        for (uint32_t k = 0; k < NSLOT; ++k) {                                                         \
+            const uint32_t lds = (k % SLOT_PER_KERNEL + 1) * SLOT_LDS_UNIT;                            \
+            if (k < SLOT_PER_KERNEL)                                                                   \
+                hipLaunchKernelGGL(ddt_slot_probe_kernel<0>, dim3(1), dim3(64), lds, stream, d_out + k); \
+            else                                                                                       \
+                hipLaunchKernelGGL(ddt_slot_probe_kernel<1>, dim3(1), dim3(64), lds, stream, d_out + k); \
+        }                                                                                              \
+        hipLaunchKernelGGL(ddt_slot_probe_kernel<0>, dim3(1), dim3(64), 0, stream, d_out + NSLOT);     \
         return hipGetLastError();                                                                      \
     }
 

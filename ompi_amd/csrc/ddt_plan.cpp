@@ -756,7 +756,7 @@ SortedList *sorted_build(Plan &P, hipStream_t stream)
         bool ok = false;
         try {
             ok = S->build(ed, uint32_t(ne), uint32_t(esz), span_elems, uint32_t(segb), bs,
-                          uint32_t(tuning().schunk));
+                          uint32_t(tuning().schunk), uint32_t(tuning().sskew));
         } catch (...) {
             pool_free(tmp);   // build() has drained its stream before throwing
             throw;

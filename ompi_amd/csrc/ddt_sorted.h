@@ -20,6 +20,9 @@ struct SortedList {
     uint32_t segb = 64;      // segment bytes: 64 or 128
     bool unpadded = false;   // runs packed end to end in U (segb = the lanes per run only)
     uint32_t nc = 0, nb = 0; // chunks, buckets
+    uint32_t skew = 0;       // U slots between consecutive buckets (r6: buckets of exactly RG slots
+                             // start 128 KiB apart, so one chunk's runs all fell on one DRAM
+                             // channel; `ddt_tune sskew` bytes, read at build)
     uint64_t slots = 0;      // U slots, runs padded to whole segments
     uint64_t dev_bytes = 0;  // device bytes held (tables + U)
     uint32_t *A = nullptr;       // [n] element offset (units of esz) of the j-th block in address order
@@ -30,7 +33,8 @@ struct SortedList {
     uint16_t *off16 = nullptr;   // [nc][nb] LDS offset of run (c, k): exclusive prefix over k of
                                  // the blocks of chunk c whose packed position is in bucket k
     uint32_t *ub = nullptr;      // [nc][nb] first U slot of run (c, k); U is bucket-major
-    uint32_t *bstart = nullptr;  // [nb + 1] first U slot of bucket k
+    uint32_t *bstart = nullptr;  // [nb + 1] first U slot of bucket k (k skews in); bucket k ends
+                                 // at bstart[k + 1] - skew
     uint16_t *upos = nullptr;    // [slots] position inside its bucket, 0xFFFF = padding
     void *U = nullptr;           // [slots] scratch elements
     hipEvent_t done = nullptr;   // recorded after every run (U reuse across streams)
@@ -41,7 +45,7 @@ struct SortedList {
     // hand the tables and U to `out` (the plan releases them behind its stream fences)
     void take_blocks(std::vector<void *> &out);
     bool build(const int32_t *disp, uint32_t n, uint32_t esz, uint64_t span_elems, uint32_t segb,
-               hipStream_t stream, uint32_t cdiv = 1);
+               hipStream_t stream, uint32_t cdiv = 1, uint32_t skew_bytes = 0);
     // pol: access policy bits (POL_* in ddt_sorted.hip; ddt_tune "spol")
     // unroll: elements per thread in flight in pack 1's address-ordered gather (4, 8 or 16)
     // k2: the same for unpack pass 2' (4, 8 or 16)

@@ -239,18 +239,18 @@ __global__ __launch_bounds__(BT) void k_chunk_tables(const uint32_t *__restrict_
 
 // chunk-major copy of the bucket-major run bases, and the first slot of every bucket
 __global__ __launch_bounds__(BT) void k_run_bases(const uint32_t *__restrict__ ubT, uint32_t nc, uint32_t nb,
-                                                  uint32_t total, uint32_t *__restrict__ ub,
+                                                  uint32_t total, uint32_t skew, uint32_t *__restrict__ ub,
                                                   uint32_t *__restrict__ bstart)
 {
     const size_t n = size_t(nc) * nb;
     for (size_t x = size_t(blockIdx.x) * BT + threadIdx.x; x < n; x += size_t(gridDim.x) * BT) {
         const uint32_t k = uint32_t(x / nc), c = uint32_t(x % nc);
-        ub[size_t(c) * nb + k] = ubT[x];
+        ub[size_t(c) * nb + k] = ubT[x] + k * skew;
         if (c == 0)
-            bstart[k] = ubT[x];
+            bstart[k] = ubT[x] + k * skew;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0)
-        bstart[nb] = total;
+        bstart[nb] = total + nb * skew;
 }
 
 __global__ __launch_bounds__(BT) void k_assign(const int32_t *__restrict__ disp, uint32_t n, uint32_t shift,
@@ -355,14 +355,14 @@ __global__ __launch_bounds__(PT / CDIV) void k_pack1(const uint8_t *__restrict__
 template <int E, int K>
 __global__ __launch_bounds__(PT) void k_pack2(const uint8_t *__restrict__ U, const uint16_t *__restrict__ upos,
                                               const uint32_t *__restrict__ bstart, uint8_t *__restrict__ packed,
-                                              uint32_t n, uint32_t pol)
+                                              uint32_t n, uint32_t pol, uint32_t skew)
 {
     using T = typename Elem<E>::T;
     constexpr uint32_t RG = LDS_BYTES / E;
     const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS;
     __shared__ T lds[RG];
     const uint32_t k = blockIdx.x;
-    const uint32_t s0 = bstart[k], s1 = bstart[k + 1];
+    const uint32_t s0 = bstart[k], s1 = bstart[k + 1] - skew;
     const T *src = reinterpret_cast<const T *>(U);
     
     for (uint32_t x0 = s0 + threadIdx.x; x0 < s1; x0 += PT * K) {
@@ -393,7 +393,7 @@ __global__ __launch_bounds__(PT) void k_pack2(const uint8_t *__restrict__ U, con
 template <int E, int K>
 __global__ __launch_bounds__(PT) void k_unpack2(const uint8_t *__restrict__ packed, const uint16_t *__restrict__ upos,
                                                 const uint32_t *__restrict__ bstart, uint8_t *__restrict__ U,
-                                                uint32_t n, uint32_t pol)
+                                                uint32_t n, uint32_t pol, uint32_t skew)
 {
     using T = typename Elem<E>::T;
     constexpr uint32_t RG = LDS_BYTES / E;
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(PT) void k_unpack2(const uint8_t *__restrict__ pack
                 lds[t0 + q * PT] = v[q];
     }
     __syncthreads();
-    const uint32_t s0 = bstart[k], s1 = bstart[k + 1];
+    const uint32_t s0 = bstart[k], s1 = bstart[k + 1] - skew;
     T *dst = reinterpret_cast<T *>(U);
     for (uint32_t x0 = s0 + threadIdx.x; x0 < s1; x0 += PT * K) {
         uint32_t p[K];
@@ -444,13 +444,13 @@ typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 template <int K>
 __global__ __launch_bounds__(PT) void k_pack2v(const uint8_t *__restrict__ U, const uint16_t *__restrict__ upos,
                                                const uint32_t *__restrict__ bstart, uint8_t *__restrict__ packed,
-                                               uint32_t n, uint32_t pol)
+                                               uint32_t n, uint32_t pol, uint32_t skew)
 {
     constexpr uint32_t RG = LDS_BYTES / 4;
     const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS, noconf = pol & POL_NOCONF;
     __shared__ uint32_t lds[RG];
     const uint32_t k = blockIdx.x;
-    const uint32_t s0 = bstart[k], s1 = bstart[k + 1];
+    const uint32_t s0 = bstart[k], s1 = bstart[k + 1] - skew;
     const u32x4 *src = reinterpret_cast<const u32x4 *>(U);
     const u16x4 *up = reinterpret_cast<const u16x4 *>(upos);
     const uint32_t q0 = s0 >> 2, q1 = (s1 + 3) >> 2;
@@ -498,7 +498,7 @@ __global__ __launch_bounds__(PT) void k_pack2v(const uint8_t *__restrict__ U, co
 template <int K>
 __global__ __launch_bounds__(PT) void k_unpack2v(const uint8_t *__restrict__ packed, const uint16_t *__restrict__ upos,
                                                  const uint32_t *__restrict__ bstart, uint8_t *__restrict__ U,
-                                                 uint32_t n, uint32_t pol)
+                                                 uint32_t n, uint32_t pol, uint32_t skew)
 {
     constexpr uint32_t RG = LDS_BYTES / 4;
     const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS;
@@ -529,7 +529,7 @@ __global__ __launch_bounds__(PT) void k_unpack2v(const uint8_t *__restrict__ pac
             lds[t] = ldp(&src[t], ntl);
     }
     __syncthreads();
-    const uint32_t s0 = bstart[k], s1 = bstart[k + 1];
+    const uint32_t s0 = bstart[k], s1 = bstart[k + 1] - skew;
     const uint32_t q0 = s0 >> 2, q1 = (s1 + 3) >> 2;
     const u16x4 *up = reinterpret_cast<const u16x4 *>(upos);
     u32x4 *dst = reinterpret_cast<u32x4 *>(U);
@@ -656,24 +656,24 @@ __global__ __launch_bounds__(PT / CDIV) void k_unpack1(uint8_t *__restrict__ use
 // pack 575 -> 587 us, so only the unpack side takes the knob.
 template <int E, int DIR>
 void launch_pass2(dim3 gb, dim3 blk, hipStream_t stream, const uint8_t *src, const uint16_t *upos,
-                  const uint32_t *bstart, uint8_t *dst, uint32_t n, uint32_t pol, uint32_t k2)
+                  const uint32_t *bstart, uint8_t *dst, uint32_t n, uint32_t pol, uint32_t k2, uint32_t skew)
 {
     constexpr int K16 = E == 4 ? 16 : 4, K8 = E <= 8 ? 8 : 4;
     if (E == 4 && (pol & POL_VEC2)) {   // K quads (4 K slots) per lane in flight
         if (DIR == 0)
-            hipLaunchKernelGGL((k_pack2v<2>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
+            hipLaunchKernelGGL((k_pack2v<2>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol, skew);
         else if (k2 >= 8)
-            hipLaunchKernelGGL((k_unpack2v<2>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
+            hipLaunchKernelGGL((k_unpack2v<2>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol, skew);
         else
-            hipLaunchKernelGGL((k_unpack2v<1>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
+            hipLaunchKernelGGL((k_unpack2v<1>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol, skew);
         return;
     }
     if (DIR == 0) {
-        hipLaunchKernelGGL((k_pack2<E, 4>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
+        hipLaunchKernelGGL((k_pack2<E, 4>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol, skew);
     } else {
-        if (k2 >= 16) hipLaunchKernelGGL((k_unpack2<E, K16>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
-        else if (k2 >= 8) hipLaunchKernelGGL((k_unpack2<E, K8>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
-        else hipLaunchKernelGGL((k_unpack2<E, 4>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol);
+        if (k2 >= 16) hipLaunchKernelGGL((k_unpack2<E, K16>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol, skew);
+        else if (k2 >= 8) hipLaunchKernelGGL((k_unpack2<E, K8>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol, skew);
+        else hipLaunchKernelGGL((k_unpack2<E, 4>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol, skew);
     }
 }
 
@@ -721,7 +721,7 @@ SortedList::~SortedList()
 // list's minimum displacement, every value a multiple of esz).  Returns false (and leaves
 // nothing allocated) when the displacements repeat.
 bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t span_elems, uint32_t segb_,
-                       hipStream_t stream, uint32_t cdiv_)
+                       hipStream_t stream, uint32_t cdiv_, uint32_t skew_bytes)
 {
     n = n_;
     esz = esz_;
@@ -807,8 +807,13 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
         uint32_t total = 0;
         HK(hipMemcpyAsync(&total, ubT + runs, 4, hipMemcpyDeviceToHost, stream));
         HK(hipStreamSynchronize(stream));
-        slots = total;
-        hipLaunchKernelGGL(k_run_bases, dim3(grid_for(runs, BT)), dim3(BT), 0, stream, ubT, nc, nb, total, ub,
+        // bucket skew: whole 16-byte quads of slots (the pass-2 quads stay aligned), and the
+        // 32-bit slot indices must still hold every slot
+        skew = (skew_bytes / esz + 3u) & ~3u;
+        if (uint64_t(total) + uint64_t(nb) * skew >= (1ull << 32))
+            skew = 0;
+        slots = uint64_t(total) + uint64_t(nb) * skew;
+        hipLaunchKernelGGL(k_run_bases, dim3(grid_for(runs, BT)), dim3(BT), 0, stream, ubT, nc, nb, total, skew, ub,
                            bstart);
         upos = dalloc<uint16_t>(slots, bytes);
         U = dalloc<uint8_t>(size_t(slots) * esz, bytes);
@@ -860,9 +865,9 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol
 #define DDT_SORTED_LAUNCH_K(E, SB, K)                                                                           \
     if (dir == 0) {                                                                                             \
         if (cdiv == 2) { DDT_SORTED_PASS1(E, SB, K, 2) } else { DDT_SORTED_PASS1(E, SB, K, 1) }                 \
-        launch_pass2<E, 0>(gb, blk, stream, u8, upos, bstart, packed, n, pol, k2);                             \
+        launch_pass2<E, 0>(gb, blk, stream, u8, upos, bstart, packed, n, pol, k2, skew);                             \
     } else {                                                                                                    \
-        launch_pass2<E, 1>(gb, blk, stream, packed, upos, bstart, u8, n, pol, k2);                             \
+        launch_pass2<E, 1>(gb, blk, stream, packed, upos, bstart, u8, n, pol, k2, skew);                             \
         if (cdiv == 2) { DDT_SORTED_PASS1(E, SB, K, 2) } else { DDT_SORTED_PASS1(E, SB, K, 1) }                 \
     }
 // K * E <= 64 bytes of elements per thread in flight: wider elements at K = 16 (or 16-byte

@@ -11,11 +11,14 @@
  * device microseconds per operation on its stream (one event pair around its loop), and the
  * aggregate host calls per second = all calls / the slowest thread's loop time.
  *
- *   ./scripts/bridgethreads [iters] [own|shared] [sync]
+ *   ./scripts/bridgethreads [iters] [own|shared] [sync|async] [face|tiny]
  *     own     each thread its own opal_datatype_t (own import, plan, descriptor sets; default)
  *     shared  one datatype for all threads (one plan: the threads share its descriptor sets)
  *     sync    no ACCELERATOR_ASYNC: every call returns with the data in place (MPI_Pack's
  *             contract), so host time per call is the whole synchronous operation
+ *     tiny    16 doubles at a 2 KiB stride (128 packed bytes) instead of the 512 KiB y face: the
+ *             device time per call is the launch alone, so host scaling is not hidden behind the
+ *             device's own throughput
  * Not part of the library.
  */
 #include <hip/hip_runtime_api.h>
@@ -45,22 +48,24 @@ typedef struct {
     opal_datatype_t dt;
 } face_type;
 
-static void make_face(face_type *f)
+static size_t g_bytes = FACE_BYTES;   /* packed bytes per call */
+
+static void make_face(face_type *f, int tiny)
 {
     memset(f, 0, sizeof(*f));
     f->desc[0].elem.common.flags = OPAL_DATATYPE_FLAG_DATA | OPAL_DATATYPE_FLAG_CONTIGUOUS;
     f->desc[0].elem.common.type = 16;   /* OPAL_DATATYPE_FLOAT8 */
-    f->desc[0].elem.count = N;
-    f->desc[0].elem.blocklen = N;
-    f->desc[0].elem.extent = (ptrdiff_t) N * N * 8;
+    f->desc[0].elem.count = tiny ? 16 : N;
+    f->desc[0].elem.blocklen = tiny ? 1 : N;
+    f->desc[0].elem.extent = tiny ? (ptrdiff_t) N * 8 : (ptrdiff_t) N * N * 8;
     f->desc[1].end_loop.common.type = OPAL_DATATYPE_END_LOOP;
-    f->desc[1].end_loop.size = FACE_BYTES;
+    f->desc[1].end_loop.size = g_bytes;
     opal_datatype_t *dt = &f->dt;
     dt->super.obj_reference_count = 1;
     dt->flags = OPAL_DATATYPE_FLAG_COMMITTED | OPAL_DATATYPE_FLAG_DATA;
-    dt->size = FACE_BYTES;
+    dt->size = g_bytes;
     dt->ub = FIELD_BYTES;
-    dt->true_ub = (ptrdiff_t) (N - 1) * N * N * 8 + N * 8;
+    dt->true_ub = tiny ? (ptrdiff_t) 15 * N * 8 + 8 : (ptrdiff_t) (N - 1) * N * N * 8 + N * 8;
     dt->desc.length = dt->opt_desc.length = 2;
     dt->desc.used = dt->opt_desc.used = 1;
     dt->desc.desc = dt->opt_desc.desc = f->desc;
@@ -106,10 +111,10 @@ static int run_calls(worker *w, int n)
             prepare(&c, w->dt, w->grid, dir == 0, &w->sobj, w->async);
             if (opal_hip_bridge_attach(&c) != OPAL_SUCCESS)
                 return 1;
-            struct iovec iov = {w->packed, FACE_BYTES};
+            struct iovec iov = {w->packed, g_bytes};
             uint32_t cnt = 1;
             size_t md = 0;
-            if (c.fAdvance(&c, &iov, &cnt, &md) != 1 || md != FACE_BYTES)
+            if (c.fAdvance(&c, &iov, &cnt, &md) != 1 || md != g_bytes)
                 return 2;
         }
     }
@@ -140,11 +145,14 @@ int main(int argc, char **argv)
     const int iters = argc > 1 ? atoi(argv[1]) : 2000;
     const int shared = argc > 2 && !strcmp(argv[2], "shared");
     const int async = !(argc > 3 && !strcmp(argv[3], "sync"));
+    const int tiny = argc > 4 && !strcmp(argv[4], "tiny");
+    if (tiny)
+        g_bytes = 128;
     if (hipSetDevice(0) != hipSuccess)
         return 2;
     static face_type types[MAXT];
     for (int t = 0; t < MAXT; ++t)
-        make_face(&types[t]);
+        make_face(&types[t], tiny);
     static worker W[MAXT];
     for (int t = 0; t < MAXT; ++t) {
         worker *w = &W[t];
@@ -198,12 +206,12 @@ int main(int argc, char **argv)
             base_rate = rate;
         int64_t si[4] = {0, 0, 0, 0};
         (void) ddt_slot_info(si);
-        printf("{\"what\": \"bridge y face pack+unpack, %s, %s\", \"threads\": %d, \"bytes\": %zu, "
+        printf("{\"what\": \"bridge %s pack+unpack, %s, %s\", \"threads\": %d, \"bytes\": %zu, "
                "\"calls_per_thread\": %d, \"host_us_per_call\": {\"mean\": %.3f, \"max\": %.3f}, "
                "\"device_us_per_op\": {\"mean\": %.3f, \"max\": %.3f}, \"aggregate_calls_per_s\": %.0f, "
                "\"speedup_vs_1\": %.3f, \"slots\": [%lld, %lld, %lld, %lld]}\n",
-               shared ? "one shared datatype" : "a datatype per thread", async ? "ACCELERATOR_ASYNC" : "synchronous",
-               T, FACE_BYTES, 2 * iters, sumh / T, maxh, sumd / T, maxd, rate, rate / base_rate,
+               tiny ? "16 doubles at 2 KiB" : "y face", shared ? "one shared datatype" : "a datatype per thread",
+               async ? "ACCELERATOR_ASYNC" : "synchronous", T, g_bytes, 2 * iters, sumh / T, maxh, sumd / T, maxd, rate, rate / base_rate,
                (long long) si[0], (long long) si[1], (long long) si[2], (long long) si[3]);
         fflush(stdout);
     }

@@ -5,6 +5,9 @@
 //   empty   an empty kernel without arguments (what an engine slot launch costs HIP)
 //   args    an empty kernel with 36 bytes of arguments (what a launch with arguments costs)
 //   copy    hipMemcpyAsync of 512 KiB device to device (the bytes of one y face)
+//   mix     the HIP calls one asynchronous engine call makes around its argument-free launch:
+//           hipGetDevice x2, hipPointerGetAttributes x2 (user buffer, iovec), hipStreamIsCapturing,
+//           then the empty kernel without arguments
 // Not part of the library.
 #include <hip/hip_runtime.h>
 
@@ -46,8 +49,19 @@ static void calls(Worker *w, int n)
             hipLaunchKernelGGL(k_empty, dim3(32), dim3(256), 0, w->s);
         else if (w->kind == 1)
             hipLaunchKernelGGL(k_args, dim3(32), dim3(256), 0, w->s, (const void *) w->a, w->b, 1ull, 2ull, 3u);
-        else
+        else if (w->kind == 2)
             (void) hipMemcpyAsync(w->b, w->a, 512 << 10, hipMemcpyDeviceToDevice, w->s);
+        else {
+            int d = 0;
+            hipPointerAttribute_t pa;
+            hipStreamCaptureStatus cs;
+            (void) hipGetDevice(&d);
+            (void) hipPointerGetAttributes(&pa, w->a);
+            (void) hipPointerGetAttributes(&pa, w->b);
+            (void) hipGetDevice(&d);
+            (void) hipStreamIsCapturing(w->s, &cs);
+            hipLaunchKernelGGL(k_empty, dim3(32), dim3(256), 0, w->s);
+        }
     }
 }
 
@@ -78,8 +92,9 @@ int main(int argc, char **argv)
             || hipEventCreate(&W[t].e1) != hipSuccess)
             return 2;
     }
-    const char *names[3] = {"empty kernel, no arguments", "empty kernel, 36 B of arguments", "hipMemcpyAsync 512 KiB D2D"};
-    for (int kind = 0; kind < 3; ++kind) {
+    const char *names[4] = {"empty kernel, no arguments", "empty kernel, 36 B of arguments", "hipMemcpyAsync 512 KiB D2D",
+                            "the engine's HIP calls around an argument-free launch"};
+    for (int kind = 0; kind < 4; ++kind) {
         double base = 0;
         for (int T : {1, 2, 4, 8}) {
             pthread_barrier_t bar;

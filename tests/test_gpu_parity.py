@@ -974,19 +974,21 @@ def test_sorted_list_engine_unpadded(device, sorted_from, esz, count, density, s
         L.ddt_tune(b"spol", 0)
 
 
+@pytest.mark.parametrize("skew", [0, 1088])
 @pytest.mark.parametrize("stagger", [0, 3])
 @pytest.mark.parametrize("seg", [1, 64])
 @pytest.mark.parametrize("schunk", [1, 2])
 @pytest.mark.parametrize("count,density", [(1, 4), (2, 4), (1, 64), (3, 2)])
-def test_sorted_list_engine_quads(device, sorted_from, count, density, schunk, seg, stagger):
+def test_sorted_list_engine_quads(device, sorted_from, count, density, schunk, seg, stagger, skew):
     """Pass 2 / 2' of 4-byte elements four U slots per lane (ddt_tune s2vec 1, round 6): quads
     shared by two buckets read whole and written slot by slot, the packed side as 16-byte
     words when aligned (instance 2 of an odd-sized message is not: the word path), padded
-    (sseg 64: padding slots) and unpadded U; with the pass-1 stagger on or off."""
+    (sseg 64: padding slots) and unpadded U; with the pass-1 stagger on or off, and with the
+    buckets skewed apart in U (sskew: gaps between buckets that no pass may read or write)."""
     import ompi_amd
     L = ompi_amd.lib()
     sorted_from(1)
-    for k, v in ((b"s2vec", 1), (b"sstagger", stagger), (b"schunk", schunk), (b"sseg", seg)):
+    for k, v in ((b"s2vec", 1), (b"sstagger", stagger), (b"schunk", schunk), (b"sseg", seg), (b"sskew", skew)):
         L.ddt_tune(k, v)
     try:
         rng = np.random.default_rng(9100 + count * 10 + density + 3 * schunk + seg)
@@ -997,8 +999,7 @@ def test_sorted_list_engine_quads(device, sorted_from, count, density, schunk, s
         _roundtrip(b, count, device, 17 + density)
         assert b.engine().engine_info()["sorted"] == 1
     finally:
-        for k, v in ((b"s2vec", 0), (b"sstagger", 0), (b"schunk", 1), (b"sseg", 1)):
-            L.ddt_tune(k, v)
+        L.ddt_tune(b"reset", 0)
 
 
 @pytest.mark.parametrize("name", ["contig16", "adv_mixed_promote", "one_contig_instance"])

@@ -330,9 +330,10 @@ def test_binding_during_foreign_capture(device, mode):
 
 
 def test_a_set_that_moves_to_other_buffers_rebinds(device):
-    """Bound on buffers A, then used on buffers B: the second call on B binds B beside A (two
-    bindings per set, a double-buffered exchange); moving on to C gives up the less recent one
-    (A, behind fences): two slots per direction stay in use, and every call moves the right bytes."""
+    """Bound on buffers A, then used on buffers B: the second call on B binds B beside A (a
+    double-buffered exchange); C binds a third binding (up to 8 per set, r6: threads sharing a
+    type bring their own buffers); with all 8 in use a ninth pair of buffers launches with
+    arguments, and every call moves the right bytes."""
     import torch
     s = torch.cuda.Stream(device)
     m = _Msg(_face(32, "z"), 2, device, s, 91)
@@ -348,9 +349,20 @@ def test_a_set_that_moves_to_other_buffers_rebinds(device):
     st = _slots()
     assert st[3] == n0 + 4 and st[0] == 2 and st[1] == 2, st
     m.step(packed=c)
-    m.step(packed=c)     # binds C in place of the less recent binding
+    m.step(packed=c)     # binds C beside A and B
     st2 = _slots()
-    assert st2[3] == st[3] + 2 and st2[0] == 2 and st2[1] == 2, st2
+    assert st2[3] == st[3] + 2 and st2[0] == 3 and st2[1] == 3, st2
+    more = [torch.zeros_like(m.packed) for _ in range(6)]
+    for p in more:       # D..I: five more bind (8 in all), the sixth finds every binding in use
+        m.step(packed=p)
+        m.step(packed=p)
+    st3 = _slots()
+    assert st3[0] == 8 and st3[1] == 8, st3
+    n1 = st3[3]
+    m.step(packed=more[-1])   # the ninth pair: no binding was free, launched with arguments
+    assert _slots()[3] == n1
+    m.step()                  # A is still bound
+    assert _slots()[3] == n1 + 2
 
 
 def test_double_buffered_exchange_alternates_two_bindings(device):
