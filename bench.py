@@ -377,7 +377,7 @@ def back_to_back(dev, fields, K=200, faces=("x", "y", "z"), with_copy=True):
         pk = torch.empty(S, dtype=torch.uint8, device=dev)
         cv = ompi_amd.Convertor()
         if k != "h":
-            kind, es, ls, ss, base, lw = face_floor_part(k, fields, grid=grid)
+            kind, es, ls, ss, base, lw = face_floor_part(k, fields)
             part = Part(kind, es, ls[0], ls[1], ls[2], lw, ss[0], ss[1], ss[2], base, 0)
 
         def engine(d):

@@ -20,13 +20,20 @@
  * bridge keeps no per-convertor side table that could outlive an opal_convertor_t.
  */
 #include <pthread.h>
+#include <sched.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "ddt_hip.h"
 #include "opal_hip_bridge.h"
 
-/* ------------------------------------------------------------------ import cache */
+/* ------------------------------------------------------------------ import cache
+ * Every fAdvance / fPosition / attach looks its datatype up here, from any thread.  Round 6
+ * (scripts/bridgethreads.c, profiles/r6_threads.jsonl): one process-wide pthread mutex taken
+ * twice per lookup convoyed under MPI_THREAD_MULTIPLE (4 threads: 5.4 us per call against 2.8
+ * through the engine's own ABI), so each bucket has its own short spin lock -- threads moving
+ * different datatypes never meet, and the critical sections are a few loads long -- and the
+ * counters are atomics. */
 typedef struct bridge_entry {
     const opal_datatype_t *key;
     const dt_elem_desc_t *desc;   /* fingerprint: the description the import was made from */
@@ -38,34 +45,62 @@ typedef struct bridge_entry {
      * stale-address eviction while calls still use it is freed by the last of them */
     size_t inflight;
     int unlinked;
+    unsigned bucket;
     struct bridge_entry *next;
 } bridge_entry;
 
 #define BRIDGE_BUCKETS 256
-static bridge_entry *g_buckets[BRIDGE_BUCKETS];
-static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
-static size_t g_entries, g_imports, g_hits, g_stale;
+typedef struct {
+    int lock;   /* 0 free, 1 held: __atomic test-and-set */
+    bridge_entry *head;
+} bridge_bucket;
+static bridge_bucket g_buckets[BRIDGE_BUCKETS];
+static size_t g_entries, g_imports, g_hits, g_stale;   /* __atomic counters */
+/* bumped whenever an entry is unlinked: a thread's pinned entries (thread_state below) are
+ * valid while it has not moved */
+static unsigned long g_gen;
 
-static size_t bucket_of(const void *p)
+static void bucket_lock(bridge_bucket *b)
+{
+    for (unsigned spins = 0; __atomic_exchange_n(&b->lock, 1, __ATOMIC_ACQUIRE); ++spins) {
+        while (__atomic_load_n(&b->lock, __ATOMIC_RELAXED)) {
+            if (++spins > 256)
+                sched_yield();   /* oversubscribed: let the holder run */
+            else
+                __builtin_ia32_pause();
+        }
+    }
+}
+
+static void bucket_unlock(bridge_bucket *b) { __atomic_store_n(&b->lock, 0, __ATOMIC_RELEASE); }
+
+static void count(size_t *c, long d) { __atomic_fetch_add(c, (size_t) d, __ATOMIC_RELAXED); }
+
+static unsigned bucket_of(const void *p)
 {
     uintptr_t x = (uintptr_t) p;
     x ^= x >> 17;
     x *= 0x9E3779B97F4A7C15ull;
-    return (size_t) (x >> 56) % BRIDGE_BUCKETS;
+    return (unsigned) ((x >> 56) % BRIDGE_BUCKETS);
 }
 
-/* FNV-1a over the first and last (up to) 8 entries: catches a different description that
- * happens to sit at a recycled address without an O(entries) hash per call. */
+/* A 64-bit mix over the first and last (up to) 8 entries, 8 bytes at a time: catches a
+ * different description that happens to sit at a recycled address without an O(entries) hash
+ * per call. */
 static uint64_t desc_sig(const dt_elem_desc_t *d, size_t used)
 {
-    uint64_t h = 1469598103934665603ull ^ used;
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ used;
     const size_t head = used < 8 ? used : 8;
     const size_t tail0 = used > head + 8 ? used - 8 : head;
     for (size_t r = 0; r < 2; ++r) {
         const size_t i0 = r ? tail0 : 0, i1 = r ? used : head;
         const unsigned char *b = (const unsigned char *) (d + i0);
-        for (size_t k = 0; k < 32 * (i1 - i0); ++k)
-            h = (h ^ b[k]) * 1099511628211ull;
+        for (size_t k = 0; k < 32 * (i1 - i0); k += 8) {
+            uint64_t w;
+            memcpy(&w, b + k, 8);
+            h = (h ^ w) * 0xBF58476D1CE4E5B9ull;
+            h ^= h >> 31;
+        }
     }
     return h;
 }
@@ -77,33 +112,43 @@ static int same_fingerprint(const bridge_entry *e, const opal_datatype_t *dt, co
            && e->ub == dt->ub && e->true_lb == dt->true_lb && e->true_ub == dt->true_ub && e->sig == sig;
 }
 
-/* Called with g_mu held on an entry already taken off its bucket list. */
-static void retire_locked(bridge_entry *e)
+/* Called with the entry's bucket locked, on an entry already taken off the bucket list.  Returns
+ * the entry when the caller must free it after unlocking (no call uses it), else NULL. */
+static bridge_entry *retire_locked(bridge_entry *e)
 {
-    --g_entries;
+    __atomic_fetch_add(&g_gen, 1, __ATOMIC_SEQ_CST);   /* before inflight is read: see thread_state */
+    count(&g_entries, -1);
     if (e->inflight) {   /* a call on another thread still moves data with it */
         e->unlinked = 1;
-        return;
+        return NULL;
     }
+    return e;
+}
+
+static void free_entry(bridge_entry *e)
+{
+    if (!e)
+        return;
     ddt_type_destroy(&e->type);
     free(e);
 }
 
 static void bridge_release(bridge_entry *e)
 {
-    pthread_mutex_lock(&g_mu);
-    if (--e->inflight == 0 && e->unlinked) {
-        ddt_type_destroy(&e->type);
-        free(e);
-    }
-    pthread_mutex_unlock(&g_mu);
+    bridge_bucket *b = &g_buckets[e->bucket];
+    bucket_lock(b);
+    const int last = --e->inflight == 0 && e->unlinked;
+    bucket_unlock(b);
+    if (last)
+        free_entry(e);
 }
 
-/* The entry of (dt, ud) in its bucket, with g_mu held; a different description found at the
- * same address is retired on the way (the old datatype died unseen). */
-static bridge_entry *lookup_locked(const opal_datatype_t *dt, const dt_type_desc_t *ud, uint64_t sig)
+/* The entry of (dt, ud) in its bucket, bucket locked; a different description found at the same
+ * address is unlinked on the way (the old datatype died unseen) and handed back in *dead. */
+static bridge_entry *lookup_locked(bridge_bucket *b, const opal_datatype_t *dt, const dt_type_desc_t *ud,
+                                   uint64_t sig, bridge_entry **dead)
 {
-    for (bridge_entry **pp = &g_buckets[bucket_of(dt)]; *pp;) {
+    for (bridge_entry **pp = &b->head; *pp;) {
         if ((*pp)->key != dt) {
             pp = &(*pp)->next;
             continue;
@@ -112,17 +157,30 @@ static bridge_entry *lookup_locked(const opal_datatype_t *dt, const dt_type_desc
             return *pp;
         bridge_entry *old = *pp;
         *pp = old->next;
-        retire_locked(old);
-        ++g_stale;
+        count(&g_stale, 1);
+        bridge_entry *f = retire_locked(old);
+        if (f) {   /* at most a few stale entries: chain them for the caller to free */
+            f->next = *dead;
+            *dead = f;
+        }
     }
     return NULL;
+}
+
+static void free_chain(bridge_entry *d)
+{
+    while (d) {
+        bridge_entry *n = d->next;
+        free_entry(d);
+        d = n;
+    }
 }
 
 /* The cache entry of (dt, ud), imported on first use.  `hold`: keep it for the caller until
  * bridge_release (a destruct or an eviction on another thread in between only unlinks it).
  * The import itself -- seconds for a description of tens of millions of entries -- runs
- * outside the cache lock, so other threads' calls on other datatypes never wait for it; two
- * threads importing the same datatype at once keep the first entry and drop the second. */
+ * outside the bucket lock, so other threads' calls never wait for it; two threads importing
+ * the same datatype at once keep the first entry and drop the second. */
 static bridge_entry *bridge_entry_of(const opal_datatype_t *dt, const dt_type_desc_t *ud, int hold, int *err)
 {
     *err = OPAL_SUCCESS;
@@ -131,16 +189,22 @@ static bridge_entry *bridge_entry_of(const opal_datatype_t *dt, const dt_type_de
         return NULL;
     }
     const uint64_t sig = desc_sig(ud->desc, ud->used);
-    pthread_mutex_lock(&g_mu);
-    bridge_entry *e = lookup_locked(dt, ud, sig);
+    const unsigned bi = bucket_of(dt);
+    bridge_bucket *bk = &g_buckets[bi];
+    bridge_entry *dead = NULL;
+    bucket_lock(bk);
+    bridge_entry *e = lookup_locked(bk, dt, ud, sig, &dead);
     if (e) {
-        ++g_hits;
         if (hold)
             ++e->inflight;
-        pthread_mutex_unlock(&g_mu);
+        bucket_unlock(bk);
+        count(&g_hits, 1);
+        free_chain(dead);
         return e;
     }
-    pthread_mutex_unlock(&g_mu);
+    bucket_unlock(bk);
+    free_chain(dead);
+    dead = NULL;
 
     ddt_datatype_t *t = NULL;
     const int rc = ddt_type_from_opal_desc(ud->desc, ud->used, dt->size, dt->lb, dt->ub, dt->true_lb,
@@ -168,33 +232,31 @@ static bridge_entry *bridge_entry_of(const opal_datatype_t *dt, const dt_type_de
     n->true_ub = dt->true_ub;
     n->sig = sig;
     n->type = t;
+    n->bucket = bi;
 
-    pthread_mutex_lock(&g_mu);
-    e = lookup_locked(dt, ud, sig);
+    bucket_lock(bk);
+    e = lookup_locked(bk, dt, ud, sig, &dead);
     if (e) {   /* another thread imported it meanwhile */
-        ++g_hits;
         if (hold)
             ++e->inflight;
-        pthread_mutex_unlock(&g_mu);
+        bucket_unlock(bk);
+        count(&g_hits, 1);
+        free_chain(dead);
         ddt_type_destroy(&n->type);
         free(n);
         return e;
     }
-    const size_t b = bucket_of(dt);
     n->inflight = hold ? 1 : 0;
-    n->next = g_buckets[b];
-    g_buckets[b] = n;
-    ++g_entries;
-    ++g_imports;
-    pthread_mutex_unlock(&g_mu);
+    n->next = bk->head;
+    bk->head = n;
+    bucket_unlock(bk);
+    count(&g_entries, 1);
+    count(&g_imports, 1);
+    free_chain(dead);
     return n;
 }
 
-static bridge_entry *bridge_type_of(const opal_convertor_t *conv, int *err)
-{
-    const opal_datatype_t *dt = conv->pDesc;
-    return bridge_entry_of(dt, conv->use_desc ? conv->use_desc : (dt ? &dt->opt_desc : NULL), 1, err);
-}
+static void unpin_current_thread(void);
 
 int opal_hip_bridge_datatype_commit(const opal_datatype_t *dt)
 {
@@ -208,40 +270,55 @@ int opal_hip_bridge_datatype_commit(const opal_datatype_t *dt)
 
 void opal_hip_bridge_datatype_destruct(const opal_datatype_t *dt)
 {
-    pthread_mutex_lock(&g_mu);
-    for (bridge_entry **pp = &g_buckets[bucket_of(dt)]; *pp;) {
+    bridge_bucket *bk = &g_buckets[bucket_of(dt)];
+    bridge_entry *dead = NULL;
+    bucket_lock(bk);
+    for (bridge_entry **pp = &bk->head; *pp;) {
         if ((*pp)->key == dt) {
             bridge_entry *old = *pp;
             *pp = old->next;
-            retire_locked(old);
+            bridge_entry *f = retire_locked(old);
+            if (f) {
+                f->next = dead;
+                dead = f;
+            }
         } else {
             pp = &(*pp)->next;
         }
     }
-    pthread_mutex_unlock(&g_mu);
+    bucket_unlock(bk);
+    free_chain(dead);
 }
 
 void opal_hip_bridge_finalize(void)
 {
-    pthread_mutex_lock(&g_mu);
+    unpin_current_thread();   /* other threads' pins go at their next call or exit */
     for (size_t b = 0; b < BRIDGE_BUCKETS; ++b) {
-        while (g_buckets[b]) {
-            bridge_entry *old = g_buckets[b];
-            g_buckets[b] = old->next;
-            retire_locked(old);
+        bridge_bucket *bk = &g_buckets[b];
+        bridge_entry *dead = NULL;
+        bucket_lock(bk);
+        while (bk->head) {
+            bridge_entry *old = bk->head;
+            bk->head = old->next;
+            bridge_entry *f = retire_locked(old);
+            if (f) {
+                f->next = dead;
+                dead = f;
+            }
         }
+        bucket_unlock(bk);
+        free_chain(dead);
     }
-    pthread_mutex_unlock(&g_mu);
 }
+
+static size_t pin_hits_total(void);
 
 void opal_hip_bridge_stats(size_t *out4)
 {
-    pthread_mutex_lock(&g_mu);
-    out4[0] = g_entries;
-    out4[1] = g_imports;
-    out4[2] = g_hits;
-    out4[3] = g_stale;
-    pthread_mutex_unlock(&g_mu);
+    out4[0] = __atomic_load_n(&g_entries, __ATOMIC_RELAXED);
+    out4[1] = __atomic_load_n(&g_imports, __ATOMIC_RELAXED);
+    out4[2] = __atomic_load_n(&g_hits, __ATOMIC_RELAXED) + pin_hits_total();
+    out4[3] = __atomic_load_n(&g_stale, __ATOMIC_RELAXED);
 }
 
 void opal_hip_bridge_layout(size_t *out8)
@@ -256,25 +333,170 @@ void opal_hip_bridge_layout(size_t *out8)
     out8[7] = sizeof(dt_elem_desc_t);
 }
 
-/* ------------------------------------------------------------------ per-thread engine convertor */
+/* ------------------------------------------------------------------ per-thread state
+ * Engine convertors are per thread (the reference's contract is one thread per convertor,
+ * opal_convertor.h:125; a thread serves many opal convertors in turn).  Each thread also pins
+ * the cache entries of the last two datatypes it moved (one reference each, taken by a normal
+ * lookup), so its next calls on them touch no shared cache line at all; a pin is dropped when
+ * the cache generation moved (an entry was unlinked somewhere: a destruct or a stale address),
+ * when the slot is reused, and at thread exit.  A destruct of a pinned datatype therefore frees
+ * its engine import at the pinning thread's next bridge call or exit. */
+#define PIN_SLOTS 2
+typedef struct {
+    bridge_entry *e;
+    const opal_datatype_t *key;
+    const dt_type_desc_t *ud;
+    uint64_t sig;
+    unsigned long gen;
+    unsigned long used;   /* LRU tick */
+} pin_slot;
+
+typedef struct thread_state {
+    ddt_convertor_t *h;
+    pin_slot pin[PIN_SLOTS];
+    unsigned long tick;
+    size_t pin_hits;   /* lookups served by a pin: written by the owner, summed by the stats */
+    struct thread_state *next, *prev;
+} thread_state;
+
 static pthread_key_t g_key;
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+/* live thread states (for the stats), and the pin hits of threads that exited */
+static pthread_mutex_t g_ts_mu = PTHREAD_MUTEX_INITIALIZER;
+static thread_state *g_ts_head;
+static size_t g_exited_pin_hits;
 
-static void conv_free(void *p) { ddt_convertor_destroy((ddt_convertor_t *) p); }
-static void key_init(void) { (void) pthread_key_create(&g_key, conv_free); }
+static void unpin_all(thread_state *ts)
+{
+    for (int i = 0; i < PIN_SLOTS; ++i)
+        if (ts->pin[i].e) {
+            bridge_release(ts->pin[i].e);
+            ts->pin[i].e = NULL;
+        }
+}
+
+static void state_free(void *p)
+{
+    thread_state *ts = (thread_state *) p;
+    pthread_mutex_lock(&g_ts_mu);
+    g_exited_pin_hits += __atomic_load_n(&ts->pin_hits, __ATOMIC_RELAXED);
+    if (ts->prev)
+        ts->prev->next = ts->next;
+    else
+        g_ts_head = ts->next;
+    if (ts->next)
+        ts->next->prev = ts->prev;
+    pthread_mutex_unlock(&g_ts_mu);
+    unpin_all(ts);
+    if (ts->h)
+        ddt_convertor_destroy(ts->h);
+    free(ts);
+}
+
+static void key_init(void) { (void) pthread_key_create(&g_key, state_free); }
+
+static size_t pin_hits_total(void)
+{
+    pthread_mutex_lock(&g_ts_mu);
+    size_t n = g_exited_pin_hits;
+    for (thread_state *t = g_ts_head; t; t = t->next)
+        n += __atomic_load_n(&t->pin_hits, __ATOMIC_RELAXED);
+    pthread_mutex_unlock(&g_ts_mu);
+    return n;
+}
+
+static void unpin_current_thread(void)
+{
+    (void) pthread_once(&g_once, key_init);
+    thread_state *ts = (thread_state *) pthread_getspecific(g_key);
+    if (ts)
+        unpin_all(ts);
+}
+
+static thread_state *thread_state_get(void)
+{
+    (void) pthread_once(&g_once, key_init);
+    thread_state *ts = (thread_state *) pthread_getspecific(g_key);
+    if (!ts) {
+        ts = (thread_state *) calloc(1, sizeof(*ts));
+        if (ts && pthread_setspecific(g_key, ts) != 0) {
+            free(ts);
+            ts = NULL;
+        }
+        if (ts) {
+            pthread_mutex_lock(&g_ts_mu);
+            ts->next = g_ts_head;
+            if (g_ts_head)
+                g_ts_head->prev = ts;
+            g_ts_head = ts;
+            pthread_mutex_unlock(&g_ts_mu);
+        }
+    }
+    return ts;
+}
 
 static ddt_convertor_t *thread_convertor(void)
 {
-    (void) pthread_once(&g_once, key_init);
-    ddt_convertor_t *h = (ddt_convertor_t *) pthread_getspecific(g_key);
-    if (!h) {
-        h = ddt_convertor_create();
-        if (h && pthread_setspecific(g_key, h) != 0) {
-            ddt_convertor_destroy(h);
-            h = NULL;
+    thread_state *ts = thread_state_get();
+    if (!ts)
+        return NULL;
+    if (!ts->h)
+        ts->h = ddt_convertor_create();
+    return ts->h;
+}
+
+/* The entry of the convertor's datatype for one call: from this thread's pins when the cache
+ * generation has not moved since they were taken (no lock, no shared write; *pinned = 1: do
+ * not release), else a normal held lookup (*pinned = 0 unless it was kept as a new pin). */
+static bridge_entry *bridge_type_of_call(const opal_convertor_t *conv, int *err, int *pinned)
+{
+    *pinned = 0;
+    const opal_datatype_t *dt = conv->pDesc;
+    const dt_type_desc_t *ud = conv->use_desc ? conv->use_desc : (dt ? &dt->opt_desc : NULL);
+    thread_state *ts = thread_state_get();
+    if (!ts || !dt || !ud || !ud->desc || !(dt->flags & OPAL_DATATYPE_FLAG_COMMITTED))
+        return bridge_entry_of(dt, ud, 1, err);
+    const uint64_t sig = desc_sig(ud->desc, ud->used);
+    const unsigned long gen = __atomic_load_n(&g_gen, __ATOMIC_SEQ_CST);
+    for (int i = 0; i < PIN_SLOTS; ++i) {
+        pin_slot *p = &ts->pin[i];
+        if (!p->e)
+            continue;
+        if (p->gen != gen) {   /* something was unlinked: this pin may be stale */
+            bridge_release(p->e);
+            p->e = NULL;
+            continue;
+        }
+        if (p->key == dt && p->ud == ud && p->sig == sig && same_fingerprint(p->e, dt, ud, sig)) {
+            p->used = ++ts->tick;
+            __atomic_store_n(&ts->pin_hits, ts->pin_hits + 1, __ATOMIC_RELAXED);
+            *err = OPAL_SUCCESS;
+            *pinned = 1;
+            return p->e;
         }
     }
-    return h;
+    bridge_entry *e = bridge_entry_of(dt, ud, 1, err);
+    if (!e)
+        return NULL;
+    /* keep the held reference as a pin in the least recently used slot, unless an entry was
+     * unlinked meanwhile (then this one may be the unlinked one: release it after the call) */
+    if (__atomic_load_n(&g_gen, __ATOMIC_SEQ_CST) != gen)
+        return e;
+    int v = 0;
+    for (int i = 1; i < PIN_SLOTS; ++i)
+        if (!ts->pin[i].e || (ts->pin[v].e && ts->pin[i].used < ts->pin[v].used))
+            v = i;
+    if (ts->pin[v].e)
+        bridge_release(ts->pin[v].e);
+    ts->pin[v] = (pin_slot){e, dt, ud, sig, gen, ++ts->tick};
+    *pinned = 1;
+    return e;
+}
+
+static void bridge_done(bridge_entry *e, int pinned)
+{
+    if (!pinned)
+        bridge_release(e);
 }
 
 static int32_t opal_code(int rc)
@@ -339,12 +561,12 @@ static int32_t bridge_advance(opal_convertor_t *conv, struct iovec *iov, uint32_
     }
     if (!(conv->flags & CONVERTOR_HOMOGENEOUS))   /* as the accelerator movers assert (:180) */
         return OPAL_ERR_NOT_SUPPORTED;
-    int err;
-    bridge_entry *e = bridge_type_of(conv, &err);
+    int err, pinned;
+    bridge_entry *e = bridge_type_of_call(conv, &err, &pinned);
     if (!e)
         return err;
     int32_t r = bridge_move(conv, e->type, iov, out_size, max_data, pack);
-    bridge_release(e);
+    bridge_done(e, pinned);
     if (r < 0)
         return r;
     conv->bConverted += *max_data;
@@ -377,12 +599,12 @@ int32_t opal_position_hip(opal_convertor_t *conv, size_t *position)
      * The snap follows the imported use_desc, so a UINT4 blen 5 carrier snaps to 4 bytes. */
     size_t p = *position;
     if (conv->flags & CONVERTOR_SEND) {
-        int err;
-        bridge_entry *e = bridge_type_of(conv, &err);
+        int err, pinned;
+        bridge_entry *e = bridge_type_of_call(conv, &err, &pinned);
         if (!e)
             return err;
         const int rc = ddt_type_snap_position(e->type, p, &p);
-        bridge_release(e);
+        bridge_done(e, pinned);
         if (rc != DDT_SUCCESS)
             return opal_code(rc);
     }
@@ -399,11 +621,11 @@ int opal_hip_bridge_attach(opal_convertor_t *conv)
         return OPAL_ERR_BAD_PARAM;
     if (!(conv->flags & CONVERTOR_ACCELERATOR) || !(conv->flags & CONVERTOR_HOMOGENEOUS))
         return OPAL_ERR_NOT_SUPPORTED;   /* host buffers keep the reference movers */
-    int err;
-    bridge_entry *e = bridge_type_of(conv, &err);
+    int err, pinned;
+    bridge_entry *e = bridge_type_of_call(conv, &err, &pinned);
     if (!e)
         return err;
-    bridge_release(e);
+    bridge_done(e, pinned);
     conv->fAdvance = (conv->flags & CONVERTOR_SEND) ? opal_pack_hip : opal_unpack_hip;
     conv->fPosition = opal_position_hip;
     return OPAL_SUCCESS;

@@ -350,7 +350,7 @@ void note_stream_locked(Plan &P, hipStream_t stream, int cap = -1)   // P.mu hel
 
 void note_stream(Plan &P, hipStream_t stream)
 {
-    std::lock_guard<std::mutex> g(P.mu);
+    std::lock_guard<SpinMutex> g(P.mu);
     note_stream_locked(P, stream);
 }
 
@@ -370,11 +370,9 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         return DDT_SUCCESS;
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
-    {
-        std::lock_guard<std::mutex> g(P.mu);
-        if (P.device < 0)
-            P.device = dev;
-    }
+    int none = -1;
+    if (P.device.load(std::memory_order_relaxed) < 0)   // a plan made without a device takes this one
+        (void) P.device.compare_exchange_strong(none, dev);
     if (P.device != dev)
         return fail(DDT_ERR_NOT_SUPPORTED, "convertor prepared on device " + std::to_string(P.device)
                                                + "; current device is " + std::to_string(dev)
@@ -419,22 +417,178 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                 uint8_t *pk = reinterpret_cast<uint8_t *>(wins[0].ptr + i * uint64_t(t->size));
                 // spol bits, plus the pass-2 quads (256) and the pass-1 stagger (bits 16..23)
                 const uint32_t pol = uint32_t(tuning().spol) | (tuning().s2vec ? 256u : 0u)
+                                     | (tuning().spipe ? 1024u : 0u)
                                      | (uint32_t(std::min<long>(tuning().sstagger, 255)) << 16);
+                SL->pipe_wgs = uint32_t(std::max<long>(tuning().spipe, 0)) > 1 ? uint32_t(tuning().spipe) : 0u;
                 HIPCHK(SL->run(u, pk, dir, pol, stream, uint32_t(tuning().sunroll),
                                uint32_t(tuning().s2unroll)));
             }
             return DDT_SUCCESS;
         }
     }
+    // The launch is enqueued outside the plan lock, so another thread may evict the set
+    // meanwhile.  This call holds it (`inflight`, taken with the lookup) so its memory is not
+    // recycled, and if it was retired, a launch by pointer leaves a late event behind it for
+    // the retirement to wait on.  A retired set that fits in the kernel arguments is launched
+    // from them instead.  (The local shared_ptr S keeps the object; Hold only points at it.)
+    struct Hold {
+        Plan &P;
+        ItemSet *S;
+        hipStream_t stream;
+        bool by_pointer = false;
+        ~Hold()
+        {
+            if (!S)
+                return;
+            std::lock_guard<SpinMutex> g(P.mu);
+            --S->inflight;
+            if (by_pointer && S->retired && !S->pinned) {
+                hipEvent_t e = nullptr;
+                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess
+                    && hipEventRecord(e, stream) == hipSuccess) {
+                    S->late.push_back(e);
+                } else {
+                    (void) hipGetLastError();
+                    if (e)
+                        (void) hipEventDestroy(e);
+                    for (const auto &sp : P.graveyard)   // pin_retired wants the owning pointer
+                        if (sp.set.get() == S) {
+                            const std::shared_ptr<ItemSet> keep = sp.set;
+                            pin_retired(P, keep);
+                            break;
+                        }
+                    S->pinned = true;
+                }
+            }
+        }
+    };
+    // A descriptor set travels in the kernel-argument segment on its first launch (no upload
+    // for one-off windows).  From its second launch on it is launched by pointer from HBM:
+    // with device-resident kernel arguments every 64-byte line of arguments is a host write
+    // across PCIe, and a 528-byte block costs 2.6 us of host time per launch against 0.7 us
+    // for a pointer (scripts/hostbench.cpp, profiles/r1_hostbench.log).
+    Item *d_items = nullptr;
+    int slot_k = -1, slot_b = -1;
+    uint32_t slot_gen = 0;
+    // the stream's capture state, queried before the plan lock: HIP answers under a global lock
+    // of its own, and threads sharing this plan must not queue behind it (r6 thread scaling)
+    const bool cap = capturing(stream);
+    Hold hold{P, nullptr, stream};
     std::shared_ptr<ItemSet> S;
+    // The launch decision for set S (plan lock held): by pointer or inline, capture pinning, the
+    // launch slot.  A cache hit makes it in the same critical section as its lookup: threads
+    // sharing a datatype take the plan lock twice per call (here and in Hold), not four times,
+    // and write the set's shared lines only when something changes (r6 thread scaling).
+    // a set with no items moves nothing; a single line-dense item may launch by value
+    // (launch_single_item): both skip the decision unless the by-value launch declines
+    auto maybe_direct = [&]() { return S->items.empty() || (S->items.size() == 1 && grid_cap == 0 && S->all_dense); };
+    auto decide = [&]() {
+        if (S->inline_ok && !S->retired && S->uses < 2 && ++S->uses >= 2 && !S->d_items && tuning().ptr) {
+            size_t bytes = S->items.size() * sizeof(Item);
+            RelaxedCapture relaxed;
+            PoolNoDeviceSync no_sync(capture_seen(stream));
+            Item *d = take_items_memory(P, bytes, !cap);
+            if (d) {
+                if (upload(d, S->items.data(), bytes) == hipSuccess)
+                    S->d_items = d;
+                else
+                    P.spare.push_back({d, bytes});
+            }
+        }
+        d_items = (S->inline_ok && (!tuning().ptr || S->retired)) ? nullptr : S->d_items;
+        if (!d_items)
+            return;
+        if (cap) {
+            // the graph keeps this pointer: never recycle it before the plan goes
+            if (S->retired && !S->pinned)
+                pin_retired(P, S);
+            S->pinned = true;
+        } else if (tuning().slots && grid_cap == 0 && !S->all_dense && !S->has_lists && !S->retired
+                   && S->bytes <= uint64_t(tuning().slot_max_kb) << 10) {
+            // an argument-free launch (ddt_move.hip.h, ddt_move_slot_kernel): a set bound to
+            // a slot for these buffers and this direction; buffers seen again within the set's
+            // last kHist launches bind one (its record is in device memory before this launch;
+            // two bindings serve a double-buffered exchange).  Small launches only: a slot
+            // kernel's workgroups first load the record (one more dependent load than
+            // arguments preloaded into registers), which a large launch of latency-bound
+            // gathers pays (the halo's 48 MiB pack 66.4 -> 68.2 us), while the host's 2.2 us
+            // saving only matters where the kernel is as short as a launch
+            const int fam = dir << 8;
+            ++S->launches;
+            int hit = -1;
+            for (int i = 0; i < ItemSet::kSetBind; ++i)
+                if (S->bind[i].slot >= 0 && (S->bind[i].slot & ~255) == fam && S->bind[i].ubase == ubase
+                    && S->bind[i].pbase == pbase)
+                    hit = i;
+            bool seen = hit >= 0;
+            for (int i = 0; i < ItemSet::kHist && !seen; ++i)
+                seen = S->hist_u[i] == ubase && S->hist_p[i] == pbase;
+            if (hit < 0 && seen && S->launches >= S->bind_backoff) {
+                // bind these buffers in a free binding, else in place of the least recently
+                // used one if it sat idle for kSetIdle launches of the set (given up behind
+                // fences on the set's streams).  A binding in use is never taken: threads
+                // sharing the set on more buffer pairs than it holds bindings keep theirs,
+                // the rest launch with arguments (round 6: taking turns rebound on every
+                // call, a synchronous record upload each, bridgethreads shared 4 threads
+                // 16.8 us per call)
+                constexpr uint64_t kSetIdle = 32, kBindBackoff = 32;
+                int pick = -1, lru = 0;
+                for (int i = 0; i < ItemSet::kSetBind && pick < 0; ++i)
+                    if (S->bind[i].slot < 0)
+                        pick = i;
+                    else if (S->bind[i].used < S->bind[lru].used)
+                        lru = i;
+                if (pick < 0 && S->launches - S->bind[lru].used >= kSetIdle)
+                    pick = lru;
+                if (pick >= 0) {
+                    ItemSet::Binding &B = S->bind[pick];
+                    if (B.slot >= 0) {
+                        slot_release(S->slot_dev, B.slot >> 8, B.slot & 255, B.gen, &S->streams);
+                        B.slot = -1;
+                    }
+                    const LaunchRec rec{uint64_t(uintptr_t(d_items)), ubase, pbase, uint32_t(S->items.size()),
+                                        S->ntasks};
+                    const int k = slot_bind(P.device, dir, rec, &B.gen);
+                    if (k >= 0) {
+                        B.slot = fam | k;
+                        B.ubase = ubase;
+                        B.pbase = pbase;
+                        S->slot_dev = P.device;
+                        hit = pick;
+                    }
+                }
+                // every binding of the set in use: do not rescan on every call (a full slot
+                // table is retried at once: each attempt ages the table's idle bindings)
+                if (pick < 0)
+                    S->bind_backoff = S->launches + kBindBackoff;
+            }
+            if (hit >= 0) {
+                S->bind[hit].used = S->launches;
+                slot_k = S->bind[hit].slot & 255;
+                slot_gen = S->bind[hit].gen;
+                slot_b = hit;
+            } else {   // the history matters only for buffers not bound yet
+                S->hist_u[S->hist_at] = ubase;
+                S->hist_p[S->hist_at] = pbase;
+                S->hist_at = (S->hist_at + 1) % ItemSet::kHist;
+            }
+        }
+        if (std::find(S->streams.begin(), S->streams.end(), stream) == S->streams.end())
+            S->streams.push_back(stream);
+        note_stream_locked(P, stream, cap ? 1 : 0);   // one capture query per call (HIP takes a global lock)
+        hold.by_pointer = true;
+    };
     {
-        std::lock_guard<std::mutex> g(P.mu);
+        std::lock_guard<SpinMutex> g(P.mu);
         for (size_t i = 0; i < P.cache.size(); ++i) {
             if (P.cache[i]->key == key) {
                 S = P.cache[i];
-                ++S->inflight;   // held until this call has enqueued its launch (Hold below)
+                ++S->inflight;   // held until this call has enqueued its launch (Hold)
+                hold.S = S.get();
                 if (i)
                     std::rotate(P.cache.begin(), P.cache.begin() + long(i), P.cache.begin() + long(i) + 1);
+                if (!maybe_direct())
+                    decide();
                 break;
             }
         }
@@ -471,8 +625,8 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             RelaxedCapture relaxed;   // reap queries, allocation, upload: leave other threads' captures be
             PoolNoDeviceSync no_sync(capture_seen(stream));
             {
-                std::lock_guard<std::mutex> g(P.mu);
-                S->d_items = take_items_memory(P, bytes, !capturing(stream));
+                std::lock_guard<SpinMutex> g(P.mu);
+                S->d_items = take_items_memory(P, bytes, !cap);
             }
             if (!S->d_items)
                 return fail(DDT_ERR_OUT_OF_RESOURCE, "descriptor memory");
@@ -480,158 +634,28 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             if (e != hipSuccess)
                 return fail(DDT_ERR_HIP, std::string("item upload: ") + hipGetErrorString(e));
         }
-        std::lock_guard<std::mutex> g(P.mu);
+        std::lock_guard<SpinMutex> g(P.mu);
         ++S->inflight;
+        hold.S = S.get();
         P.cache.insert(P.cache.begin(), S);
         if (P.cache.size() > kCacheEntries) {
             retire(P, P.cache.back());
             P.cache.pop_back();
         }
+        if (!maybe_direct())
+            decide();
     }
-    // The launch is enqueued outside the plan lock, so another thread may evict the set
-    // meanwhile.  This call holds it (`inflight`, taken with the lookup) so its memory is not
-    // recycled, and if it was retired, a launch by pointer leaves a late event behind it for
-    // the retirement to wait on.  A retired set that fits in the kernel arguments is launched
-    // from them instead.
-    struct Hold {
-        Plan &P;
-        std::shared_ptr<ItemSet> S;
-        hipStream_t stream;
-        bool by_pointer = false;
-        ~Hold()
-        {
-            std::lock_guard<std::mutex> g(P.mu);
-            --S->inflight;
-            if (by_pointer && S->retired && !S->pinned) {
-                hipEvent_t e = nullptr;
-                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess
-                    && hipEventRecord(e, stream) == hipSuccess) {
-                    S->late.push_back(e);
-                } else {
-                    (void) hipGetLastError();
-                    if (e)
-                        (void) hipEventDestroy(e);
-                    pin_retired(P, S);
-                }
-            }
-        }
-    } hold{P, S, stream};
     if (S->items.empty())
         return DDT_SUCCESS;
-    if (S->items.size() == 1 && grid_cap == 0) {
+    if (maybe_direct()) {
         // a large single-item line-dense launch carries the item's fields by value
         hipError_t e = hipSuccess;
         if (launch_single_item(S->items[0], dir, ubase, pbase, stream, &e)) {
             HIPCHK(e);
             return DDT_SUCCESS;
         }
-    }
-    // A descriptor set travels in the kernel-argument segment on its first launch (no upload
-    // for one-off windows).  From its second launch on it is launched by pointer from HBM:
-    // with device-resident kernel arguments every 64-byte line of arguments is a host write
-    // across PCIe, and a 528-byte block costs 2.6 us of host time per launch against 0.7 us
-    // for a pointer (scripts/hostbench.cpp, profiles/r1_hostbench.log).
-    Item *d_items = nullptr;
-    int slot_k = -1, slot_b = -1;
-    uint32_t slot_gen = 0;
-    // the stream's capture state, queried before the plan lock: HIP answers under a global lock
-    // of its own, and threads sharing this plan must not queue behind it (r6 thread scaling)
-    const bool cap = capturing(stream);
-    {
-        std::lock_guard<std::mutex> g(P.mu);
-        if (S->inline_ok && !S->retired && ++S->uses >= 2 && !S->d_items && tuning().ptr) {
-            size_t bytes = S->items.size() * sizeof(Item);
-            RelaxedCapture relaxed;
-            PoolNoDeviceSync no_sync(capture_seen(stream));
-            Item *d = take_items_memory(P, bytes, !capturing(stream));
-            if (d) {
-                if (upload(d, S->items.data(), bytes) == hipSuccess)
-                    S->d_items = d;
-                else
-                    P.spare.push_back({d, bytes});
-            }
-        }
-        d_items = (S->inline_ok && (!tuning().ptr || S->retired)) ? nullptr : S->d_items;
-        if (d_items) {
-            if (cap) {
-                // the graph keeps this pointer: never recycle it before the plan goes
-                if (S->retired && !S->pinned)
-                    pin_retired(P, S);
-                S->pinned = true;
-            } else if (tuning().slots && grid_cap == 0 && !S->all_dense && !S->has_lists && !S->retired
-                       && S->bytes <= uint64_t(tuning().slot_max_kb) << 10) {
-                // an argument-free launch (ddt_move.hip.h, ddt_move_slot_kernel): a set bound to
-                // a slot for these buffers and this direction; buffers seen again within the set's
-                // last kHist launches bind one (its record is in device memory before this launch;
-                // two bindings serve a double-buffered exchange).  Small launches only: a slot
-                // kernel's workgroups first load the record (one more dependent load than
-                // arguments preloaded into registers), which a large launch of latency-bound
-                // gathers pays (the halo's 48 MiB pack 66.4 -> 68.2 us), while the host's 2.2 us
-                // saving only matters where the kernel is as short as a launch
-                const int fam = dir << 8;
-                ++S->launches;
-                int hit = -1;
-                for (int i = 0; i < ItemSet::kSetBind; ++i)
-                    if (S->bind[i].slot >= 0 && (S->bind[i].slot & ~255) == fam && S->bind[i].ubase == ubase
-                        && S->bind[i].pbase == pbase)
-                        hit = i;
-                bool seen = false;
-                for (int i = 0; i < ItemSet::kHist; ++i)
-                    seen = seen || (S->hist_u[i] == ubase && S->hist_p[i] == pbase);
-                if (hit < 0 && seen && S->launches >= S->bind_backoff) {
-                    // bind these buffers in a free binding, else in place of the least recently
-                    // used one if it sat idle for kSetIdle launches of the set (given up behind
-                    // fences on the set's streams).  A binding in use is never taken: threads
-                    // sharing the set on more buffer pairs than it holds bindings keep theirs,
-                    // the rest launch with arguments (round 6: taking turns rebound on every
-                    // call, a synchronous record upload each, bridgethreads shared 4 threads
-                    // 16.8 us per call)
-                    constexpr uint64_t kSetIdle = 32, kBindBackoff = 32;
-                    int pick = -1, lru = 0;
-                    for (int i = 0; i < ItemSet::kSetBind && pick < 0; ++i)
-                        if (S->bind[i].slot < 0)
-                            pick = i;
-                        else if (S->bind[i].used < S->bind[lru].used)
-                            lru = i;
-                    if (pick < 0 && S->launches - S->bind[lru].used >= kSetIdle)
-                        pick = lru;
-                    if (pick >= 0) {
-                        ItemSet::Binding &B = S->bind[pick];
-                        if (B.slot >= 0) {
-                            slot_release(S->slot_dev, B.slot >> 8, B.slot & 255, B.gen, &S->streams);
-                            B.slot = -1;
-                        }
-                        const LaunchRec rec{uint64_t(uintptr_t(d_items)), ubase, pbase, uint32_t(S->items.size()),
-                                            S->ntasks};
-                        const int k = slot_bind(P.device, dir, rec, &B.gen);
-                        if (k >= 0) {
-                            B.slot = fam | k;
-                            B.ubase = ubase;
-                            B.pbase = pbase;
-                            S->slot_dev = P.device;
-                            hit = pick;
-                        }
-                    }
-                    // every binding of the set in use: do not rescan on every call (a full slot
-                    // table is retried at once: each attempt ages the table's idle bindings)
-                    if (pick < 0)
-                        S->bind_backoff = S->launches + kBindBackoff;
-                }
-                if (hit >= 0) {
-                    S->bind[hit].used = S->launches;
-                    slot_k = S->bind[hit].slot & 255;
-                    slot_gen = S->bind[hit].gen;
-                    slot_b = hit;
-                }
-                S->hist_u[S->hist_at] = ubase;
-                S->hist_p[S->hist_at] = pbase;
-                S->hist_at = (S->hist_at + 1) % ItemSet::kHist;
-            }
-            if (std::find(S->streams.begin(), S->streams.end(), stream) == S->streams.end())
-                S->streams.push_back(stream);
-            note_stream_locked(P, stream, cap ? 1 : 0);   // one capture query per call (HIP takes a global lock)
-            hold.by_pointer = true;
-        }
+        std::lock_guard<SpinMutex> g(P.mu);   // declined: the ordinary decision
+        decide();
     }
     if (!d_items && S->has_lists)
         note_stream(P, stream);   // an inline launch of index lists reads the plan's lists
@@ -641,7 +665,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             HIPCHK(e);
             return DDT_SUCCESS;
         }
-        std::lock_guard<std::mutex> g(P.mu);   // the binding was ended (evicted): launch with arguments
+        std::lock_guard<SpinMutex> g(P.mu);   // the binding was ended (evicted): launch with arguments
         ItemSet::Binding &B = S->bind[slot_b];
         if (B.slot == ((dir << 8) | slot_k) && B.gen == slot_gen)
             B.slot = -1;
@@ -659,6 +683,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
 
 struct ddt_convertor {
     ddt_datatype *dt = nullptr;
+    uint64_t dt_serial = 0;   // dt->serial when prepared (a recycled address is another type)
     std::shared_ptr<Plan> plan;
     uint64_t count = 0;
     uint64_t base = 0;
@@ -865,7 +890,9 @@ int prepare(ddt_convertor *c, const ddt_datatype *t, size_t count, const void *b
     if (!(t->flags & F_COMMITTED))
         return fail(DDT_ERR_NOT_COMMITTED, "datatype not committed");
     ddt_datatype *dt = const_cast<ddt_datatype *>(t);
+    const bool same_type = c->dt == dt && c->dt_serial == dt->serial && c->plan;
     c->dt = dt;
+    c->dt_serial = dt->serial;
     c->count = count;
     c->base = uint64_t(uintptr_t(buf));
     c->send = send;
@@ -882,6 +909,13 @@ int prepare(ddt_convertor *c, const ddt_datatype *t, size_t count, const void *b
     if (classify(static_cast<const char *>(buf) + t->true_lb) != MEM_DEVICE)
         return fail(DDT_ERR_NOT_DEVICE, "user buffer is not device memory: the HIP engine is the "
                                         "accelerator slot of the convertor");
+    // a convertor prepared again with the type it holds keeps its plan when the device is the
+    // same (the bridge re-prepares its per-thread convertor on every fAdvance: no shared plan
+    // table lock or reference count per call, r6 thread scaling)
+    int dev = -1;
+    if (same_type && hipGetDevice(&dev) == hipSuccess && c->plan->device == dev)
+        return DDT_SUCCESS;
+    (void) hipGetLastError();
     try {
         c->plan = get_plan(dt);
     } catch (const std::exception &ex) {
@@ -1665,7 +1699,7 @@ int ddt_type_engine_info(const ddt_datatype_t *t, int64_t *out4)
     } catch (const std::exception &ex) {
         return fail(DDT_ERR_OUT_OF_RESOURCE, ex.what());
     }
-    std::lock_guard<std::mutex> g(P->mu);
+    std::lock_guard<SpinMutex> g(P->mu);
     out4[0] = P->sorted_state;
     out4[1] = P->sorted ? int64_t(P->sorted->dev_bytes) : 0;
     out4[2] = P->sorted ? int64_t(P->sorted->nc) : 0;
@@ -1685,7 +1719,7 @@ int ddt_type_cache_info(const ddt_datatype_t *t, int64_t *out4)
     } catch (const std::exception &ex) {
         return fail(DDT_ERR_OUT_OF_RESOURCE, ex.what());
     }
-    std::lock_guard<std::mutex> g(P->mu);
+    std::lock_guard<SpinMutex> g(P->mu);
     reap(*P, false);
     out4[0] = int64_t(P->cache.size());
     out4[1] = int64_t(P->graveyard.size());
@@ -1932,6 +1966,8 @@ int ddt_tune(const char *key, long value)
         tuning().sigspin_us = value < 0 ? 0 : value;
     else if (k == "s2vec")
         tuning().s2vec = value ? 1 : 0;
+    else if (k == "spipe")
+        tuning().spipe = value < 0 ? 0 : (value > 4096 ? 4096 : value);
     else if (k == "sskew")
         tuning().sskew = value < 0 ? 0 : (value > (1 << 20) ? (1 << 20) : value);
     else if (k == "sstagger")

@@ -14,6 +14,7 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <sched.h>
 #include <mutex>
 #include <vector>
 
@@ -23,6 +24,32 @@
 #include "ddt_sorted.h"
 
 namespace ddt {
+
+// A lock for short critical sections taken on every pack / unpack call (a plan's descriptor
+// cache, a type's plan table, a launch slot): it spins briefly, then yields, and never parks the
+// thread in the kernel.  Under MPI_THREAD_MULTIPLE threads sharing one datatype take its plan's
+// lock several times per call; a futex-based mutex convoyed there (r6, scripts/bridgethreads.c
+// shared: 8 threads 31.7 us per call, profiles/r6_threads.jsonl).
+class SpinMutex {
+public:
+    void lock()
+    {
+        for (unsigned spins = 0; flag_.exchange(true, std::memory_order_acquire);) {
+            while (flag_.load(std::memory_order_relaxed)) {
+                if (++spins < 2048)
+                    __builtin_ia32_pause();
+                else
+                    sched_yield();   // the holder is descheduled or in a long section (an upload)
+            }
+        }
+    }
+    bool try_lock() { return !flag_.exchange(true, std::memory_order_acquire); }
+    void unlock() { flag_.store(false, std::memory_order_release); }
+
+private:
+    std::atomic<bool> flag_{false};
+};
+
 
 enum : uint32_t {
     F_PREDEFINED = 0x0002u,
@@ -182,9 +209,9 @@ struct Plan {
     std::vector<Leaf> leaves;
     std::vector<DevList> dev;     // one per LIST leaf (index in Leaf order, others empty)
     uint64_t dev_bytes = 0;       // device metadata bytes
-    bool dev_ready = false;       // index lists uploaded
-    std::mutex mu;
-    int device = -1;              // HIP device holding this plan's device state (first use)
+    std::atomic<bool> dev_ready{false};   // index lists uploaded (read without the lock)
+    SpinMutex mu;
+    std::atomic<int> device{-1};  // HIP device holding this plan's device state (first use)
     std::vector<std::shared_ptr<ItemSet>> cache;      // most recent first
     std::vector<Retired> graveyard;                   // evicted, freed once their events pass
     std::vector<std::shared_ptr<ItemSet>> pinned;     // evicted but held by captured graphs
@@ -202,7 +229,12 @@ struct Plan {
 
 }  // namespace ddt
 
+uint64_t ddt_next_serial();   // ddt_typemap.cpp: process-unique datatype serial numbers
+
 struct ddt_datatype {
+    // process-unique, never reused (a convertor re-prepared with the datatype it already holds
+    // keeps its plan: an address alone could belong to a destroyed type's successor)
+    const uint64_t serial = ddt_next_serial();
     uint16_t id = 0;              // predefined OPAL id, 0 for derived
     uint32_t flags = ddt::F_CONTIGUOUS;
     int64_t size = 0;
@@ -221,7 +253,7 @@ struct ddt_datatype {
     bool imported = false;        // desc is already a committed opt_desc (ddt_type_from_opal_desc)
     uint32_t opt_flags = 0;       // OPAL_DATATYPE_OPTIMIZED_RESTRICTED after commit (ddt_optimize.h)
     std::vector<uint64_t> opt_prefix;  // packed offset of each top-level opt node
-    std::mutex plan_mu;
+    ddt::SpinMutex plan_mu;
     // one plan per HIP device the type is moved on (index = device ordinal): a plan's descriptor
     // sets, lists and tables live in that device's HBM
     std::vector<std::shared_ptr<ddt::Plan>> plans;

@@ -153,7 +153,7 @@ ExtPlan::~ExtPlan()
 
 std::shared_ptr<ExtPlan> get_ext_plan(ddt_datatype *t)
 {
-    std::lock_guard<std::mutex> g(t->plan_mu);
+    std::lock_guard<ddt::SpinMutex> g(t->plan_mu);
     if (t->ext)
         return t->ext;
     auto X = std::make_shared<ExtPlan>();

@@ -207,14 +207,18 @@ Plan::~Plan()
 // of the binding follows (its generation moved), and later binds and ddt_trim retry the fences
 // (the entry is never picked as an eviction victim or freed without them).
 namespace {
-constexpr uint64_t kEvictIdle = 256;   // ticks: slot launches and bind attempts of the process
+// ticks: bind attempts of the process (a slot launch only reads the tick: no cache line all
+// launching threads write, r6 thread scaling); a binding not launched during the last kEvictIdle
+// attempts may be evicted
+constexpr uint64_t kEvictIdle = 256;
 constexpr int kMaxDev = 64;
 struct SlotEntry {
-    std::mutex mu;                      // launches of this record; changes of its binding
+    SpinMutex mu;                       // launches of this record; changes of its binding
     bool used = false;
     bool ending = false;                // binding ended, fences not recorded yet: retry
     uint32_t gen = 0;                   // bumped when a binding ends
-    std::atomic<uint64_t> last{0};      // tick of the last launch or bind
+    std::atomic<uint64_t> last{0};      // tick at the last launch or bind
+    int64_t launches = 0;               // argument-free launches of this record (statistics)
     std::vector<hipStream_t> streams;   // streams the binding launched on
     std::vector<hipEvent_t> fences;     // the last binding's launches: passed before the next bind
 };
@@ -228,7 +232,7 @@ struct Slots {
     std::mutex mu;                                   // creation of a device's families
     std::atomic<std::array<SlotFamily, 2> *> dev[kMaxDev] = {};   // per device: pack, unpack
     std::atomic<uint64_t> tick{0};
-    std::atomic<int64_t> binds{0}, launches{0};
+    std::atomic<int64_t> binds{0};
 };
 Slots &slots()
 {
@@ -266,7 +270,7 @@ bool fences_passed(std::vector<hipEvent_t> &f)
 // recorded now; the entry stays taken and ending, for a later retry).  Family lock held.
 bool end_binding(SlotEntry &E, const std::vector<hipStream_t> *extra = nullptr)
 {
-    std::lock_guard<std::mutex> g(E.mu);   // after any launch of the binding in progress
+    std::lock_guard<SpinMutex> g(E.mu);   // after any launch of the binding in progress
     if (!E.used)
         return true;
     if (!E.ending) {
@@ -376,7 +380,7 @@ int slot_bind(int dev, int dir, const LaunchRec &rec, uint32_t *gen)
             (void) hipGetLastError();
             return -1;
         }
-        std::lock_guard<std::mutex> ge(E.mu);
+        std::lock_guard<SpinMutex> ge(E.mu);
         E.used = true;
         E.last.store(++S.tick, std::memory_order_relaxed);
         *gen = E.gen;
@@ -397,14 +401,16 @@ bool slot_launch(int dev, int dir, int k, uint32_t gen, uint32_t ntasks, hipStre
     if (!F)
         return false;
     SlotEntry &E = F->e[k];
-    std::lock_guard<std::mutex> g(E.mu);   // this entry only: other slots launch concurrently
+    std::lock_guard<SpinMutex> g(E.mu);   // this entry only: other slots launch concurrently
     if (!E.used || E.ending || E.gen != gen)
         return false;   // the binding ended
     if (std::find(E.streams.begin(), E.streams.end(), stream) == E.streams.end())
         E.streams.push_back(stream);
-    E.last.store(++S.tick, std::memory_order_relaxed);
+    const uint64_t now = S.tick.load(std::memory_order_relaxed);
+    if (E.last.load(std::memory_order_relaxed) != now)
+        E.last.store(now, std::memory_order_relaxed);
     *err = launch_move_slot(dir, uint32_t(k), ntasks, stream);
-    ++S.launches;
+    ++E.launches;
     return true;
 }
 
@@ -419,7 +425,7 @@ void slot_release(int dev, int dir, int k, uint32_t gen, const std::vector<hipSt
     std::lock_guard<std::mutex> g(F->mu);
     SlotEntry &E = F->e[k];
     {
-        std::lock_guard<std::mutex> ge(E.mu);
+        std::lock_guard<SpinMutex> ge(E.mu);
         if (!E.used || E.ending || E.gen != gen)
             return;   // already ended (evicted)
         if (!fence_streams) {   // its launches have all passed
@@ -470,7 +476,14 @@ void slot_stats(int dev, int64_t *out4)
                 out4[dir] += E.used ? 1 : 0;
         }
     out4[2] = S.binds.load();
-    out4[3] = S.launches.load();
+    out4[3] = 0;
+    for (int d = 0; d < kMaxDev; ++d)
+        if (std::array<SlotFamily, 2> *f2 = families(S, d, false))
+            for (SlotFamily &F : *f2)
+                for (SlotEntry &E : F.e) {
+                    std::lock_guard<SpinMutex> ge(E.mu);
+                    out4[3] += E.launches;
+                }
 }
 
 // Test hook (ddt_slot_debug): the state of slot k of (dev, dir): bit 0 used, bit 1 ending,
@@ -483,7 +496,7 @@ int slot_debug_state(int dev, int dir, int k)
         return -1;
     std::lock_guard<std::mutex> g(F->mu);
     SlotEntry &E = F->e[k];
-    std::lock_guard<std::mutex> ge(E.mu);
+    std::lock_guard<SpinMutex> ge(E.mu);
     return (E.used ? 1 : 0) | (E.ending ? 2 : 0) | int(E.streams.size() << 8);
 }
 
@@ -596,7 +609,7 @@ std::shared_ptr<Plan> get_plan(ddt_datatype *t)
         dev = -1;
     }
     const size_t slot = dev < 0 ? 0 : size_t(dev);
-    std::lock_guard<std::mutex> g(t->plan_mu);
+    std::lock_guard<ddt::SpinMutex> g(t->plan_mu);
     if (t->plans.size() <= slot)
         t->plans.resize(slot + 1);
     if (t->plans[slot])
@@ -626,7 +639,9 @@ std::shared_ptr<Plan> get_plan(ddt_datatype *t)
 // Upload the index lists of a plan to HBM (first execution only).
 void ensure_device_lists(Plan &P)
 {
-    std::lock_guard<std::mutex> g(P.mu);
+    if (P.dev_ready.load(std::memory_order_acquire))
+        return;
+    std::lock_guard<SpinMutex> g(P.mu);
     if (P.dev_ready)
         return;
     for (size_t i = 0; i < P.leaves.size(); ++i) {
@@ -720,7 +735,7 @@ SortedList *sorted_build(Plan &P, hipStream_t stream)
         P.sorted_state = -1;
         return nullptr;
     }
-    std::lock_guard<std::mutex> g_(P.mu);
+    std::lock_guard<SpinMutex> g_(P.mu);
     if (P.sorted_state == 0) {
         // the build allocates and waits for its own stream: never while the caller's stream
         // captures (a graph captured before the first eager use keeps the per-block kernel)
@@ -810,7 +825,7 @@ int prebuild_device(ddt_datatype *t)
         return DDT_SUCCESS;   // no device here: the first move builds it
     }
     {
-        std::lock_guard<std::mutex> g(P->mu);
+        std::lock_guard<SpinMutex> g(P->mu);
         if (P->device < 0)
             P->device = dev;
         if (P->device != dev)

@@ -709,6 +709,12 @@ uint64_t snap_down_to_element(const ddt_datatype *t, uint64_t p)
 
 }  // namespace ddt
 
+uint64_t ddt_next_serial()
+{
+    static std::atomic<uint64_t> next{1};
+    return next.fetch_add(1, std::memory_order_relaxed);
+}
+
 // ================================================================ C ABI: construction
 namespace ddt {
 namespace {

@@ -17,6 +17,8 @@ for f in ddt_kernels ddt_sorted ddt_move_p0 ddt_move_p1 ddt_move_u0 ddt_move_u1;
     -c $f.hip -o build_asan/$f.o &
 done
 wait
+printf 'extern "C" const char *ddt_build_id(void) { return "%s"; }\n' "$(python3 ../../scripts/srcsha.py)" > build_asan/ddt_build_id.cpp
+g++ -O1 -fPIC -c build_asan/ddt_build_id.cpp -o build_asan/ddt_build_id.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Xarch_host -fsanitize=address \
   -o build_asan/libddt_hip_asan.so build_asan/*.o
 cd ../..

@@ -16,6 +16,11 @@
  *     shared  one datatype for all threads (one plan: the threads share its descriptor sets)
  *     sync    no ACCELERATOR_ASYNC: every call returns with the data in place (MPI_Pack's
  *             contract), so host time per call is the whole synchronous operation
+ *   [direct|bridge] [slots|noslots]   (bisection of the per-call path)
+ *     direct  the engine's own convertor ABI (ddt_convertor_prepare_* + pack / unpack on a
+ *             per-thread ddt_convertor_t and a per-type ddt_datatype_t imported once) instead of
+ *             the opal bridge's fAdvance
+ *     noslots ddt_tune("slots", 0): every launch carries its kernel arguments
  *     tiny    16 doubles at a 2 KiB stride (128 packed bytes) instead of the 512 KiB y face: the
  *             device time per call is the launch alone, so host scaling is not hidden behind the
  *             device's own throughput
@@ -91,8 +96,10 @@ static void prepare(opal_convertor_t *c, opal_datatype_t *dt, void *buf, int sen
 }
 
 typedef struct {
-    int id, iters, async;
+    int id, iters, async, direct;
     opal_datatype_t *dt;
+    ddt_datatype_t *edt;   /* direct: the engine's import of dt */
+    ddt_convertor_t *ec;
     void *grid, *packed;
     hipStream_t hs;
     opal_accelerator_stream_t sobj;
@@ -105,6 +112,23 @@ typedef struct {
 
 static int run_calls(worker *w, int n)
 {
+    if (w->direct) {
+        for (int i = 0; i < n; ++i) {
+            for (int dir = 0; dir < 2; ++dir) {
+                struct iovec iov = {w->packed, g_bytes};
+                uint32_t cnt = 1;
+                size_t md = 0;
+                int rc = dir == 0 ? ddt_convertor_prepare_for_send(w->ec, w->edt, 1, w->grid)
+                                  : ddt_convertor_prepare_for_recv(w->ec, w->edt, 1, w->grid);
+                if (rc != 0)
+                    return 4;
+                rc = dir == 0 ? ddt_convertor_pack(w->ec, &iov, &cnt, &md) : ddt_convertor_unpack(w->ec, &iov, &cnt, &md);
+                if (rc != 1 || md != g_bytes)
+                    return 5;
+            }
+        }
+        return 0;
+    }
     for (int i = 0; i < n; ++i) {
         for (int dir = 0; dir < 2; ++dir) {   /* pack, then unpack into the same field */
             opal_convertor_t c;
@@ -146,6 +170,9 @@ int main(int argc, char **argv)
     const int shared = argc > 2 && !strcmp(argv[2], "shared");
     const int async = !(argc > 3 && !strcmp(argv[3], "sync"));
     const int tiny = argc > 4 && !strcmp(argv[4], "tiny");
+    const int direct = argc > 5 && !strcmp(argv[5], "direct");
+    if (argc > 6 && !strcmp(argv[6], "noslots"))
+        (void) ddt_tune("slots", 0);
     if (tiny)
         g_bytes = 128;
     if (hipSetDevice(0) != hipSuccess)
@@ -168,6 +195,19 @@ int main(int argc, char **argv)
         memset(&w->sobj, 0, sizeof(w->sobj));
         w->sobj.stream = cell;
         w->dt = &types[shared ? 0 : t].dt;
+        w->direct = direct;
+        if (direct) {
+            const opal_datatype_t *d = w->dt;
+            if (shared && t > 0) {
+                w->edt = W[0].edt;
+            } else if (ddt_type_from_opal_desc(d->opt_desc.desc, d->opt_desc.used, d->size, d->lb, d->ub, d->true_lb,
+                                               d->true_ub, &w->edt) != 0) {
+                return 3;
+            }
+            w->ec = ddt_convertor_create();
+            if (!w->ec || ddt_convertor_set_stream(w->ec, w->hs, async) != 0)
+                return 3;
+        }
     }
     const int Ts[] = {1, 2, 4, 8};
     double base_rate = 0;
@@ -206,12 +246,13 @@ int main(int argc, char **argv)
             base_rate = rate;
         int64_t si[4] = {0, 0, 0, 0};
         (void) ddt_slot_info(si);
-        printf("{\"what\": \"bridge %s pack+unpack, %s, %s\", \"threads\": %d, \"bytes\": %zu, "
+        printf("{\"what\": \"%s %s pack+unpack, %s, %s%s\", \"threads\": %d, \"bytes\": %zu, "
                "\"calls_per_thread\": %d, \"host_us_per_call\": {\"mean\": %.3f, \"max\": %.3f}, "
                "\"device_us_per_op\": {\"mean\": %.3f, \"max\": %.3f}, \"aggregate_calls_per_s\": %.0f, "
                "\"speedup_vs_1\": %.3f, \"slots\": [%lld, %lld, %lld, %lld]}\n",
-               tiny ? "16 doubles at 2 KiB" : "y face", shared ? "one shared datatype" : "a datatype per thread",
-               async ? "ACCELERATOR_ASYNC" : "synchronous", T, g_bytes, 2 * iters, sumh / T, maxh, sumd / T, maxd, rate, rate / base_rate,
+               direct ? "engine ABI" : "bridge", tiny ? "16 doubles at 2 KiB" : "y face",
+               shared ? "one shared datatype" : "a datatype per thread", async ? "ACCELERATOR_ASYNC" : "synchronous",
+               argc > 6 && !strcmp(argv[6], "noslots") ? ", no launch slots" : "", T, g_bytes, 2 * iters, sumh / T, maxh, sumd / T, maxd, rate, rate / base_rate,
                (long long) si[0], (long long) si[1], (long long) si[2], (long long) si[3]);
         fflush(stdout);
     }

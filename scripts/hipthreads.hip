@@ -8,6 +8,8 @@
 //   mix     the HIP calls one asynchronous engine call makes around its argument-free launch:
 //           hipGetDevice x2, hipPointerGetAttributes x2 (user buffer, iovec), hipStreamIsCapturing,
 //           then the empty kernel without arguments
+//   cap / attr / dev   the empty kernel without arguments after ONE kind of those calls only:
+//           hipStreamIsCapturing, hipPointerGetAttributes x2, hipGetDevice x2
 // Not part of the library.
 #include <hip/hip_runtime.h>
 
@@ -55,11 +57,16 @@ static void calls(Worker *w, int n)
             int d = 0;
             hipPointerAttribute_t pa;
             hipStreamCaptureStatus cs;
-            (void) hipGetDevice(&d);
-            (void) hipPointerGetAttributes(&pa, w->a);
-            (void) hipPointerGetAttributes(&pa, w->b);
-            (void) hipGetDevice(&d);
-            (void) hipStreamIsCapturing(w->s, &cs);
+            if (w->kind == 3 || w->kind == 6)
+                (void) hipGetDevice(&d);
+            if (w->kind == 3 || w->kind == 5) {
+                (void) hipPointerGetAttributes(&pa, w->a);
+                (void) hipPointerGetAttributes(&pa, w->b);
+            }
+            if (w->kind == 3 || w->kind == 6)
+                (void) hipGetDevice(&d);
+            if (w->kind == 3 || w->kind == 4)
+                (void) hipStreamIsCapturing(w->s, &cs);
             hipLaunchKernelGGL(k_empty, dim3(32), dim3(256), 0, w->s);
         }
     }
@@ -92,9 +99,13 @@ int main(int argc, char **argv)
             || hipEventCreate(&W[t].e1) != hipSuccess)
             return 2;
     }
-    const char *names[4] = {"empty kernel, no arguments", "empty kernel, 36 B of arguments", "hipMemcpyAsync 512 KiB D2D",
-                            "the engine's HIP calls around an argument-free launch"};
-    for (int kind = 0; kind < 4; ++kind) {
+    const char *names[7] = {"empty kernel, no arguments", "empty kernel, 36 B of arguments", "hipMemcpyAsync 512 KiB D2D",
+                            "the engine's HIP calls around an argument-free launch",
+                            "hipStreamIsCapturing + argument-free launch", "hipPointerGetAttributes x2 + argument-free launch",
+                            "hipGetDevice x2 + argument-free launch"};
+    const int kmin = argc > 2 ? atoi(argv[2]) : 0;
+    const int kmax = argc > 3 ? atoi(argv[3]) : 7;
+    for (int kind = kmin; kind < kmax; ++kind) {
         double base = 0;
         for (int T : {1, 2, 4, 8}) {
             pthread_barrier_t bar;

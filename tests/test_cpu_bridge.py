@@ -274,3 +274,56 @@ def test_import_cache_under_concurrent_threads():
     for t in types:
         t.destruct()
     assert S.stats()["entries"] == 0
+
+
+def test_import_cache_under_threads_with_destructs():
+    """MPI_THREAD_MULTIPLE on the import cache (r6: per-bucket spin locks, per-thread pinned
+    entries): eight threads attach convertors of their own datatype and of one shared datatype
+    while a ninth destructs and re-creates types; every attach succeeds, and once the threads
+    are done and the cache finalized no entry is left and every lookup was counted as an import
+    or a hit."""
+    import threading
+    L = S.bridge_lib()
+    L.opal_hip_bridge_finalize()
+    base = S.stats()
+    shared = _xface()
+    own = [_xface(8 + i) for i in range(8)]
+    errors, calls = [], [0] * 8
+    stop = threading.Event()
+
+    def worker(i):
+        try:
+            for k in range(400):
+                t = shared if k % 2 else own[i]
+                rc = S.Convertor().prepare(t, 1 + k % 3, 0x7000_0000_0000, send=bool(k % 4 < 2))
+                if rc != S.OPAL_SUCCESS:
+                    errors.append((i, k, rc))
+                    return
+                calls[i] += 1
+        except Exception as ex:   # surface to the main thread
+            errors.append(repr(ex))
+
+    def churn():
+        while not stop.is_set():
+            t = _xface(5)
+            S.Convertor().prepare(t, 1, 0x7000_0000_0000, send=True)
+            t.destruct()
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(8)]
+    ch = threading.Thread(target=churn)
+    ch.start()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    stop.set()
+    ch.join(timeout=60)
+    assert not errors, errors
+    assert sum(calls) == 8 * 400
+    st = S.stats()
+    # each attach is one lookup: served by an import or a hit (shared or pinned)
+    assert (st["imports"] - base["imports"]) + (st["hits"] - base["hits"]) >= 8 * 400
+    for t in own + [shared]:
+        t.destruct()
+    L.opal_hip_bridge_finalize()
+    assert S.stats()["entries"] == 0
