@@ -1361,11 +1361,12 @@ def main():
 
     if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_faces and not split:
         # config 3's faces alone: dim0 / dim1 / dim2 of the 512^3 float grid,
-        # cold and clean over --face-fields fields (default 64 here: 32 GiB of fields), with
-        # each face's bare kernel under the same protocol
+        # cold and clean over --face-fields fields (at most 256 here: 128 GiB of fields, 256 MiB
+        # per plane face, so one launch is not dominated by the event and launch floor as it is
+        # at 64 fields), with each face's bare kernel under the same protocol
         user = packed = None
         torch.cuda.empty_cache()
-        ff = min(args.face_fields, 64)
+        ff = min(args.face_fields, 256)
         result["faces"] = face_throughput(dev, ff, max(5, min(args.steps, 20)),
                                           faces=("dim0", "dim1", "dim2"), grid="cfg3")
 

@@ -312,8 +312,13 @@ void pin_retired(Plan &P, const std::shared_ptr<ItemSet> &S)   // P.mu held
 void retire(Plan &P, const std::shared_ptr<ItemSet> &S)   // P.mu held
 {
     S->retired = true;
-    if (!S->d_items)
+    if (!S->d_items) {
+        // nothing on the device; a call that looked it up still holds a plain pointer to it
+        // until its launch is enqueued: the graveyard keeps the object until then
+        if (S->inflight)
+            P.graveyard.push_back(Retired{S, {}});
         return;
+    }
     if (S->pinned) {
         P.pinned.push_back(S);
         return;
@@ -417,9 +422,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                 uint8_t *pk = reinterpret_cast<uint8_t *>(wins[0].ptr + i * uint64_t(t->size));
                 // spol bits, plus the pass-2 quads (256) and the pass-1 stagger (bits 16..23)
                 const uint32_t pol = uint32_t(tuning().spol) | (tuning().s2vec ? 256u : 0u)
-                                     | (tuning().spipe ? 1024u : 0u)
                                      | (uint32_t(std::min<long>(tuning().sstagger, 255)) << 16);
-                SL->pipe_wgs = uint32_t(std::max<long>(tuning().spipe, 0)) > 1 ? uint32_t(tuning().spipe) : 0u;
                 HIPCHK(SL->run(u, pk, dir, pol, stream, uint32_t(tuning().sunroll),
                                uint32_t(tuning().s2unroll)));
             }
@@ -440,9 +443,17 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         {
             if (!S)
                 return;
+            // Not retired when the launch was already enqueued: a later retirement records its
+            // fences after this launch, so the hold ends without the plan lock.  Retired before
+            // the launch: the late event and the release are made under the lock, where reap
+            // cannot come between them.
+            if (!(by_pointer && S->retired.load())) {
+                S->inflight.fetch_sub(1);
+                return;
+            }
             std::lock_guard<SpinMutex> g(P.mu);
             --S->inflight;
-            if (by_pointer && S->retired && !S->pinned) {
+            if (!S->pinned) {
                 hipEvent_t e = nullptr;
                 if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess
                     && hipEventRecord(e, stream) == hipSuccess) {
@@ -474,7 +485,11 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
     // of its own, and threads sharing this plan must not queue behind it (r6 thread scaling)
     const bool cap = capturing(stream);
     Hold hold{P, nullptr, stream};
-    std::shared_ptr<ItemSet> S;
+    // S points into the plan's cache (or graveyard): `inflight` keeps the object alive until the
+    // launch is enqueued (retire parks a held set in the graveyard), so no shared_ptr copy --
+    // an atomic on a line every thread of a shared datatype writes -- is taken per call
+    ItemSet *S = nullptr;
+    const std::shared_ptr<ItemSet> *owner = nullptr;   // valid inside the plan lock only
     // The launch decision for set S (plan lock held): by pointer or inline, capture pinning, the
     // launch slot.  A cache hit makes it in the same critical section as its lookup: threads
     // sharing a datatype take the plan lock twice per call (here and in Hold), not four times,
@@ -501,7 +516,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         if (cap) {
             // the graph keeps this pointer: never recycle it before the plan goes
             if (S->retired && !S->pinned)
-                pin_retired(P, S);
+                pin_retired(P, *owner);
             S->pinned = true;
         } else if (tuning().slots && grid_cap == 0 && !S->all_dense && !S->has_lists && !S->retired
                    && S->bytes <= uint64_t(tuning().slot_max_kb) << 10) {
@@ -582,19 +597,26 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         std::lock_guard<SpinMutex> g(P.mu);
         for (size_t i = 0; i < P.cache.size(); ++i) {
             if (P.cache[i]->key == key) {
-                S = P.cache[i];
-                ++S->inflight;   // held until this call has enqueued its launch (Hold)
-                hold.S = S.get();
-                if (i)
+                // least recently used order, but the two most recent sets (a pack and an unpack
+                // alternating) are not swapped on every call
+                if (i >= 2) {
                     std::rotate(P.cache.begin(), P.cache.begin() + long(i), P.cache.begin() + long(i) + 1);
+                    i = 0;
+                }
+                owner = &P.cache[i];
+                S = owner->get();
+                ++S->inflight;   // held until this call has enqueued its launch (Hold)
+                hold.S = S;
                 if (!maybe_direct())
                     decide();
                 break;
             }
         }
     }
+    std::shared_ptr<ItemSet> fresh;
     if (!S) {
-        S = std::make_shared<ItemSet>();
+        fresh = std::make_shared<ItemSet>();
+        S = fresh.get();
         S->key = key;
         try {
             for (const Window &w : wins)
@@ -636,12 +658,13 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
         }
         std::lock_guard<SpinMutex> g(P.mu);
         ++S->inflight;
-        hold.S = S.get();
-        P.cache.insert(P.cache.begin(), S);
+        hold.S = S;
+        P.cache.insert(P.cache.begin(), fresh);
         if (P.cache.size() > kCacheEntries) {
             retire(P, P.cache.back());
             P.cache.pop_back();
         }
+        owner = &P.cache[0];
         if (!maybe_direct())
             decide();
     }
@@ -655,6 +678,18 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
             return DDT_SUCCESS;
         }
         std::lock_guard<SpinMutex> g(P.mu);   // declined: the ordinary decision
+        owner = nullptr;
+        for (const auto &sp : P.cache)
+            if (sp.get() == S)
+                owner = &sp;
+        for (const Retired &r : P.graveyard)
+            if (!owner && r.set.get() == S)
+                owner = &r.set;
+        for (const auto &sp : P.pinned)
+            if (!owner && sp.get() == S)
+                owner = &sp;
+        if (!owner)   // a held set is always in one of them (retire parks it)
+            return fail(DDT_ERROR, "descriptor set lost while held");
         decide();
     }
     if (!d_items && S->has_lists)
@@ -1966,8 +2001,6 @@ int ddt_tune(const char *key, long value)
         tuning().sigspin_us = value < 0 ? 0 : value;
     else if (k == "s2vec")
         tuning().s2vec = value ? 1 : 0;
-    else if (k == "spipe")
-        tuning().spipe = value < 0 ? 0 : (value > 4096 ? 4096 : value);
     else if (k == "sskew")
         tuning().sskew = value < 0 ? 0 : (value > (1 << 20) ? (1 << 20) : value);
     else if (k == "sstagger")

@@ -159,8 +159,8 @@ struct ItemSet {
     // A launch by pointer is enqueued outside the plan lock: `inflight` counts launches
     // between taking d_items and enqueuing them, and a launch that finds the set evicted
     // meanwhile records a `late` event behind itself for the retirement to wait on too.
-    uint32_t inflight = 0;
-    bool retired = false;
+    std::atomic<uint32_t> inflight{0};   // raised under the plan lock; lowered without it unless retired
+    std::atomic<bool> retired{false};
     std::vector<hipEvent_t> late;
     ItemBlock blk{};
     // argument-free launches (run_windows): up to kSetBind launch-slot bindings, each for one

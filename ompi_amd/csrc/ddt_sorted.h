@@ -20,7 +20,6 @@ struct SortedList {
     uint32_t segb = 64;      // segment bytes: 64 or 128
     bool unpadded = false;   // runs packed end to end in U (segb = the lanes per run only)
     uint32_t nc = 0, nb = 0; // chunks, buckets
-    uint32_t pipe_wgs = 0;   // pipelined pack pass 1: persistent workgroups (0: 256, one per CU)
     uint32_t skew = 0;       // U slots between consecutive buckets (r6: buckets of exactly RG slots
                              // start 128 KiB apart, so one chunk's runs all fell on one DRAM
                              // channel; `ddt_tune sskew` bytes, read at build)

@@ -80,10 +80,6 @@ constexpr uint32_t POL_VEC2 = 256;
 // timing only (wrong results): LDS writes of the permutations go to conflict-free addresses
 // (pass 1: the element's own index, pass 2: its U slot), to price the bank conflicts
 constexpr uint32_t POL_NOCONF = 512;
-// pack pass 1 as a persistent, software-pipelined kernel (round 6): each workgroup walks several
-// chunks and issues the first register batch of its NEXT chunk's gather before it emits the
-// current chunk's runs, so the gather's loads are in flight during the emission
-constexpr uint32_t POL_PIPE = 1024;
 // bits 16..23: pass 1 / 1' start stagger (round 6 A/B): the first wave of workgroups (one per CU)
 // sleeps ((blockIdx / 8) % 4) x this many s_sleep(127) periods, so the CUs' gather and emission
 // phases do not run in lockstep
@@ -353,77 +349,6 @@ __global__ __launch_bounds__(PT / CDIV) void k_pack1(const uint8_t *__restrict__
     }
     __syncthreads();
     emit_runs<E, SEGB, NT>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, nts, pol & POL_UNPADDED);
-}
-
-// pack pass 1, pipelined (POL_PIPE): a persistent workgroup handles virtual blocks w, w + G,
-// w + 2G, ... (G a multiple of 8: every block of a workgroup maps to one XCD's slab through
-// chunk_of, as the one-chunk-per-workgroup form does).  Per chunk: the first batch of K elements
-// per thread was loaded into registers during the previous chunk's emission; it goes to LDS,
-// the rest of the chunk is gathered, and the next chunk's first batch is issued before this
-// chunk's runs are emitted.
-template <int E, int K>
-__device__ __forceinline__ void gather_batch(const typename Elem<E>::T *src, const AddrList &al,
-                                             const uint16_t *__restrict__ SL, uint32_t j0, uint32_t m, uint32_t t0,
-                                             bool ntl, bool ntu, typename Elem<E>::T (&v)[K], uint32_t (&sl)[K])
-{
-#pragma unroll
-    for (int q = 0; q < K; ++q) {
-        const uint32_t t = t0 + q * PT;
-        if (t < m) {
-            sl[q] = ldp(&SL[j0 + t], ntl);
-            v[q] = ldp(&src[addr_at(al, j0 + t, ntl)], ntu);
-        }
-    }
-}
-
-template <int E, int SEGB, int K>
-__global__ __launch_bounds__(PT) void k_pack1p(const uint8_t *__restrict__ user, const AddrList al,
-                                               const uint16_t *__restrict__ SL, const uint16_t *__restrict__ off16,
-                                               const uint32_t *__restrict__ ub, uint8_t *__restrict__ U, uint32_t n,
-                                               uint32_t nb, uint32_t nc, uint32_t pol)
-{
-    using T = typename Elem<E>::T;
-    constexpr uint32_t CH = LDS_BYTES / E, SEG = SEGB / E;
-    const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS, ntu = pol & POL_USER_NTL;
-    __shared__ T lds[CH + SEG];
-    __shared__ uint16_t toff[MAXNB + 1];
-    __shared__ uint32_t tub[MAXNB];
-    const T *src = reinterpret_cast<const T *>(user);
-    const uint32_t G = gridDim.x;
-    T v[K];
-    uint32_t sl[K];
-    uint32_t b = blockIdx.x;
-    uint32_t c = chunk_of(b, nc, pol), j0 = c * CH, m = min(CH, n - j0);
-    gather_batch<E, K>(src, al, SL, j0, m, threadIdx.x, ntl, ntu, v, sl);
-    bool emit = false;
-    for (;;) {
-        if (emit)   // the previous chunk's runs, while this chunk's first batch is in flight
-            emit_runs<E, SEGB, PT>(lds, toff, tub, U, nb, nts, pol & POL_UNPADDED);
-        __syncthreads();
-        if (b >= nc)
-            break;
-        stage_tables<PT>(off16, ub, c, nb, m, toff, tub);
-#pragma unroll
-        for (int q = 0; q < K; ++q)
-            if (threadIdx.x + q * PT < m)
-                lds[sl[q]] = v[q];
-        for (uint32_t t0 = threadIdx.x + PT * K; t0 < m; t0 += PT * K) {
-            gather_batch<E, K>(src, al, SL, j0, m, t0, ntl, ntu, v, sl);
-#pragma unroll
-            for (int q = 0; q < K; ++q)
-                if (t0 + q * PT < m)
-                    lds[sl[q]] = v[q];
-        }
-        __syncthreads();
-        emit = true;
-        b += G;
-        if (b < nc) {
-            c = chunk_of(b, nc, pol);
-            j0 = c * CH;
-            m = min(CH, n - j0);
-            gather_batch<E, K>(src, al, SL, j0, m, threadIdx.x, ntl, ntu, v, sl);
-        }
-    }
 }
 
 // pack pass 2: the bucket's runs scatter into LDS by destination, then stream out
@@ -928,18 +853,12 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol
             return e;
     }
     const dim3 gc(nc), gb(nb), blk(PT), blk1(PT / cdiv);
-    // the pipelined pack pass 1: one persistent workgroup per CU (pipe_wgs, a multiple of 8 so a
-    // workgroup's blocks stay on one XCD slab), at most one per chunk
-    const uint32_t pw = pipe_wgs ? pipe_wgs : 256;
-    const dim3 gp(nc >= 8 ? std::min<uint32_t>(nc, pw) & ~7u : nc);
     const AddrList al{A, A16, Abase};
     uint8_t *u8 = static_cast<uint8_t *>(U);
     if (unpadded)   // r5 A/B (profiles/r5_ab_cfg4_unpadded.jsonl): the slabs pay only without padding
         pol |= POL_UNPADDED | POL_XCD_SLAB;
 #define DDT_SORTED_PASS1(E, SB, K, CD)                                                                          \
-    if (dir == 0 && CD == 1 && (pol & POL_PIPE))                                                               \
-        hipLaunchKernelGGL((k_pack1p<E, SB, K>), gp, blk, 0, stream, user, al, SL, off16, ub, u8, n, nb, nc, pol); \
-    else if (dir == 0)                                                                                          \
+    if (dir == 0)                                                                                               \
         hipLaunchKernelGGL((k_pack1<E, SB, K, CD>), gc, blk1, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol); \
     else                                                                                                        \
         hipLaunchKernelGGL((k_unpack1<E, SB, 4, CD>), gc, blk1, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol);
