@@ -422,7 +422,6 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                 uint8_t *pk = reinterpret_cast<uint8_t *>(wins[0].ptr + i * uint64_t(t->size));
                 // spol bits, plus the pass-2 quads (256) and the pass-1 stagger (bits 16..23)
                 const uint32_t pol = uint32_t(tuning().spol) | (tuning().s2vec ? 256u : 0u)
-                                     | (tuning().sprefetch ? 2048u : 0u)
                                      | (uint32_t(std::min<long>(tuning().sstagger, 255)) << 16);
                 HIPCHK(SL->run(u, pk, dir, pol, stream, uint32_t(tuning().sunroll),
                                uint32_t(tuning().s2unroll)));
@@ -2002,8 +2001,6 @@ int ddt_tune(const char *key, long value)
         tuning().sigspin_us = value < 0 ? 0 : value;
     else if (k == "s2vec")
         tuning().s2vec = value ? 1 : 0;
-    else if (k == "sprefetch")
-        tuning().sprefetch = value ? 1 : 0;
     else if (k == "sskew")
         tuning().sskew = value < 0 ? 0 : (value > (1 << 20) ? (1 << 20) : value);
     else if (k == "sstagger")

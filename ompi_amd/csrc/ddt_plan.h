@@ -51,7 +51,6 @@ struct Tuning {
     long s2vec = 1;       // address-ordered engine, 4-byte elements: pass 2 / 2' four slots per lane (r6)
     long sskew = 4160;    // address-ordered engine: bytes of U between buckets, read at build (r6:
                           // 128 KiB-apart buckets camped on one DRAM channel; cfg4 pack 620 -> 585 us)
-    long sprefetch = 0;   // address-ordered engine: unpack pass 1' reads its chunk's user span first (r6 A/B)
     long sstagger = 0;    // address-ordered engine: pass 1 / 1' first-wave stagger, s_sleep(127) units (r6 A/B)
     long sseg = 1;        // address-ordered engine: U run padding, read at plan build: 1 = none (runs end
                           // to end, pass-1 chunks in XCD slabs; r5) or whole 32/64/128-byte segments

@@ -77,10 +77,6 @@ constexpr uint32_t POL_XCD_SLAB = 128;
 // pass 2 / 2' of 4-byte elements move four U slots per lane (one 16-byte U load or store, one
 // 8-byte upos load; round 6) and the packed side as 16-byte words when it is 16-byte aligned
 constexpr uint32_t POL_VEC2 = 256;
-// unpack pass 1': read the chunk's whole user span (16-byte loads, plain) before its scatter, so
-// the scatter's partial-line writes find their lines cached and merge there instead of being
-// completed by a read-modify-write below the L2 (r6 A/B)
-constexpr uint32_t POL_PREFETCH = 2048;
 // timing only (wrong results): LDS writes of the permutations go to conflict-free addresses
 // (pass 1: the element's own index, pass 2: its U slot), to price the bank conflicts
 constexpr uint32_t POL_NOCONF = 512;
@@ -628,19 +624,6 @@ __global__ __launch_bounds__(PT / CDIV) void k_unpack1(uint8_t *__restrict__ use
     const uint32_t c = chunk_of(blockIdx.x, gridDim.x, pol), j0 = c * CH;
     const uint32_t m = min(CH, n - j0);
     stage_tables<NT>(off16, ub, c, nb, m, toff, tub);
-    if ((pol & POL_PREFETCH) && m) {
-        // whole aligned 16-byte blocks holding the first to the last element: a block never
-        // crosses a page, so no byte outside the pages the elements live on is read
-        const uintptr_t lo = (reinterpret_cast<uintptr_t>(user) + uint64_t(addr_at(al, j0, false)) * E) & ~uintptr_t(15);
-        const uintptr_t hi = reinterpret_cast<uintptr_t>(user) + (uint64_t(addr_at(al, j0 + m - 1, false)) + 1) * E;
-        const u32x4 *p = reinterpret_cast<const u32x4 *>(lo);
-        const uint64_t nq = (hi - lo + 15) >> 4;
-        uint32_t acc = 0;
-#pragma unroll 8
-        for (uint64_t q = threadIdx.x; q < nq; q += NT)
-            acc ^= p[q].x;
-        asm volatile("" ::"v"(acc));   // the loads are the point: keep them
-    }
     __syncthreads();
     load_runs<E, SEGB, NT>(lds, toff, tub, U, (pol & POL_SKIP_RUNS) ? 0u : nb, ntl);
     __syncthreads();

@@ -1002,30 +1002,6 @@ def test_sorted_list_engine_quads(device, sorted_from, count, density, schunk, s
         L.ddt_tune(b"reset", 0)
 
 
-@pytest.mark.parametrize("shift", [0, 4, 12])
-@pytest.mark.parametrize("esz,density", [(4, 4), (8, 3), (16, 2)])
-def test_sorted_list_engine_span_prefetch(device, sorted_from, esz, density, shift):
-    """Unpack pass 1' reading its chunk's whole user span before the scatter (ddt_tune
-    sprefetch 1): the reads cover whole aligned 16-byte blocks from the first to the last
-    element of a chunk, also when the list's base is not 16-byte aligned; bit-exact both ways."""
-    import ompi_amd
-    L = ompi_amd.lib()
-    sorted_from(1)
-    L.ddt_tune(b"sprefetch", 1)
-    try:
-        rng = np.random.default_rng(9700 + esz * 10 + density + shift)
-        ch = (128 << 10) // esz
-        n = 2 * ch + 311
-        unit = {4: ("basic", 15), 8: ("basic", 16), 16: ("basic", 16)}[esz]
-        per = esz // (8 if esz == 16 else esz)
-        disps = (rng.permutation(density * n)[:n] * per).astype(np.int64)
-        b = R.Built(("indexed_block", per, disps.tolist(), unit))
-        _roundtrip(b, 1, device, 23 + esz, shift=shift)
-        assert b.engine().engine_info()["sorted"] == 1
-    finally:
-        L.ddt_tune(b"reset", 0)
-
-
 @pytest.mark.parametrize("name", ["contig16", "adv_mixed_promote", "one_contig_instance"])
 def test_no_op_types_fill_fragments_to_the_byte(device, name):
     """A convertor the reference marks NO_OP (OPAL_CONVERTOR_PREPARE, opal_convertor.c:
