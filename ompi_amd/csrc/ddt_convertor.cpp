@@ -422,6 +422,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
                 uint8_t *pk = reinterpret_cast<uint8_t *>(wins[0].ptr + i * uint64_t(t->size));
                 // spol bits, plus the pass-2 quads (256) and the pass-1 stagger (bits 16..23)
                 const uint32_t pol = uint32_t(tuning().spol) | (tuning().s2vec ? 256u : 0u)
+                                     | (uint32_t(tuning().slayout & 3) << 10)
                                      | (uint32_t(std::min<long>(tuning().sstagger, 255)) << 16);
                 HIPCHK(SL->run(u, pk, dir, pol, stream, uint32_t(tuning().sunroll),
                                uint32_t(tuning().s2unroll)));
@@ -1999,6 +2000,8 @@ int ddt_tune(const char *key, long value)
         tuning().sigsync = value ? 1 : 0;
     else if (k == "sigspin_us")
         tuning().sigspin_us = value < 0 ? 0 : value;
+    else if (k == "slayout")
+        tuning().slayout = value & 3;
     else if (k == "s2vec")
         tuning().s2vec = value ? 1 : 0;
     else if (k == "sskew")
@@ -2006,7 +2009,7 @@ int ddt_tune(const char *key, long value)
     else if (k == "sstagger")
         tuning().sstagger = value < 0 ? 0 : (value > 255 ? 255 : value);
     else if (k == "sunroll")
-        tuning().sunroll = value >= 16 ? 16 : (value >= 8 ? 8 : 4);
+        tuning().sunroll = value >= 32 ? 32 : (value >= 16 ? 16 : (value >= 8 ? 8 : 4));
     else if (k == "sseg")
         tuning().sseg = (value == 128 || value == 64 || value == 32) ? value : 1;
     else if (k == "schunk")

@@ -51,6 +51,8 @@ struct Tuning {
     long s2vec = 1;       // address-ordered engine, 4-byte elements: pass 2 / 2' four slots per lane (r6)
     long sskew = 4160;    // address-ordered engine: bytes of U between buckets, read at build (r6:
                           // 128 KiB-apart buckets camped on one DRAM channel; cfg4 pack 620 -> 585 us)
+    long slayout = 1;     // address-ordered engine: chunk-major U for the pack (1) / the unpack (2) (r6:
+                          // cfg4 pack 586 -> 514 us; the unpack's scattered run writes lose, 737 -> 871+)
     long sstagger = 0;    // address-ordered engine: pass 1 / 1' first-wave stagger, s_sleep(127) units (r6 A/B)
     long sseg = 1;        // address-ordered engine: U run padding, read at plan build: 1 = none (runs end
                           // to end, pass-1 chunks in XCD slabs; r5) or whole 32/64/128-byte segments

@@ -23,6 +23,7 @@ struct SortedList {
     uint32_t skew = 0;       // U slots between consecutive buckets (r6: buckets of exactly RG slots
                              // start 128 KiB apart, so one chunk's runs all fell on one DRAM
                              // channel; `ddt_tune sskew` bytes, read at build)
+    uint32_t cst = 0;        // chunk-major U: elements from one chunk image to the next (ch + skew)
     uint64_t slots = 0;      // U slots, runs padded to whole segments
     uint64_t dev_bytes = 0;  // device bytes held (tables + U)
     uint32_t *A = nullptr;       // [n] element offset (units of esz) of the j-th block in address order
@@ -36,6 +37,12 @@ struct SortedList {
     uint32_t *bstart = nullptr;  // [nb + 1] first U slot of bucket k (k skews in); bucket k ends
                                  // at bstart[k + 1] - skew
     uint16_t *upos = nullptr;    // [slots] position inside its bucket, 0xFFFF = padding
+    // chunk-major U (r6, `ddt_tune slayout`): a direction may keep U as the chunk images end to
+    // end instead, so pass 1 / 1' streams its image and pass 2 / 2' reads / writes the runs
+    // scattered; per bucket, the runs' U element offsets and their first slots within the bucket
+    uint32_t *physT = nullptr;   // [nb][nc] c * cst + off(c, k)   (unpadded plans with nc <= 4096)
+    uint16_t *vrelT = nullptr;   // [nb][nc] first slot of run (c, k) inside bucket k
+                                 // in aligned quads, run by run)
     void *U = nullptr;           // [slots] scratch elements
     hipEvent_t done = nullptr;   // recorded after every run (U reuse across streams)
     hipStream_t last_stream = nullptr;

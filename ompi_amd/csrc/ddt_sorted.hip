@@ -80,6 +80,15 @@ constexpr uint32_t POL_VEC2 = 256;
 // timing only (wrong results): LDS writes of the permutations go to conflict-free addresses
 // (pass 1: the element's own index, pass 2: its U slot), to price the bank conflicts
 constexpr uint32_t POL_NOCONF = 512;
+// chunk-major U for the pack (1024) / the unpack (2048) (r6): pass 1 / 1' stream the chunk image
+// to / from U[c * CH ..], pass 2 / 2' move the bucket's runs from / to their places in the images;
+// the scattered accesses are then the pack's reads and the unpack's writes of pass 2 / 2'
+constexpr uint32_t POL_CMAJ_PACK = 1024;
+constexpr uint32_t POL_CMAJ_UNPACK = 2048;
+// pass 2 / 2' of a chunk-major direction: buckets dealt to the XCDs in slabs (neighbouring
+// buckets' runs share lines in every chunk image; set by run(), r6 A/B: pack 546 -> 519 us,
+// chunk-major unpack 920 -> 871 us)
+constexpr uint32_t POL_P2_SLAB = 4096;
 // bits 16..23: pass 1 / 1' start stagger (round 6 A/B): the first wave of workgroups (one per CU)
 // sleeps ((blockIdx / 8) % 4) x this many s_sleep(127) periods, so the CUs' gather and emission
 // phases do not run in lockstep
@@ -251,6 +260,19 @@ __global__ __launch_bounds__(BT) void k_run_bases(const uint32_t *__restrict__ u
     }
     if (blockIdx.x == 0 && threadIdx.x == 0)
         bstart[nb] = total + nb * skew;
+}
+
+// bucket-major run tables of the chunk-major layout
+__global__ __launch_bounds__(BT) void k_cmaj_tables(const uint16_t *__restrict__ off16, const uint32_t *__restrict__ ubT,
+                                                    uint32_t nc, uint32_t nb, uint32_t cst, uint32_t *__restrict__ physT,
+                                                    uint16_t *__restrict__ vrelT)
+{
+    const size_t n = size_t(nc) * nb;
+    for (size_t x = size_t(blockIdx.x) * BT + threadIdx.x; x < n; x += size_t(gridDim.x) * BT) {
+        const uint32_t k = uint32_t(x / nc), c = uint32_t(x % nc);
+        physT[x] = c * cst + off16[size_t(c) * nb + k];
+        vrelT[x] = uint16_t(ubT[x] - ubT[size_t(k) * nc]);
+    }
 }
 
 __global__ __launch_bounds__(BT) void k_assign(const int32_t *__restrict__ disp, uint32_t n, uint32_t shift,
@@ -651,6 +673,266 @@ __global__ __launch_bounds__(PT / CDIV) void k_unpack1(uint8_t *__restrict__ use
     }
 }
 
+
+// ------------------------------------------------------------------ chunk-major U (r6)
+constexpr uint32_t MAXNC = 4096;
+
+// pass 1 of a chunk-major pack: the address-ordered gather into the LDS image, then the image
+// out to U[c * CH ..] as one stream
+template <int E, int K>
+__global__ __launch_bounds__(PT) void k_pack1c(const uint8_t *__restrict__ user, const AddrList al,
+                                               const uint16_t *__restrict__ SL, uint8_t *__restrict__ U, uint32_t n,
+                                               uint32_t cst, uint32_t pol)
+{
+    using T = typename Elem<E>::T;
+    constexpr uint32_t CH = LDS_BYTES / E;
+    const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS, ntu = pol & POL_USER_NTL;
+    __shared__ T lds[CH];
+    const uint32_t c = blockIdx.x, j0 = c * CH;
+    const uint32_t m = min(CH, n - j0);
+    const T *src = reinterpret_cast<const T *>(user);
+    const uint32_t mg = (pol & POL_SKIP_USER) ? 0u : m;
+    for (uint32_t t0 = threadIdx.x; t0 < mg; t0 += PT * K) {
+        T v[K];
+        uint32_t s[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const uint32_t t = t0 + q * PT;
+            if (t < m) {
+                s[q] = ldp(&SL[j0 + t], ntl);
+                v[q] = ldp(&src[addr_at(al, j0 + t, ntl)], ntu);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            if (t0 + q * PT < m)
+                lds[s[q]] = v[q];
+    }
+    __syncthreads();
+    if (pol & POL_SKIP_RUNS)
+        return;
+    // the image is CH * E = 128 KiB at a 128 KiB-aligned offset of U: whole 16-byte words
+    const uint32_t mq = m * E / 16;
+    u32x4 *dst = reinterpret_cast<u32x4 *>(U + size_t(c) * cst * E);
+    const u32x4 *l4 = reinterpret_cast<const u32x4 *>(lds);
+    for (uint32_t t = threadIdx.x; t < mq; t += PT)
+        stp(&dst[t], l4[t], nts);
+    T *dt = reinterpret_cast<T *>(U) + size_t(c) * cst;
+    for (uint32_t t = mq * 16 / E + threadIdx.x; t < m; t += PT)
+        dt[t] = lds[t];
+}
+
+// unpack pass 1' of the chunk-major layout: the image in from U[c * CH ..] as one stream, then
+// scattered to the user side in address order
+template <int E, int K>
+__global__ __launch_bounds__(PT) void k_unpack1c(uint8_t *__restrict__ user, const AddrList al,
+                                                 const uint16_t *__restrict__ SL, const uint8_t *__restrict__ U,
+                                                 uint32_t n, uint32_t cst, uint32_t pol)
+{
+    using T = typename Elem<E>::T;
+    constexpr uint32_t CH = LDS_BYTES / E;
+    const bool ntl = pol & POL_STREAM_NTL, wt = pol & POL_USER_WT;
+    __shared__ T lds[CH];
+    const uint32_t c = blockIdx.x, j0 = c * CH;
+    const uint32_t m = min(CH, n - j0);
+    if (!(pol & POL_SKIP_RUNS)) {
+        const uint32_t mq = m * E / 16;
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(U + size_t(c) * cst * E);
+        u32x4 *l4 = reinterpret_cast<u32x4 *>(lds);
+        for (uint32_t t0 = threadIdx.x; t0 < mq; t0 += PT * 8) {
+            u32x4 v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (t0 + q * PT < mq)
+                    v[q] = ldp(&src[t0 + q * PT], ntl);
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (t0 + q * PT < mq)
+                    l4[t0 + q * PT] = v[q];
+        }
+        const T *st = reinterpret_cast<const T *>(U) + size_t(c) * cst;
+        for (uint32_t t = mq * 16 / E + threadIdx.x; t < m; t += PT)
+            lds[t] = st[t];
+    }
+    __syncthreads();
+    T *dst = reinterpret_cast<T *>(user);
+    const uint32_t ms = (pol & POL_SKIP_USER) ? 0u : m;
+    for (uint32_t t0 = threadIdx.x; t0 < ms; t0 += PT * K) {
+        uint32_t a[K];
+        T v[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const uint32_t t = t0 + q * PT;
+            if (t < m) {
+                a[q] = addr_at(al, j0 + t, ntl);
+                v[q] = lds[ldp(&SL[j0 + t], ntl)];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            if (t0 + q * PT < m) {
+                if (wt)
+                    st_sc1(&dst[a[q]], v[q]);
+                else
+                    dst[a[q]] = v[q];
+            }
+    }
+}
+
+// the bucket's run table (U element offset, first slot inside the bucket) staged in LDS
+__device__ __forceinline__ void stage_cmaj(const uint32_t *__restrict__ physT, const uint16_t *__restrict__ vrelT,
+                                           uint32_t k, uint32_t nc, uint32_t m, uint32_t *tph, uint16_t *tv)
+{
+    for (uint32_t c = threadIdx.x; c < nc; c += PT) {
+        tph[c] = physT[size_t(k) * nc + c];
+        tv[c] = vrelT[size_t(k) * nc + c];
+    }
+    if (threadIdx.x == 0)
+        tv[nc] = uint16_t(m);   // m <= RG <= 32 Ki
+}
+
+// pack pass 2 of the chunk-major layout: the bucket's runs from the chunk images into LDS by
+// destination (SEG lanes per run, B runs per round in flight), then streamed out
+template <int E, int B, int NPF>
+__global__ __launch_bounds__(PT) void k_pack2c(const uint8_t *__restrict__ U, const uint16_t *__restrict__ upos,
+                                               const uint32_t *__restrict__ bstart, const uint32_t *__restrict__ physT,
+                                               const uint16_t *__restrict__ vrelT, uint8_t *__restrict__ packed,
+                                               uint32_t n, uint32_t nc, uint32_t pol)
+{
+    using T = typename Elem<E>::T;
+    constexpr uint32_t RG = LDS_BYTES / E, SEG = 64 / E, NSUB = PT / SEG;
+    const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS;
+    __shared__ T lds[RG];
+    __shared__ uint32_t tph[MAXNC];
+    __shared__ uint16_t tv[MAXNC + 1];
+    const uint32_t k = chunk_of(blockIdx.x, gridDim.x, (pol & POL_P2_SLAB) ? POL_XCD_SLAB : 0u);
+    const uint32_t m = min(RG, n - k * RG);
+    stage_cmaj(physT, vrelT, k, nc, m, tph, tv);
+    __syncthreads();
+    const T *src = reinterpret_cast<const T *>(U);
+    const uint16_t *up = upos + bstart[k];
+    const uint32_t sub = threadIdx.x / SEG, lane = threadIdx.x % SEG;
+    const uint32_t ncr = (pol & POL_SKIP_RUNS) ? 0u : nc;
+    for (uint32_t cb = sub; cb < ncr; cb += NSUB * B) {
+        T v[B][NPF];
+        uint16_t p[B][NPF];
+        uint32_t o[B], cn[B], ph[B];
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+            const uint32_t c = cb + uint32_t(i) * NSUB;
+            cn[i] = 0;
+            if (c < nc) {
+                o[i] = tv[c];
+                cn[i] = tv[c + 1] - o[i];
+                ph[i] = tph[c];
+#pragma unroll
+                for (int f = 0; f < NPF; ++f)
+                    if (lane + f * SEG < cn[i]) {
+                        v[i][f] = ldp(&src[ph[i] + lane + f * SEG], ntl);
+                        p[i][f] = ldp(&up[o[i] + lane + f * SEG], ntl);
+                    }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+#pragma unroll
+            for (int f = 0; f < NPF; ++f)
+                if (lane + f * SEG < cn[i])
+                    lds[p[i][f]] = v[i][f];
+        }
+#pragma unroll
+        for (int i = 0; i < B; ++i)
+            for (uint32_t q = lane + NPF * SEG; q < cn[i]; q += SEG)
+                lds[up[o[i] + q]] = src[ph[i] + q];
+    }
+    __syncthreads();
+    uint8_t *dst8 = packed + size_t(k) * RG * E;
+    if ((reinterpret_cast<uintptr_t>(dst8) & 15) == 0) {
+        u32x4 *dst = reinterpret_cast<u32x4 *>(dst8);
+        const u32x4 *l4 = reinterpret_cast<const u32x4 *>(lds);
+        const uint32_t mq = m * E / 16;
+        for (uint32_t t = threadIdx.x; t < mq; t += PT)
+            stp(&dst[t], l4[t], nts);
+        for (uint32_t t = mq * 16 / E + threadIdx.x; t < m; t += PT)
+            reinterpret_cast<T *>(dst8)[t] = lds[t];
+    } else {
+        T *dst = reinterpret_cast<T *>(dst8);
+        for (uint32_t t = threadIdx.x; t < m; t += PT)
+            stp(&dst[t], lds[t], nts);
+    }
+}
+
+// unpack pass 2' of the chunk-major layout: the bucket's packed elements into LDS, then out to
+// their runs' places in the chunk images
+template <int E>
+__global__ __launch_bounds__(PT) void k_unpack2c(const uint8_t *__restrict__ packed, const uint16_t *__restrict__ upos,
+                                                 const uint32_t *__restrict__ bstart, const uint32_t *__restrict__ physT,
+                                                 const uint16_t *__restrict__ vrelT, uint8_t *__restrict__ U,
+                                                 uint32_t n, uint32_t nc, uint32_t pol)
+{
+    using T = typename Elem<E>::T;
+    constexpr uint32_t RG = LDS_BYTES / E, SEG = 64 / E, NSUB = PT / SEG;
+    constexpr int B = 8;
+    const bool ntl = pol & POL_STREAM_NTL, nts = pol & POL_STREAM_NTS;
+    __shared__ T lds[RG];
+    __shared__ uint32_t tph[MAXNC];
+    __shared__ uint16_t tv[MAXNC + 1];
+    const uint32_t k = chunk_of(blockIdx.x, gridDim.x, (pol & POL_P2_SLAB) ? POL_XCD_SLAB : 0u);
+    const uint32_t m = min(RG, n - k * RG);
+    stage_cmaj(physT, vrelT, k, nc, m, tph, tv);
+    const uint8_t *src8 = packed + size_t(k) * RG * E;
+    if ((reinterpret_cast<uintptr_t>(src8) & 15) == 0) {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(src8);
+        u32x4 *l4 = reinterpret_cast<u32x4 *>(lds);
+        const uint32_t mq = m * E / 16;
+        for (uint32_t t0 = threadIdx.x; t0 < mq; t0 += PT * 2) {
+            u32x4 v[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                if (t0 + q * PT < mq)
+                    v[q] = ldp(&src[t0 + q * PT], ntl);
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                if (t0 + q * PT < mq)
+                    l4[t0 + q * PT] = v[q];
+        }
+        for (uint32_t t = mq * 16 / E + threadIdx.x; t < m; t += PT)
+            lds[t] = reinterpret_cast<const T *>(src8)[t];
+    } else {
+        const T *src = reinterpret_cast<const T *>(src8);
+        for (uint32_t t = threadIdx.x; t < m; t += PT)
+            lds[t] = ldp(&src[t], ntl);
+    }
+    __syncthreads();
+    T *dst = reinterpret_cast<T *>(U);
+    const uint16_t *up = upos + bstart[k];
+    const uint32_t sub = threadIdx.x / SEG, lane = threadIdx.x % SEG;
+    const uint32_t ncr = (pol & POL_SKIP_RUNS) ? 0u : nc;
+    for (uint32_t cb = sub; cb < ncr; cb += NSUB * B) {
+        uint16_t p[B];
+        uint32_t o[B], cn[B];
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+            const uint32_t c = cb + uint32_t(i) * NSUB;
+            cn[i] = 0;
+            if (c < nc) {
+                o[i] = tv[c];
+                cn[i] = tv[c + 1] - o[i];
+                if (lane < cn[i])
+                    p[i] = ldp(&up[o[i] + lane], ntl);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+            const uint32_t c = cb + uint32_t(i) * NSUB;
+            if (lane < cn[i])
+                stp(&dst[tph[c] + lane], lds[p[i]], nts);
+            for (uint32_t q = lane + SEG; q < cn[i]; q += SEG)
+                stp(&dst[tph[c] + q], lds[up[o[i] + q]], nts);
+        }
+    }
+}
+
 // pass 2 with 4 elements per thread in flight; pass 2' with k2 (4, 8 or 16; E * k2 <= 64
 // bytes).  cfg4 A/B (profiles/r2_ab_sorted_pass2_unroll.log): unpack 780 -> 751 us at 8 or 16,
 // pack 575 -> 587 us, so only the unpack side takes the knob.
@@ -698,7 +980,7 @@ T *dalloc(size_t n, uint64_t &bytes)
 void SortedList::take_blocks(std::vector<void *> &out)
 {
     for (void **p : {(void **) &A, (void **) &A16, (void **) &Abase, (void **) &SL, (void **) &off16,
-                     (void **) &ub, (void **) &bstart, (void **) &upos, &U})
+                     (void **) &ub, (void **) &bstart, (void **) &upos, (void **) &physT, (void **) &vrelT, &U})
         if (*p) {
             out.push_back(*p);
             *p = nullptr;
@@ -815,8 +1097,20 @@ bool SortedList::build(const int32_t *disp, uint32_t n_, uint32_t esz_, uint64_t
         slots = uint64_t(total) + uint64_t(nb) * skew;
         hipLaunchKernelGGL(k_run_bases, dim3(grid_for(runs, BT)), dim3(BT), 0, stream, ubT, nc, nb, total, skew, ub,
                            bstart);
+        uint64_t uslots = slots;
+        cst = ch;
+        if (unpadded && cdiv == 1 && nc <= MAXNC) {   // the chunk-major layout's run tables
+            // chunk images `skew` slots apart too (a bucket's runs sit one per image)
+            if (uint64_t(nc) * (ch + skew) < (1ull << 32))
+                cst = ch + skew;
+            uslots = std::max<uint64_t>(uslots, uint64_t(nc) * cst);
+            physT = dalloc<uint32_t>(runs, bytes);
+            vrelT = dalloc<uint16_t>(runs, bytes);
+            hipLaunchKernelGGL(k_cmaj_tables, dim3(grid_for(runs, BT)), dim3(BT), 0, stream, off16, ubT, nc, nb, cst,
+                               physT, vrelT);
+        }
         upos = dalloc<uint16_t>(slots, bytes);
-        U = dalloc<uint8_t>(size_t(slots) * esz, bytes);
+        U = dalloc<uint8_t>(size_t(uslots) * esz, bytes);
         HK(hipMemsetAsync(upos, 0xFF, size_t(slots) * 2, stream));
         hipLaunchKernelGGL(k_assign, dim3(grid_for(n, BT)), dim3(BT), 0, stream, disp, n, shift, bm, wpre, ch, rg,
                            nb, rr, off16, ub, SL, upos);
@@ -857,6 +1151,31 @@ hipError_t SortedList::run(uint8_t *user, uint8_t *packed, int dir, uint32_t pol
     uint8_t *u8 = static_cast<uint8_t *>(U);
     if (unpadded)   // r5 A/B (profiles/r5_ab_cfg4_unpadded.jsonl): the slabs pay only without padding
         pol |= POL_UNPADDED | POL_XCD_SLAB;
+    if (physT && (pol & (dir == 0 ? POL_CMAJ_PACK : POL_CMAJ_UNPACK))) {   // chunk-major U (r6)
+        pol |= POL_P2_SLAB;
+#define DDT_CMAJ(E, K)                                                                                          \
+    if (dir == 0) {                                                                                             \
+        hipLaunchKernelGGL((k_pack1c<E, K>), gc, blk, 0, stream, user, al, SL, u8, n, cst, pol);                      \
+        hipLaunchKernelGGL((k_pack2c<E, 8, 2>), gb, blk, 0, stream, u8, upos, bstart, physT, vrelT, packed, n, nc, pol); \
+    } else {                                                                                                    \
+        hipLaunchKernelGGL((k_unpack2c<E>), gb, blk, 0, stream, packed, upos, bstart, physT, vrelT, u8, n, nc, pol); \
+        hipLaunchKernelGGL((k_unpack1c<E, 4>), gc, blk, 0, stream, user, al, SL, u8, n, cst, pol);                    \
+    }
+        if (esz == 4) {
+            if (unroll >= 32) { DDT_CMAJ(4, 32) } else if (unroll >= 16) { DDT_CMAJ(4, 16) } else if (unroll >= 8) { DDT_CMAJ(4, 8) } else { DDT_CMAJ(4, 4) }
+        } else if (esz == 8) {
+            if (unroll >= 8) { DDT_CMAJ(8, 8) } else { DDT_CMAJ(8, 4) }
+        } else {
+            DDT_CMAJ(16, 4)
+        }
+#undef DDT_CMAJ
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess)
+            return e;
+        used = true;
+        last_stream = stream;
+        return hipEventRecord(done, stream);
+    }
 #define DDT_SORTED_PASS1(E, SB, K, CD)                                                                          \
     if (dir == 0)                                                                                               \
         hipLaunchKernelGGL((k_pack1<E, SB, K, CD>), gc, blk1, 0, stream, user, al, SL, off16, ub, u8, n, nb, pol); \

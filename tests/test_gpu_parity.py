@@ -1002,6 +1002,35 @@ def test_sorted_list_engine_quads(device, sorted_from, count, density, schunk, s
         L.ddt_tune(b"reset", 0)
 
 
+@pytest.mark.parametrize("vec", [1, 0])
+@pytest.mark.parametrize("skew", [0, 4160])
+@pytest.mark.parametrize("layout", [0, 1, 2, 3])
+@pytest.mark.parametrize("esz,count,density", [(4, 1, 4), (4, 2, 3), (8, 1, 5), (16, 2, 4), (4, 1, 64)])
+def test_sorted_list_engine_chunk_major(device, sorted_from, esz, count, density, layout, skew, vec):
+    """Chunk-major U (ddt_tune slayout, round 6): pass 1 / 1' stream the chunk images to / from U,
+    pass 2 / 2' read / write every bucket's runs in place inside them, for the pack (1), the
+    unpack (2), both (3) or neither (0), chunk images and buckets skewed apart or not, pass 2 / 2'
+    quads on or off (s2vec: the bucket-major direction's kernels); ragged last chunk and bucket,
+    bit-exact."""
+    import ompi_amd
+    L = ompi_amd.lib()
+    sorted_from(1)
+    for k, v in ((b"slayout", layout), (b"sskew", skew), (b"s2vec", vec)):
+        L.ddt_tune(k, v)
+    try:
+        rng = np.random.default_rng(esz * 31 + count * 7 + density + layout)
+        ch = (128 << 10) // esz
+        n = 3 * ch + 1237
+        unit = {4: ("basic", 15), 8: ("basic", 16), 16: ("basic", 16)}[esz]
+        per = esz // (8 if esz == 16 else esz)
+        disps = (rng.permutation(density * n)[:n] * per).astype(np.int64)
+        b = R.Built(("indexed_block", per, disps.tolist(), unit))
+        _roundtrip(b, count, device, 21 + esz)
+        assert b.engine().engine_info()["sorted"] == 1
+    finally:
+        L.ddt_tune(b"reset", 0)
+
+
 @pytest.mark.parametrize("name", ["contig16", "adv_mixed_promote", "one_contig_instance"])
 def test_no_op_types_fill_fragments_to_the_byte(device, name):
     """A convertor the reference marks NO_OP (OPAL_CONVERTOR_PREPARE, opal_convertor.c:
