@@ -706,7 +706,7 @@ __global__ __launch_bounds__(PT) void k_pack1c(const uint8_t *__restrict__ user,
 #pragma unroll
         for (int q = 0; q < K; ++q)
             if (t0 + q * PT < m)
-                lds[s[q]] = v[q];
+                lds[(pol & POL_NOCONF) ? t0 + q * PT : s[q]] = v[q];
     }
     __syncthreads();
     if (pol & POL_SKIP_RUNS)
@@ -944,6 +944,8 @@ void launch_pass2(dim3 gb, dim3 blk, hipStream_t stream, const uint8_t *src, con
     if (E == 4 && (pol & POL_VEC2)) {   // K quads (4 K slots) per lane in flight
         if (DIR == 0)
             hipLaunchKernelGGL((k_pack2v<2>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol, skew);
+        else if (k2 >= 16)
+            hipLaunchKernelGGL((k_unpack2v<4>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol, skew);
         else if (k2 >= 8)
             hipLaunchKernelGGL((k_unpack2v<2>), gb, blk, 0, stream, src, upos, bstart, dst, n, pol, skew);
         else
