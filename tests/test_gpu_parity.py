@@ -5,6 +5,7 @@ Bit-exact on every byte: packed streams, unpacked user buffers (gaps pre-filled 
 """
 from __future__ import annotations
 
+import os
 import random
 
 import numpy as np
@@ -1027,6 +1028,40 @@ def test_sorted_list_engine_chunk_major(device, sorted_from, esz, count, density
         b = R.Built(("indexed_block", per, disps.tolist(), unit))
         _roundtrip(b, count, device, 21 + esz)
         assert b.engine().engine_info()["sorted"] == 1
+    finally:
+        L.ddt_tune(b"reset", 0)
+
+
+def test_sorted_list_engine_fuzz(device, sorted_from):
+    """Random address-ordered plans (DDT_FUZZ_SORTED_SEEDS, default 6): element size 4 / 8 / 16,
+    1.2-5.5 chunks of elements (ragged last chunk, bucket and quad), density 1.1-40 slots per
+    element, 1-3 instances, every U layout (slayout 0-3), bucket / image skew on or off, pass 2
+    quads on or off; whole-message pack and unpack bit-exact against the oracle, and a fragment
+    trace through the convertor for one seed in four."""
+    import ompi_amd
+    L = ompi_amd.lib()
+    sorted_from(1)
+    seeds = int(os.environ.get("DDT_FUZZ_SORTED_SEEDS", "6"))
+    try:
+        for seed in range(seeds):
+            rng = np.random.default_rng(77000 + seed)
+            esz = int(rng.choice([4, 4, 8, 16]))
+            ch = (128 << 10) // esz
+            n = int(ch * rng.uniform(1.2, 5.5))
+            density = float(rng.uniform(1.1, 40.0))
+            count = int(rng.integers(1, 4))
+            L.ddt_tune(b"reset", 0)
+            sorted_from(1)   # reset restores the default threshold
+            for k, v in ((b"slayout", int(rng.integers(0, 4))), (b"sskew", int(rng.choice([0, 4160, 1088]))),
+                         (b"s2vec", int(rng.integers(0, 2)))):
+                L.ddt_tune(k, v)
+            unit = {4: ("basic", 15), 8: ("basic", 16), 16: ("basic", 16)}[esz]
+            per = esz // (8 if esz == 16 else esz)
+            disps = (rng.permutation(int(density * n))[:n] * per).astype(np.int64)
+            b = R.Built(("indexed_block", per, disps.tolist(), unit))
+            frags = [int(x) for x in rng.integers(1, 1 << 16, 3)] if seed % 4 == 3 else None
+            _roundtrip(b, count, device, 500 + seed, frags=frags)
+            assert b.engine().engine_info()["sorted"] == 1, seed
     finally:
         L.ddt_tune(b"reset", 0)
 
