@@ -16,7 +16,12 @@
 //            lds[upos[s]] = U[s];  packed[k*RG + t] = lds[t]
 //   unpack is the same two passes reversed.
 //
-// U is bucket-major, the (chunk, bucket) runs end to end (round 5; they were padded to whole
+// The pack keeps U chunk-major by default (round 6, ddt_tune slayout): pass 1 streams its whole
+// chunk image to U[c * (CH + skew)] and pass 2 reads the bucket's runs in place inside the images
+// (k_pack1c / k_pack2c), so the pack's scattered accesses are reads; the unpack keeps the
+// bucket-major U below (mirrored, its pass 2' would write the runs scattered).
+//
+// Bucket-major U: the (chunk, bucket) runs end to end (round 5; they were padded to whole
 // 64-byte segments before: 43 % of U was padding at cfg4).  Neighbouring chunks' runs share
 // segments, so pass 1 deals its chunks to the XCDs in contiguous slabs and both halves of a
 // shared segment meet in one L2.  CH = RG = 128 KiB / element size, so the LDS image of a
