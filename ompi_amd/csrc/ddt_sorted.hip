@@ -683,7 +683,7 @@ __global__ __launch_bounds__(PT / CDIV) void k_unpack1(uint8_t *__restrict__ use
 constexpr uint32_t MAXNC = 4096;
 
 // pass 1 of a chunk-major pack: the address-ordered gather into the LDS image, then the image
-// out to U[c * CH ..] as one stream
+// out to U[c * cst ..] as one stream (cst = CH + the skew, a whole number of 16-byte quads)
 template <int E, int K>
 __global__ __launch_bounds__(PT) void k_pack1c(const uint8_t *__restrict__ user, const AddrList al,
                                                const uint16_t *__restrict__ SL, uint8_t *__restrict__ U, uint32_t n,
@@ -716,7 +716,7 @@ __global__ __launch_bounds__(PT) void k_pack1c(const uint8_t *__restrict__ user,
     __syncthreads();
     if (pol & POL_SKIP_RUNS)
         return;
-    // the image is CH * E = 128 KiB at a 128 KiB-aligned offset of U: whole 16-byte words
+    // the image starts 16-byte aligned (c * cst * E): whole 16-byte words, then the tail
     const uint32_t mq = m * E / 16;
     u32x4 *dst = reinterpret_cast<u32x4 *>(U + size_t(c) * cst * E);
     const u32x4 *l4 = reinterpret_cast<const u32x4 *>(lds);
@@ -727,7 +727,7 @@ __global__ __launch_bounds__(PT) void k_pack1c(const uint8_t *__restrict__ user,
         dt[t] = lds[t];
 }
 
-// unpack pass 1' of the chunk-major layout: the image in from U[c * CH ..] as one stream, then
+// unpack pass 1' of the chunk-major layout: the image in from U[c * cst ..] as one stream, then
 // scattered to the user side in address order
 template <int E, int K>
 __global__ __launch_bounds__(PT) void k_unpack1c(uint8_t *__restrict__ user, const AddrList al,
