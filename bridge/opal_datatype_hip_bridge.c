@@ -418,7 +418,12 @@ static thread_state *thread_state_get(void)
     (void) pthread_once(&g_once, key_init);
     thread_state *ts = (thread_state *) pthread_getspecific(g_key);
     if (!ts) {
-        ts = (thread_state *) calloc(1, sizeof(*ts));
+        /* a line-aligned state of its own: the tick and pin counters written on every call must
+         * not share a cache line with another thread's (r6 thread A/B) */
+        const size_t tsz = (sizeof(*ts) + 127) & ~(size_t) 127;
+        ts = (thread_state *) aligned_alloc(128, tsz);
+        if (ts)
+            memset(ts, 0, tsz);
         if (ts && pthread_setspecific(g_key, ts) != 0) {
             free(ts);
             ts = NULL;

@@ -717,7 +717,7 @@ int run_windows(ddt_datatype *t, Plan &P, uint64_t count, uint64_t user,
 
 }  // namespace
 
-struct ddt_convertor {
+struct alignas(128) ddt_convertor {   // per-thread objects on lines of their own (r6)
     ddt_datatype *dt = nullptr;
     uint64_t dt_serial = 0;   // dt->serial when prepared (a recycled address is another type)
     std::shared_ptr<Plan> plan;

@@ -142,7 +142,7 @@ struct DevList {                  // device copy of an IndexList
 // Items hold addresses relative to the launch's two bases (16-byte aligned), so the key is
 // the request's shape and alignment only: a double-buffered halo, a staged pipeline's HBM
 // slots or a PML fragment stream reuse one set across buffers.
-struct ItemSet {
+struct alignas(128) ItemSet {   // written on every call: a line of its own (r6)
     std::vector<uint64_t> key;
     std::vector<Item> items;
     Item *d_items = nullptr;
@@ -205,7 +205,7 @@ struct Retired {
 struct ExtPlan;
 struct DescForm;
 
-struct Plan {
+struct alignas(128) Plan {
     std::vector<Leaf> leaves;
     std::vector<DevList> dev;     // one per LIST leaf (index in Leaf order, others empty)
     uint64_t dev_bytes = 0;       // device metadata bytes

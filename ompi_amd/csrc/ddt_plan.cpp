@@ -212,7 +212,9 @@ namespace {
 // attempts may be evicted
 constexpr uint64_t kEvictIdle = 256;
 constexpr int kMaxDev = 64;
-struct SlotEntry {
+// one record per 128 bytes: the records of threads launching at once must not share a cache
+// line (lock, launch count and tick are written on every launch; r6 thread A/B)
+struct alignas(128) SlotEntry {
     SpinMutex mu;                       // launches of this record; changes of its binding
     bool used = false;
     bool ending = false;                // binding ended, fences not recorded yet: retry
